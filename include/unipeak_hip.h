@@ -1,0 +1,149 @@
+/*
+ * include/unipeak_hip.h -- the drop-in C-ABI boundary of unipeak-mi355x.
+ *
+ * The reference's hot path is an in-process C++ class driven position by
+ * position (misc/peakcall.hpp:57-77):
+ *
+ *   Kernel(bw, 1/background)                         misc/kernel.hpp:16
+ *   ProfileBuffer(kernel, r, k, u, t, fwd, control,
+ *                 coeffs, contigs, regionsOut, prof) misc/peakcall.hpp:57-69
+ *   ProfileBuffer::add(counts, contig, pos, fwd)     misc/peakcall.hpp:76
+ *   ProfileBuffer::flushContig()                     misc/peakcall.hpp:75
+ *   nRegions()/nRegionRejects()/nTagsInRegions()     misc/peakcall.hpp:71-74
+ *   Region::exptSums/posKurtosis/strandCorr          misc/data.hpp:66-72
+ *
+ * On MI355X the same work is done in batches: every add() that one buffer
+ * receives between two flushes (one "unit" = one buffer x one contig pass)
+ * is a dense per-position count track resident in HBM, and up_run()
+ * performs, for all units at once, what the sequence of add()/flushContig()
+ * calls computes: pooled counts, the Epanechnikov KDE, the threshold scan,
+ * region segmentation and processRegion()'s statistics and filters.
+ * Mapping of entry points to the reference interface:
+ *
+ *   up_kernel_weights   <- Kernel::Kernel            misc/kernel.cpp:16-35
+ *   up_open/up_set_params <- ProfileBuffer ctor      misc/peakcall.cpp:88-135
+ *   up_add_unit + up_unit_scatter (or up_unit_ptr)
+ *                        <- the add() calls of one unit misc/peakcall.cpp:161-222
+ *   up_run              <- add()'s window scatter + processPosition +
+ *                          processRegion + flushContig  misc/peakcall.cpp:33-86,224-231
+ *   up_get_regions      <- regionsOut vector + Region statistics
+ *                          misc/peakcall.cpp:45, misc/data.cpp:104-193
+ *   up_shift_scan       <- Region::strandCorr(shift) loop src/strand_shift.cpp:205-228
+ *
+ * Conventions: plain C types only; the caller owns host buffers, the library
+ * owns device memory; one context per GPU, driven by one host thread (not
+ * re-entrant, like ProfileBuffer).  Every entry point returns UP_OK (0) or a
+ * negative UP_E_* code (up_strerror); nothing exits the process.
+ */
+#ifndef UNIPEAK_HIP_H
+#define UNIPEAK_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UP_OK 0
+#define UP_E_ARG (-1)         /* bad argument */
+#define UP_E_HIP (-2)         /* HIP runtime error */
+#define UP_E_NOMEM (-3)       /* device allocation failed */
+#define UP_E_STATE (-4)       /* call out of order (e.g. no params) */
+#define UP_E_UNSUPPORTED (-5) /* configuration outside the GPU path */
+#define UP_E_NODEV (-6)       /* no HIP device */
+#define UP_E_INTERNAL (-7)    /* internal consistency check failed */
+
+typedef struct up_ctx up_ctx;
+
+/* Parameters of one ProfileBuffer pair (misc/peakcall.hpp:57-69) as the
+ * CLI computes them (src/regions.cpp:152-232, src/strand_shift.cpp:131-142). */
+typedef struct {
+    uint16_t bw;              /* kernel bandwidth (-b) */
+    uint16_t n_samples;       /* S = all samples, controls included */
+    int32_t nondir;           /* 0: one strand per unit; 1: both strands in one unit */
+    double background;        /* kernel sums to 1/background */
+    double region_thr;        /* -r */
+    double kurt_thr;          /* -k (0 disables) */
+    double corr_thr;          /* -u (<= -1 disables) */
+    double hit_thr;           /* already multiplied by S_nc where the CLI does */
+    const uint8_t *is_control;/* [S] or NULL */
+    const double *coeffs;     /* NULL or [n_coeffs] = normalised -z coefficients */
+    uint32_t n_coeffs;
+    int32_t want_corr;        /* evaluate strandCorr(0) for every region */
+} up_params;
+
+/* One candidate region (accepted or rejected by processRegion). */
+typedef struct {
+    uint32_t unit;            /* unit the region was closed in */
+    uint32_t left, right;     /* inclusive positions (right may exceed the contig, Q16) */
+    uint32_t peak;            /* first position of the maximal f+r */
+    uint32_t sum;             /* Region::sum() (uint32, wraps) */
+    uint32_t nonctl_sum;      /* sum over non-control samples of exptSums */
+    int32_t accepted;         /* passed the hit/kurtosis/correlation filters */
+    int32_t reserved;
+    double peak_score;        /* f+r at peak */
+    double kurtosis;          /* Region::posKurtosis() */
+    double corr;              /* Region::strandCorr(0) or NaN when not evaluated */
+} up_region;
+
+/* library / device */
+int up_version(void);
+const char *up_strerror(int code);
+int up_device_count(int *n);
+
+/* Kernel::Kernel(bw, sum) -- 2*bw+1 weights into w (host computation). */
+int up_kernel_weights(uint16_t bw, double sum, double *w);
+
+int up_open(int hip_device, up_ctx **out);
+void up_close(up_ctx *ctx);
+int up_set_params(up_ctx *ctx, const up_params *p);
+
+/* Units.  A unit is one ProfileBuffer (buffer_id 0 = forward buffer, 1 =
+ * reverse buffer) over one contig pass; units of one buffer must be added in
+ * the order the buffer sees them.  nstrands is 1 (directional) or 2
+ * (nondirectional: strand 0 forward, 1 reverse).  Count tracks are zeroed
+ * uint32 arrays covering positions 1..contig_len. */
+int up_add_unit(up_ctx *ctx, uint32_t contig_len, int32_t nstrands,
+                int32_t buffer_id, uint32_t *unit_id);
+int up_unit_count(up_ctx *ctx, uint32_t *n);
+/* device pointer to the track: position p (1-based) lives at ptr[p-1] */
+int up_unit_ptr(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
+                uint32_t **dev_ptr);
+/* write n (pos, count) host pairs (positions 1..len, unique) into a track */
+int up_unit_scatter(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
+                    size_t n, const uint32_t *pos, const uint32_t *counts);
+/* fill a track with the synthetic hg19-shaped spec */
+int up_unit_synth(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
+                  uint64_t seed, uint32_t contig_index, int32_t synth_strand,
+                  int32_t nondir, int32_t with_peaks);
+/* total tags of one track (sum of its counts, uint64) */
+int up_unit_tag_total(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
+                      uint64_t *total);
+/* override the last add position of a unit (host knows control-only adds) */
+int up_unit_set_last_add(up_ctx *ctx, uint32_t unit, uint32_t last_add);
+int up_unit_last_add(up_ctx *ctx, uint32_t unit, uint32_t *last_add);
+int up_reset_units(up_ctx *ctx);
+
+/* Run K1..K3 over every unit (stream-ordered, blocking). */
+int up_run(up_ctx *ctx, uint64_t *n_regions);
+/* Copy region records (unit-major, left-ascending) and optionally the
+ * per-sample exptSums [n][S]. */
+int up_get_regions(up_ctx *ctx, up_region *out, uint32_t *counts, size_t cap);
+
+/* strandCorr(shift) for shift = 0..max_shift of the given regions
+ * (indices into up_get_regions order); out is [n][max_shift+1]. */
+int up_shift_scan(up_ctx *ctx, const uint64_t *region_idx, size_t n,
+                  uint16_t max_shift, double *out);
+
+/* device-side timings of the last up_run in ms: [0]=K1 scan, [1]=K2
+ * segment, [2]=K3 stats, [3]=whole up_run wall, [4]=K1 launches */
+int up_timings(up_ctx *ctx, double *ms, int n);
+/* dense per-position score f+r of one unit (testing/-w): out[len] */
+int up_unit_profile(up_ctx *ctx, uint32_t unit, double *out_f, double *out_r,
+                    uint32_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,151 @@
+"""Parity of the HIP path (through the C-ABI) with the oracle, one unit at a
+time: every candidate region (accepted and rejected), its peak, per-sample
+counts and filters bit-exact; FP64 peak score and KDE profile bit-exact;
+kurtosis and strand correlation within 1e-12 relative (north star allows
+1e-6)."""
+import numpy as np
+import pytest
+
+from tests.gen import random_unit
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-12
+
+
+def close(a, b, rel=REL):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    both_nan = np.isnan(a) & np.isnan(b)
+    ok = both_nan | (a == b) | (np.abs(a - b) <= rel * np.maximum(np.abs(a), np.abs(b)))
+    return bool(np.all(ok))
+
+
+def run_gpu(capi, bw, bg, length, pos, cf, cr=None, *, nondir=False, control=None,
+            coeffs=None, region_thr=25.0, kurt_thr=50.0, corr_thr=-1.0, hit_thr=10.0,
+            want_corr=False, strand_label=0):
+    S = (cf if cf is not None else cr).shape[1]
+    with capi.Lib(0) as g:
+        g.set_params(bw, S, bg, region_thr=region_thr, kurt_thr=kurt_thr, corr_thr=corr_thr,
+                     hit_thr=hit_thr, nondir=nondir, control=control, coeffs=coeffs,
+                     want_corr=want_corr)
+        u = g.add_unit(length)
+        tracks = [cf] if not nondir else [cf, cr]
+        for st, c in enumerate(tracks):
+            for s in range(S):
+                m = c[:, s] != 0
+                g.scatter(u, st, s, pos[m], c[m, s])
+        n = g.run()
+        regs, cnt = g.regions(n)
+        f, r = g.profile(u, length)
+        last = g.last_add(u)
+    return regs, cnt, f, r, last
+
+
+def compare(ref, ref_sums, regs, cnt):
+    assert len(ref) == len(regs), (len(ref), len(regs))
+    for k in ("left", "right", "peak", "sum", "accepted"):
+        assert np.array_equal(ref[k], regs[k]), k
+    assert np.array_equal(ref_sums, cnt)
+    assert ref["peak_score"].tobytes() == regs["peak_score"].tobytes()
+    assert close(ref["kurtosis"], regs["kurtosis"])
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("bw", [50, 20, 90])
+def test_directional_single_sample(gpu_lib, oracle, seed, bw):
+    rng = np.random.default_rng(seed)
+    length = int(rng.integers(20_000, 300_000))
+    pos, cnt = random_unit(rng, length, bw)
+    bg = 0.003
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt)
+    regs, gcnt, f, r, last = run_gpu(gpu_lib, bw, bg, length, pos, cnt)
+    compare(ref, ref_sums, regs, gcnt)
+    prof = oracle.profile(bw, bg, length, pos, cnt)
+    assert prof.tobytes() == f.tobytes()
+    assert last == pos[-1]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_reverse_buffer_unit(gpu_lib, oracle, seed):
+    rng = np.random.default_rng(100 + seed)
+    length, bw, bg = 120_000, 50, 0.002
+    pos, cnt = random_unit(rng, length, bw)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, None, cnt, buffer_forward=False)
+    regs, gcnt, f, r, _ = run_gpu(gpu_lib, bw, bg, length, pos, cnt)
+    compare(ref, ref_sums, regs, gcnt)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_multi_sample_with_control(gpu_lib, oracle, seed):
+    rng = np.random.default_rng(200 + seed)
+    length, bw, bg, S = 150_000, 50, 0.004, 4
+    pos, cnt = random_unit(rng, length, bw, S=S)
+    control = [0, 0, 1, 0]
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, control=control, hit_thr=30.0)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, control=control, hit_thr=30.0)
+    compare(ref, ref_sums, regs, gcnt)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_coefficients_q5(gpu_lib, oracle, seed):
+    rng = np.random.default_rng(300 + seed)
+    length, bw, bg, S = 100_000, 50, 0.004, 3
+    pos, cnt = random_unit(rng, length, bw, S=S)
+    coeffs = [0.37, 1.91, 0.7]
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, coeffs=coeffs)
+    regs, gcnt, f, _, _ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, coeffs=coeffs)
+    compare(ref, ref_sums, regs, gcnt)
+    prof = oracle.profile(bw, bg, length, pos, cnt, coeffs=coeffs)
+    assert prof.tobytes() == f.tobytes()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_nondirectional_with_corr(gpu_lib, oracle, seed):
+    rng = np.random.default_rng(400 + seed)
+    length, bw, bg = 200_000, 50, 0.005
+    pos_f, cnt_f = random_unit(rng, length, bw)
+    pos_r, cnt_r = random_unit(rng, length, bw)
+    allp = np.union1d(pos_f, pos_r).astype(np.uint32)
+    cf = np.zeros((allp.size, 1), np.uint32)
+    cr = np.zeros((allp.size, 1), np.uint32)
+    cf[np.searchsorted(allp, pos_f)] = cnt_f
+    cr[np.searchsorted(allp, pos_r)] = cnt_r
+    ref, ref_sums = oracle.run_unit(bw, bg, allp, cf, cr, nondir=True, corr_thr=0.3)
+    regs, gcnt, f, r, _ = run_gpu(gpu_lib, bw, bg, length, allp, cf, cr, nondir=True,
+                                  corr_thr=0.3, want_corr=True)
+    compare(ref, ref_sums, regs, gcnt)
+    assert close(ref["corr"], regs["corr"])
+    prof = oracle.profile(bw, bg, length, allp, cf, cr, nondir=True)
+    assert prof.tobytes() == (f + r).tobytes()
+
+
+def test_empty_unit(gpu_lib, oracle):
+    regs, gcnt, f, r, last = run_gpu(gpu_lib, 50, 0.003, 5000, np.zeros(0, np.uint32),
+                                     np.zeros((0, 1), np.uint32))
+    assert len(regs) == 0 and last == 0 and not f.any()
+
+
+def test_dense_unit_overflows_inline_records(gpu_lib, oracle):
+    """Alternating narrow regions: many runs per 1024-position strip."""
+    length, bw, bg = 40_000, 5, 0.01
+    pos = np.arange(200, 30_000, 13, dtype=np.uint32)
+    cnt = np.full((pos.size, 1), 50, np.uint32)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, kurt_thr=0.0, hit_thr=1.0)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, kurt_thr=0.0, hit_thr=1.0)
+    compare(ref, ref_sums, regs, gcnt)
+    assert len(regs) > 1000
+
+
+def test_synthetic_track_matches_oracle_spec(gpu_lib, oracle):
+    """Device synthetic generator == oracle's host generator (same spec)."""
+    import ctypes
+    length, bw = 400_000, 50
+    pos, cnt = oracle.synth_track(1000, 3, 1, False, length, bw)
+    with gpu_lib.Lib(0) as g:
+        g.set_params(bw, 1, 0.003)
+        u = g.add_unit(length)
+        g.synth(u, 0, 0, 1000, 3, 1, nondir=False, peaks=True)
+        n = g.run()
+        f, _ = g.profile(u, length)
+    ref = oracle.profile(bw, 0.003, length, pos, cnt.reshape(-1, 1))
+    assert ref.tobytes() == f.tobytes()

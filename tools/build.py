@@ -1,0 +1,79 @@
+"""Build every native artefact in-tree (used by __graft_entry__.build()).
+
+  unipeak_amd/lib/libunipeak_hip.so   HIP kernels + C-ABI (gfx950)
+  bin/regions, bin/strand_shift, bin/tags_in_regions   C++ host CLIs
+  oracle/_build/liboracle.so, oracle/_build/orc        CPU restatement
+                                                       (test infrastructure)
+Rebuilds only what is older than its sources.
+"""
+import glob
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("UNIPEAK_ARCH", "gfx950")
+
+
+def _stale(target, sources):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def _run(cmd, cwd=ROOT):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, cwd=cwd, check=True)
+
+
+def build_lib(force=False):
+    out = os.path.join(ROOT, "unipeak_amd", "lib", "libunipeak_hip.so")
+    srcs = glob.glob(os.path.join(ROOT, "unipeak_amd", "csrc", "*")) + [
+        os.path.join(ROOT, "include", "unipeak_hip.h")]
+    if force or _stale(out, srcs):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-ffp-contract=off", "-fno-fast-math", "-I", os.path.join(ROOT, "include"),
+              "-o", out, os.path.join(ROOT, "unipeak_amd", "csrc", "api.hip")])
+    return out
+
+
+def build_cli(force=False):
+    lib = os.path.join(ROOT, "unipeak_amd", "lib")
+    hsrc = sorted(glob.glob(os.path.join(ROOT, "unipeak_amd", "host", "*.cpp")))
+    hdrs = glob.glob(os.path.join(ROOT, "unipeak_amd", "host", "*.hpp"))
+    if not hsrc:
+        return []
+    common = [s for s in hsrc if not os.path.basename(s).startswith("main_")]
+    outs = []
+    os.makedirs(os.path.join(ROOT, "bin"), exist_ok=True)
+    for m in [s for s in hsrc if os.path.basename(s).startswith("main_")]:
+        name = os.path.basename(m)[len("main_"):-len(".cpp")]
+        out = os.path.join(ROOT, "bin", name)
+        deps = common + hdrs + [m, os.path.join(lib, "libunipeak_hip.so"),
+                                os.path.join(ROOT, "include", "unipeak_hip.h")]
+        if force or _stale(out, deps):
+            _run(["g++", "-O2", "-std=c++17", "-Wall", "-ffp-contract=off", "-fno-fast-math",
+                  "-I", os.path.join(ROOT, "include"), "-o", out, m] + common +
+                 ["-L", lib, "-lunipeak_hip", "-Wl,-rpath,$ORIGIN/../unipeak_amd/lib",
+                  "-lpthread"])
+        outs.append(out)
+    return outs
+
+
+def build_oracle(force=False):
+    if force:
+        _run(["make", "-C", os.path.join(ROOT, "oracle"), "clean"])
+    _run(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+def build_all(force=False):
+    build_oracle(force)
+    build_lib(force)
+    build_cli(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

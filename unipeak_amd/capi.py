@@ -1,0 +1,243 @@
+"""ctypes binding of include/unipeak_hip.h (libunipeak_hip.so).
+
+Mirrors the C-ABI one-to-one; every failing call raises UpError carrying
+the library's error text (up_strerror), the analogue of the reference's
+`error: ...` exits.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libunipeak_hip.so")
+
+UP_OK = 0
+
+
+class UpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (code {code})")
+        self.code = code
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("bw", ctypes.c_uint16),
+        ("n_samples", ctypes.c_uint16),
+        ("nondir", ctypes.c_int32),
+        ("background", ctypes.c_double),
+        ("region_thr", ctypes.c_double),
+        ("kurt_thr", ctypes.c_double),
+        ("corr_thr", ctypes.c_double),
+        ("hit_thr", ctypes.c_double),
+        ("is_control", ctypes.POINTER(ctypes.c_uint8)),
+        ("coeffs", ctypes.POINTER(ctypes.c_double)),
+        ("n_coeffs", ctypes.c_uint32),
+        ("want_corr", ctypes.c_int32),
+    ]
+
+
+class Region(ctypes.Structure):
+    _fields_ = [
+        ("unit", ctypes.c_uint32),
+        ("left", ctypes.c_uint32),
+        ("right", ctypes.c_uint32),
+        ("peak", ctypes.c_uint32),
+        ("sum", ctypes.c_uint32),
+        ("nonctl_sum", ctypes.c_uint32),
+        ("accepted", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("peak_score", ctypes.c_double),
+        ("kurtosis", ctypes.c_double),
+        ("corr", ctypes.c_double),
+    ]
+
+
+REGION_DTYPE = np.dtype([
+    ("unit", "<u4"), ("left", "<u4"), ("right", "<u4"), ("peak", "<u4"),
+    ("sum", "<u4"), ("nonctl_sum", "<u4"), ("accepted", "<i4"), ("reserved", "<i4"),
+    ("peak_score", "<f8"), ("kurtosis", "<f8"), ("corr", "<f8")])
+assert REGION_DTYPE.itemsize == ctypes.sizeof(Region)
+
+_lib = None
+
+EXPORTS = [
+    "up_version", "up_strerror", "up_device_count", "up_kernel_weights", "up_open",
+    "up_close", "up_set_params", "up_add_unit", "up_unit_count", "up_unit_ptr",
+    "up_unit_scatter", "up_unit_synth", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
+    "up_reset_units", "up_run", "up_get_regions", "up_shift_scan", "up_timings",
+    "up_unit_profile",
+]
+
+
+def load_library(path=LIB_PATH):
+    """Load libunipeak_hip.so (raises OSError when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"{path} not built: run `python __graft_entry__.py` / tools/build.py")
+    L = ctypes.CDLL(path)
+    c = ctypes
+    vp, u32p = c.c_void_p, c.POINTER(c.c_uint32)
+    sig = {
+        "up_version": (c.c_int, []),
+        "up_strerror": (c.c_char_p, [c.c_int]),
+        "up_device_count": (c.c_int, [c.POINTER(c.c_int)]),
+        "up_kernel_weights": (c.c_int, [c.c_uint16, c.c_double, vp]),
+        "up_open": (c.c_int, [c.c_int, c.POINTER(vp)]),
+        "up_close": (None, [vp]),
+        "up_set_params": (c.c_int, [vp, c.POINTER(Params)]),
+        "up_add_unit": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_int32, u32p]),
+        "up_unit_count": (c.c_int, [vp, u32p]),
+        "up_unit_ptr": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.POINTER(vp)]),
+        "up_unit_scatter": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.c_size_t, vp, vp]),
+        "up_unit_synth": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.c_uint64,
+                                    c.c_uint32, c.c_int32, c.c_int32, c.c_int32]),
+        "up_unit_tag_total": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16,
+                                        c.POINTER(c.c_uint64)]),
+        "up_unit_set_last_add": (c.c_int, [vp, c.c_uint32, c.c_uint32]),
+        "up_unit_last_add": (c.c_int, [vp, c.c_uint32, u32p]),
+        "up_reset_units": (c.c_int, [vp]),
+        "up_run": (c.c_int, [vp, c.POINTER(c.c_uint64)]),
+        "up_get_regions": (c.c_int, [vp, vp, vp, c.c_size_t]),
+        "up_shift_scan": (c.c_int, [vp, vp, c.c_size_t, c.c_uint16, vp]),
+        "up_timings": (c.c_int, [vp, vp, c.c_int]),
+        "up_unit_profile": (c.c_int, [vp, c.c_uint32, vp, vp, c.c_uint32]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _ck(code):
+    if code != UP_OK:
+        raise UpError(code, _lib.up_strerror(code).decode())
+
+
+def kernel_weights(bw, total=1.0):
+    L = load_library()
+    w = np.zeros(2 * bw + 1, np.float64)
+    _ck(L.up_kernel_weights(bw, total, w.ctypes.data))
+    return w
+
+
+def device_count():
+    L = load_library()
+    n = ctypes.c_int(0)
+    _ck(L.up_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Lib:
+    """One up_ctx (one GPU)."""
+
+    def __init__(self, device=0):
+        self.L = load_library()
+        self.ctx = ctypes.c_void_p()
+        _ck(self.L.up_open(device, ctypes.byref(self.ctx)))
+        self.S = None
+
+    def close(self):
+        if self.ctx:
+            self.L.up_close(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_params(self, bw, n_samples, background, region_thr=25.0, kurt_thr=50.0,
+                   corr_thr=-1.0, hit_thr=10.0, nondir=False, control=None, coeffs=None,
+                   want_corr=False):
+        p = Params()
+        p.bw, p.n_samples, p.nondir = bw, n_samples, int(bool(nondir))
+        p.background, p.region_thr, p.kurt_thr = background, region_thr, kurt_thr
+        p.corr_thr, p.hit_thr, p.want_corr = corr_thr, hit_thr, int(bool(want_corr))
+        self._ctl = None
+        if control is not None:
+            self._ctl = (ctypes.c_uint8 * n_samples)(*[1 if x else 0 for x in control])
+            p.is_control = self._ctl
+        self._coef = None
+        if coeffs is not None and len(coeffs):
+            self._coef = (ctypes.c_double * len(coeffs))(*coeffs)
+            p.coeffs = self._coef
+            p.n_coeffs = len(coeffs)
+        _ck(self.L.up_set_params(self.ctx, ctypes.byref(p)))
+        self.S = n_samples
+        self.nondir = bool(nondir)
+
+    def add_unit(self, length, buffer_id=0):
+        u = ctypes.c_uint32()
+        _ck(self.L.up_add_unit(self.ctx, length, 2 if self.nondir else 1, buffer_id,
+                               ctypes.byref(u)))
+        return u.value
+
+    def scatter(self, unit, strand, sample, pos, counts):
+        pos = np.ascontiguousarray(pos, np.uint32)
+        counts = np.ascontiguousarray(counts, np.uint32)
+        assert pos.shape == counts.shape
+        _ck(self.L.up_unit_scatter(self.ctx, unit, strand, sample, pos.size,
+                                   pos.ctypes.data, counts.ctypes.data))
+
+    def synth(self, unit, strand, sample, seed, contig_index, synth_strand, nondir=False,
+              peaks=True):
+        _ck(self.L.up_unit_synth(self.ctx, unit, strand, sample, seed, contig_index,
+                                 synth_strand, int(nondir), int(peaks)))
+
+    def tag_total(self, unit, strand, sample):
+        v = ctypes.c_uint64()
+        _ck(self.L.up_unit_tag_total(self.ctx, unit, strand, sample, ctypes.byref(v)))
+        return v.value
+
+    def unit_ptr(self, unit, strand, sample):
+        p = ctypes.c_void_p()
+        _ck(self.L.up_unit_ptr(self.ctx, unit, strand, sample, ctypes.byref(p)))
+        return p.value
+
+    def set_last_add(self, unit, pos):
+        _ck(self.L.up_unit_set_last_add(self.ctx, unit, pos))
+
+    def last_add(self, unit):
+        v = ctypes.c_uint32()
+        _ck(self.L.up_unit_last_add(self.ctx, unit, ctypes.byref(v)))
+        return v.value
+
+    def reset_units(self):
+        _ck(self.L.up_reset_units(self.ctx))
+
+    def run(self):
+        n = ctypes.c_uint64()
+        _ck(self.L.up_run(self.ctx, ctypes.byref(n)))
+        return n.value
+
+    def regions(self, n, with_counts=True):
+        out = np.zeros(n, REGION_DTYPE)
+        cnt = np.zeros((n, self.S), np.uint32) if with_counts else None
+        _ck(self.L.up_get_regions(self.ctx, out.ctypes.data,
+                                  cnt.ctypes.data if cnt is not None else None, n))
+        return out, cnt
+
+    def shift_scan(self, idx, max_shift):
+        idx = np.ascontiguousarray(idx, np.uint64)
+        out = np.zeros((idx.size, max_shift + 1), np.float64)
+        _ck(self.L.up_shift_scan(self.ctx, idx.ctypes.data, idx.size, max_shift,
+                                 out.ctypes.data))
+        return out
+
+    def timings(self):
+        t = np.zeros(5, np.float64)
+        _ck(self.L.up_timings(self.ctx, t.ctypes.data, 5))
+        return t
+
+    def profile(self, unit, length):
+        f = np.zeros(length, np.float64)
+        r = np.zeros(length, np.float64)
+        _ck(self.L.up_unit_profile(self.ctx, unit, f.ctypes.data, r.ctypes.data, length))
+        return f, r

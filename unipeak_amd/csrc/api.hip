@@ -1,0 +1,711 @@
+// unipeak_amd/csrc/api.hip -- C-ABI implementation (include/unipeak_hip.h):
+// device memory for the unit tracks, kernel launches and the glue between
+// them.  Host-side only; kernels live in kernels.hip.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/unipeak_hip.h"
+#include "kernels.h"
+
+#include "kernels.hip"  // single translation unit: kernels + C-ABI
+
+using namespace upk;
+
+namespace {
+
+struct Unit {
+    uint32_t len = 0;
+    int32_t nstrands = 1;
+    int32_t buffer = 0;
+    uint32_t *dptr = nullptr;
+    uint64_t stride = 0;
+    uint32_t nstrips = 0;
+    uint32_t strip0 = 0;
+    uint32_t last_override = 0;
+    bool has_override = false;
+};
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        size_t cap = want < 16 ? 16 : want + want / 4;
+        hipError_t e = hipMalloc(&p, cap * sizeof(T));
+        if (e == hipSuccess) n = cap;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+
+struct up_ctx {
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    bool have_params = false;
+    up_params p{};
+    std::vector<uint8_t> ctl;
+    std::vector<double> coef, kern;
+    std::vector<int32_t> nc;
+    DevBuf<double> d_kern, d_coef;
+    DevBuf<int32_t> d_nc;
+    DevBuf<uint8_t> d_ctl;
+    std::vector<Unit> units;
+    bool units_dirty = true;
+    DevBuf<UnitDesc> d_units;
+    uint32_t nstrips = 0;
+    int bw_layout = -1;  // bw the strip layout was computed for
+    DevBuf<uint32_t> d_info, d_rec, d_lastnz, d_ovf_count, d_ovf_rec, d_unit_last;
+    DevBuf<uint64_t> d_cnt, d_off, d_nreg;
+    DevBuf<unsigned char> d_tmp;
+    DevBuf<uint32_t> d_starts, d_ends, d_runit, d_counts;
+    DevBuf<up_region> d_regions;
+    uint32_t ovf_cap = 4096;
+    uint64_t nreg = 0;
+    bool ran = false;
+    std::vector<uint32_t> unit_last;
+    hipEvent_t ev[8] = {};
+    double times[5] = {0, 0, 0, 0, 0};
+};
+
+#define HIPCHK(x)                                                                   \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            fprintf(stderr, "unipeak_hip: %s failed: %s (%s:%d)\n", #x,             \
+                    hipGetErrorString(e_), __FILE__, __LINE__);                     \
+            return e_ == hipErrorOutOfMemory ? UP_E_NOMEM : UP_E_HIP;               \
+        }                                                                           \
+    } while (0)
+
+// public entry points: C linkage comes from the declarations in
+// include/unipeak_hip.h
+
+int up_version(void) { return 10000; }
+
+const char *up_strerror(int code) {
+    switch (code) {
+    case UP_OK: return "ok";
+    case UP_E_ARG: return "bad argument";
+    case UP_E_HIP: return "HIP runtime error";
+    case UP_E_NOMEM: return "device memory exhausted";
+    case UP_E_STATE: return "call out of order";
+    case UP_E_UNSUPPORTED: return "configuration outside the GPU path";
+    case UP_E_NODEV: return "no HIP device";
+    case UP_E_INTERNAL: return "internal consistency check failed";
+    default: return "unknown error";
+    }
+}
+
+int up_device_count(int *n) {
+    if (!n) return UP_E_ARG;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return UP_OK;
+}
+
+// Kernel::Kernel (misc/kernel.cpp:16-35): f(i/bw) = 3(1 - (i/bw)^2)/4 for
+// i = -bw..bw, summed left to right, then every weight scaled by sum/total.
+int up_kernel_weights(uint16_t bw, double sum, double *w) {
+    if (!w) return UP_E_ARG;
+    double acc = 0;
+    for (int i = -(int)bw, j = 0; i <= (int)bw; ++i, ++j) {
+        const double x = (double)i / (double)bw;
+        const double x2 = x * x;
+        w[j] = 3 * (1 - x2) / 4;
+        acc += w[j];
+    }
+    const double scale = sum / acc;
+    for (int j = 0; j < 2 * (int)bw + 1; ++j) w[j] *= scale;
+    return UP_OK;
+}
+
+int up_open(int hip_device, up_ctx **out) {
+    if (!out) return UP_E_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return UP_E_NODEV;
+    if (hip_device < 0 || hip_device >= n) return UP_E_ARG;
+    up_ctx *c = new up_ctx();
+    c->dev = hip_device;
+    HIPCHK(hipSetDevice(hip_device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
+    *out = c;
+    return UP_OK;
+}
+
+static void free_units(up_ctx *c) {
+    for (auto &u : c->units)
+        if (u.dptr) (void)hipFree(u.dptr);
+    c->units.clear();
+    c->units_dirty = true;
+    c->ran = false;
+}
+
+void up_close(up_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->dev);
+    (void)hipStreamSynchronize(c->stream);
+    free_units(c);
+    c->d_kern.release(); c->d_coef.release(); c->d_nc.release(); c->d_ctl.release();
+    c->d_units.release(); c->d_info.release(); c->d_rec.release(); c->d_lastnz.release();
+    c->d_ovf_count.release(); c->d_ovf_rec.release(); c->d_unit_last.release();
+    c->d_cnt.release(); c->d_off.release(); c->d_nreg.release(); c->d_tmp.release();
+    c->d_starts.release(); c->d_ends.release(); c->d_runit.release(); c->d_counts.release();
+    c->d_regions.release();
+    for (auto &e : c->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int up_set_params(up_ctx *c, const up_params *p) {
+    if (!c || !p) return UP_E_ARG;
+    if (p->n_samples == 0 || p->bw == 0) return UP_E_ARG;
+    HIPCHK(hipSetDevice(c->dev));
+    c->p = *p;
+    const int S = p->n_samples;
+    c->ctl.assign(S, 0);
+    if (p->is_control)
+        for (int s = 0; s < S; ++s) c->ctl[s] = p->is_control[s] ? 1 : 0;
+    c->nc.clear();
+    for (int s = 0; s < S; ++s)
+        if (!c->ctl[s]) c->nc.push_back(s);
+    c->coef.clear();
+    if (p->n_coeffs) {
+        if (!p->coeffs || p->n_coeffs != c->nc.size()) return UP_E_ARG;
+        c->coef.assign(p->coeffs, p->coeffs + p->n_coeffs);
+    }
+    c->p.is_control = nullptr;
+    c->p.coeffs = nullptr;
+    c->kern.assign(2 * p->bw + 1, 0.0);
+    up_kernel_weights(p->bw, 1 / p->background, c->kern.data());
+    HIPCHK(c->d_kern.ensure(c->kern.size()));
+    HIPCHK(hipMemcpy(c->d_kern.p, c->kern.data(), c->kern.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(c->d_nc.ensure(c->nc.size() + 1));
+    if (!c->nc.empty())
+        HIPCHK(hipMemcpy(c->d_nc.p, c->nc.data(), c->nc.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(c->d_ctl.ensure(S));
+    HIPCHK(hipMemcpy(c->d_ctl.p, c->ctl.data(), S, hipMemcpyHostToDevice));
+    HIPCHK(c->d_coef.ensure(c->coef.size() + 1));
+    if (!c->coef.empty())
+        HIPCHK(hipMemcpy(c->d_coef.p, c->coef.data(), c->coef.size() * sizeof(double), hipMemcpyHostToDevice));
+    c->have_params = true;
+    c->units_dirty = true;
+    return UP_OK;
+}
+
+// track geometry: positions 1..len plus the scan domain up to len+bw (Q16),
+// rounded to whole strips, with kPad zero elements on both sides
+static uint64_t unit_stride(uint32_t len) {
+    const uint64_t dom = (uint64_t)len + kMaxBw + 1;
+    const uint64_t strips = (dom + kStrip - 1) / kStrip;
+    return (uint64_t)kPad + strips * kStrip + kPad;
+}
+
+int up_add_unit(up_ctx *c, uint32_t len, int32_t nstrands, int32_t buffer_id, uint32_t *unit_id) {
+    if (!c || !c->have_params || (nstrands != 1 && nstrands != 2)) return c && !c->have_params ? UP_E_STATE : UP_E_ARG;
+    if (nstrands != (c->p.nondir ? 2 : 1)) return UP_E_ARG;
+    HIPCHK(hipSetDevice(c->dev));
+    Unit u;
+    u.len = len;
+    u.nstrands = nstrands;
+    u.buffer = buffer_id;
+    u.stride = unit_stride(len);
+    const size_t bytes = u.stride * (size_t)c->p.n_samples * nstrands * sizeof(uint32_t);
+    hipError_t e = hipMalloc(&u.dptr, bytes);
+    if (e != hipSuccess) return UP_E_NOMEM;
+    HIPCHK(hipMemsetAsync(u.dptr, 0, bytes, c->stream));
+    c->units.push_back(u);
+    c->units_dirty = true;
+    c->ran = false;
+    if (unit_id) *unit_id = (uint32_t)(c->units.size() - 1);
+    return UP_OK;
+}
+
+int up_unit_count(up_ctx *c, uint32_t *n) {
+    if (!c || !n) return UP_E_ARG;
+    *n = (uint32_t)c->units.size();
+    return UP_OK;
+}
+
+int up_reset_units(up_ctx *c) {
+    if (!c) return UP_E_ARG;
+    (void)hipSetDevice(c->dev);
+    (void)hipStreamSynchronize(c->stream);
+    free_units(c);
+    return UP_OK;
+}
+
+static uint32_t *track_ptr(up_ctx *c, uint32_t unit, int strand, uint16_t sample) {
+    const Unit &u = c->units[unit];
+    return u.dptr + ((uint64_t)strand * c->p.n_samples + sample) * u.stride;
+}
+
+static int check_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample) {
+    if (!c || !c->have_params) return UP_E_STATE;
+    if (unit >= c->units.size() || strand < 0 || strand >= c->units[unit].nstrands ||
+        sample >= c->p.n_samples)
+        return UP_E_ARG;
+    return UP_OK;
+}
+
+int up_unit_ptr(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uint32_t **ptr) {
+    int r = check_track(c, unit, strand, sample);
+    if (r) return r;
+    if (!ptr) return UP_E_ARG;
+    *ptr = track_ptr(c, unit, strand, sample) + kPad;
+    return UP_OK;
+}
+
+int up_unit_scatter(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, size_t n,
+                    const uint32_t *pos, const uint32_t *counts) {
+    int r = check_track(c, unit, strand, sample);
+    if (r) return r;
+    if (n == 0) return UP_OK;
+    if (!pos || !counts) return UP_E_ARG;
+    const uint32_t len = c->units[unit].len;
+    for (size_t i = 0; i < n; ++i)
+        if (pos[i] == 0 || pos[i] > len) return UP_E_ARG;
+    HIPCHK(hipSetDevice(c->dev));
+    uint32_t *d = nullptr;
+    HIPCHK(hipMalloc(&d, 2 * n * sizeof(uint32_t)));
+    HIPCHK(hipMemcpyAsync(d, pos, n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d + n, counts, n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
+                       track_ptr(c, unit, strand, sample), d, d + n, (uint64_t)n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipFree(d));
+    c->ran = false;
+    return UP_OK;
+}
+
+// ---- synthetic input (DESIGN.md "Synthetic input"; oracle/orc_synth.c) ----
+static uint64_t hmix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+int up_unit_synth(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uint64_t seed,
+                  uint32_t contig_index, int32_t synth_strand, int32_t nondir, int32_t with_peaks) {
+    int r = check_track(c, unit, strand, sample);
+    if (r) return r;
+    HIPCHK(hipSetDevice(c->dev));
+    const uint32_t len = c->units[unit].len;
+    const int bw = c->p.bw;
+    const uint64_t skey = hmix(seed);
+    const uint64_t ckey = hmix(skey ^ (uint64_t)(contig_index + 1));
+    const uint64_t tkey = hmix(ckey ^ (uint64_t)(0x100 + synth_strand));
+    const uint64_t pkey = hmix(ckey ^ (uint64_t)(0x200 + (nondir ? 0 : synth_strand)));
+    const int64_t lo = 2 * (int64_t)bw + 2, hi = (int64_t)len - 2 * (int64_t)bw - 1;
+    if (hi < lo) return UP_OK;
+    SynthThr thr;
+    {
+        const double lambda = 0.002925;
+        double pr = std::exp(-lambda), cdf = pr;
+        for (int k = 0; k < 6; ++k) {
+            thr.t[k] = cdf >= 1.0 ? ~0ull : (uint64_t)(cdf * 18446744073709551616.0);
+            pr *= lambda / (double)(k + 1);
+            cdf += pr;
+        }
+    }
+    uint32_t *trk = track_ptr(c, unit, strand, sample);
+    const uint64_t npos = (uint64_t)(hi - lo + 1);
+    hipLaunchKernelGGL(synth_bg_kernel, dim3((unsigned)((npos + 255) / 256)), dim3(256), 0,
+                       c->stream, trk, tkey, lo, hi, thr);
+    HIPCHK(hipGetLastError());
+    if (with_peaks) {
+        std::vector<uint32_t> tags;
+        uint32_t npk = len / 150000u;
+        if (npk < 1) npk = 1;
+        int64_t clo, chi;
+        if (len >= 20001u) { clo = 10000; chi = (int64_t)len - 10000; }
+        else { clo = 2 * (int64_t)bw + 200; chi = (int64_t)len - 2 * (int64_t)bw - 200; }
+        const int64_t shift = (nondir && synth_strand == 1) ? 150 : 0;
+        for (uint32_t j = 0; chi >= clo && j < npk; ++j) {
+            const uint64_t h = hmix(pkey ^ hmix(0x7065616B00000000ull + j));
+            const int64_t centre = clo + (int64_t)(h % (uint64_t)(chi - clo + 1));
+            const uint32_t n = 20u + (uint32_t)(hmix(h) % 180u);
+            for (uint32_t i = 0; i < n; ++i) {
+                int64_t s = 0;
+                const uint64_t b = hmix(tkey ^ h ^ hmix(0x74616700000000ull + i));
+                for (int m = 0; m < 12; ++m) s += (int64_t)(hmix(b + (uint64_t)m) >> 32);
+                const int64_t off = (60 * (s - 6 * 4294967296ll) + 2147483648ll) >> 32;
+                const int64_t p = centre + shift + off;
+                if (p >= lo && p <= hi) tags.push_back((uint32_t)p);
+            }
+        }
+        if (!tags.empty()) {
+            uint32_t *d = nullptr;
+            HIPCHK(hipMalloc(&d, tags.size() * sizeof(uint32_t)));
+            HIPCHK(hipMemcpyAsync(d, tags.data(), tags.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+            hipLaunchKernelGGL(synth_peak_kernel, dim3((unsigned)((tags.size() + 255) / 256)), dim3(256), 0,
+                               c->stream, trk, d, (uint64_t)tags.size());
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(c->stream));
+            HIPCHK(hipFree(d));
+        }
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->ran = false;
+    return UP_OK;
+}
+
+int up_unit_tag_total(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uint64_t *total) {
+    int r = check_track(c, unit, strand, sample);
+    if (r) return r;
+    if (!total) return UP_E_ARG;
+    HIPCHK(hipSetDevice(c->dev));
+    unsigned long long *d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(d, 0, sizeof(unsigned long long), c->stream));
+    const Unit &u = c->units[unit];
+    hipLaunchKernelGGL(track_sum_kernel, dim3(1024), dim3(256), 0, c->stream,
+                       track_ptr(c, unit, strand, sample), (uint64_t)u.stride, d);
+    HIPCHK(hipGetLastError());
+    unsigned long long h = 0;
+    HIPCHK(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    (void)hipFree(d);
+    *total = h;
+    return UP_OK;
+}
+
+int up_unit_set_last_add(up_ctx *c, uint32_t unit, uint32_t last) {
+    if (!c || unit >= c->units.size()) return UP_E_ARG;
+    c->units[unit].last_override = last;
+    c->units[unit].has_override = true;
+    return UP_OK;
+}
+
+int up_unit_last_add(up_ctx *c, uint32_t unit, uint32_t *last) {
+    if (!c || !last || unit >= c->units.size()) return UP_E_ARG;
+    if (c->units[unit].has_override) { *last = c->units[unit].last_override; return UP_OK; }
+    if (!c->ran) return UP_E_STATE;
+    *last = c->unit_last[unit];
+    return UP_OK;
+}
+
+static int sync_units(up_ctx *c) {
+    if (!c->units_dirty && c->bw_layout == c->p.bw) return UP_OK;
+    std::vector<UnitDesc> d(c->units.size());
+    uint32_t strip = 0;
+    for (size_t i = 0; i < c->units.size(); ++i) {
+        Unit &u = c->units[i];
+        const uint64_t dom = (uint64_t)u.len + c->p.bw;
+        u.nstrips = (uint32_t)((dom + kStrip - 1) / kStrip);
+        u.strip0 = strip;
+        strip += u.nstrips;
+        d[i] = UnitDesc{(uint64_t)(uintptr_t)u.dptr, u.stride, u.len, u.strip0, u.nstrips, u.nstrands};
+    }
+    c->nstrips = strip;
+    HIPCHK(c->d_units.ensure(d.size()));
+    HIPCHK(hipMemcpy(c->d_units.p, d.data(), d.size() * sizeof(UnitDesc), hipMemcpyHostToDevice));
+    c->units_dirty = false;
+    c->bw_layout = c->p.bw;
+    return UP_OK;
+}
+
+static int pool_mode(const up_ctx *c) {
+    if (!c->coef.empty()) return 2;
+    return c->nc.size() == 1 ? 0 : 1;
+}
+
+static ScanParams scan_params(up_ctx *c) {
+    ScanParams P{};
+    P.units = c->d_units.p;
+    P.nunits = (uint32_t)c->units.size();
+    P.nstrips = c->nstrips;
+    P.S = c->p.n_samples;
+    P.nnc = (int32_t)c->nc.size();
+    P.nc = c->d_nc.p;
+    P.coef = c->d_coef.p;
+    P.kern = c->d_kern.p;
+    P.bw = c->p.bw;
+    P.thr = c->p.region_thr;
+    P.strip_info = c->d_info.p;
+    P.rec = c->d_rec.p;
+    P.strip_lastnz = c->d_lastnz.p;
+    P.ovf_count = c->d_ovf_count.p;
+    P.ovf_rec = c->d_ovf_rec.p;
+    P.ovf_cap = c->ovf_cap;
+    return P;
+}
+
+template <int NH, int POOL, bool ND, bool PROF>
+static void launch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e) {
+    const uint32_t waves = e - b;
+    uint32_t blocks = (waves + 3) / 4;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks == 0) return;
+    const size_t lds = (2 * (size_t)P.bw + 1) * sizeof(double);
+    hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF>), dim3(blocks), dim3(256), lds, c->stream, P, b, e);
+}
+
+template <bool PROF>
+static void dispatch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e) {
+    const int nh = P.bw <= 63 ? 1 : 2;
+    const int pool = pool_mode(c);
+    const bool nd = c->p.nondir != 0;
+#define UPK_SCAN(NH, PL, ND) \
+    if (nh == NH && pool == PL && nd == ND) return launch_scan<NH, PL, ND, PROF>(c, P, b, e);
+    UPK_SCAN(1, 0, false) UPK_SCAN(1, 1, false) UPK_SCAN(1, 2, false)
+    UPK_SCAN(1, 0, true) UPK_SCAN(1, 1, true) UPK_SCAN(1, 2, true)
+    UPK_SCAN(2, 0, false) UPK_SCAN(2, 1, false) UPK_SCAN(2, 2, false)
+    UPK_SCAN(2, 0, true) UPK_SCAN(2, 1, true) UPK_SCAN(2, 2, true)
+#undef UPK_SCAN
+}
+
+static StatParams stat_params(up_ctx *c) {
+    StatParams P{};
+    P.units = c->d_units.p;
+    P.S = c->p.n_samples;
+    P.nnc = (int32_t)c->nc.size();
+    P.nc = c->d_nc.p;
+    P.is_control = c->d_ctl.p;
+    P.coef = c->d_coef.p;
+    P.kern = c->d_kern.p;
+    P.bw = c->p.bw;
+    P.nondir = c->p.nondir;
+    P.want_corr = c->p.want_corr;
+    P.region_thr = c->p.region_thr;
+    P.kurt_thr = c->p.kurt_thr;
+    P.corr_thr = c->p.corr_thr;
+    P.hit_thr = c->p.hit_thr;
+    P.starts = c->d_starts.p;
+    P.ends = c->d_ends.p;
+    P.reg_unit = c->d_runit.p;
+    P.nreg = c->d_nreg.p;
+    P.out = c->d_regions.p;
+    P.out_counts = c->d_counts.p;
+    return P;
+}
+
+static void dispatch_stats(up_ctx *c, const StatParams &P, uint64_t nreg) {
+    const int nh = P.bw <= 63 ? 1 : 2;
+    const int pool = pool_mode(c);
+    const bool nd = c->p.nondir != 0;
+    uint64_t blocks = (nreg + 3) / 4;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks == 0) return;
+    const size_t lds = (2 * (size_t)P.bw + 1) * sizeof(double);
+#define UPK_ST(NH, PL, ND)                                                                   \
+    if (nh == NH && pool == PL && nd == ND) {                                                \
+        hipLaunchKernelGGL((stats_kernel<NH, PL, ND>), dim3((unsigned)blocks), dim3(256), lds, \
+                           c->stream, P);                                                     \
+        return;                                                                              \
+    }
+    UPK_ST(1, 0, false) UPK_ST(1, 1, false) UPK_ST(1, 2, false)
+    UPK_ST(1, 0, true) UPK_ST(1, 1, true) UPK_ST(1, 2, true)
+    UPK_ST(2, 0, false) UPK_ST(2, 1, false) UPK_ST(2, 2, false)
+    UPK_ST(2, 0, true) UPK_ST(2, 1, true) UPK_ST(2, 2, true)
+#undef UPK_ST
+}
+
+static int check_runnable(up_ctx *c) {
+    if (!c || !c->have_params) return UP_E_STATE;
+    if (c->p.bw < 1 || c->p.bw > kMaxBw) return UP_E_UNSUPPORTED;
+    if (c->p.n_samples > 256) return UP_E_UNSUPPORTED;
+    // thresholds <= 0 make the leap path of processPosition (Q11) live
+    if (!(c->p.region_thr > 0)) return UP_E_UNSUPPORTED;
+    return UP_OK;
+}
+
+int up_run(up_ctx *c, uint64_t *n_regions) {
+    int r = check_runnable(c);
+    if (r) return r;
+    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(hipSetDevice(c->dev));
+    c->ran = false;
+    c->nreg = 0;
+    if (c->units.empty()) {
+        if (n_regions) *n_regions = 0;
+        c->ran = true;
+        return UP_OK;
+    }
+    if ((r = sync_units(c))) return r;
+    const uint32_t ns = c->nstrips;
+    HIPCHK(c->d_info.ensure(ns));
+    HIPCHK(c->d_lastnz.ensure(ns));
+    HIPCHK(c->d_rec.ensure((size_t)ns * 2 * kCap));
+    HIPCHK(c->d_cnt.ensure(ns));
+    HIPCHK(c->d_off.ensure(ns));
+    HIPCHK(c->d_ovf_count.ensure(1));
+    HIPCHK(c->d_nreg.ensure(1));
+    HIPCHK(c->d_unit_last.ensure(c->units.size()));
+    size_t tmp = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, c->d_cnt.p, c->d_off.p, (int)ns, c->stream));
+    HIPCHK(c->d_tmp.ensure(tmp + 16));
+
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        HIPCHK(c->d_ovf_rec.ensure((size_t)c->ovf_cap * kOvfStride));
+        HIPCHK(hipMemsetAsync(c->d_ovf_count.p, 0, sizeof(uint32_t), c->stream));
+        ScanParams SP = scan_params(c);
+        HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        dispatch_scan<false>(c, SP, 0, ns);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev[1], c->stream));
+        hipLaunchKernelGGL(finalize_kernel, dim3((ns + 255) / 256), dim3(256), 0, c->stream,
+                           c->d_info.p, c->d_cnt.p, ns);
+        HIPCHK(hipGetLastError());
+        size_t tb = c->d_tmp.n;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->d_tmp.p, tb, c->d_cnt.p, c->d_off.p, (int)ns, c->stream));
+        uint64_t tail[2];
+        uint32_t ovf = 0;
+        HIPCHK(hipMemcpyAsync(&tail[0], c->d_cnt.p + ns - 1, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(&tail[1], c->d_off.p + ns - 1, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(&ovf, c->d_ovf_count.p, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (ovf > c->ovf_cap) {  // more spilled strips than slots: grow and redo
+            c->ovf_cap = ovf + ovf / 2 + 64;
+            continue;
+        }
+        const uint64_t tot = tail[0] + tail[1];
+        const uint64_t nst = tot & 0xFFFFFFFFull, nen = tot >> 32;
+        if (nst != nen) return UP_E_INTERNAL;
+        c->nreg = nst;
+        break;
+    }
+    const uint64_t nreg = c->nreg;
+    HIPCHK(c->d_starts.ensure(nreg + 1));
+    HIPCHK(c->d_ends.ensure(nreg + 1));
+    HIPCHK(c->d_runit.ensure(nreg + 1));
+    HIPCHK(c->d_regions.ensure(nreg + 1));
+    HIPCHK(c->d_counts.ensure((nreg + 1) * c->p.n_samples));
+    hipLaunchKernelGGL(compact_kernel, dim3((ns + 255) / 256), dim3(256), 0, c->stream, c->d_units.p,
+                       (uint32_t)c->units.size(), c->d_info.p, c->d_cnt.p, c->d_off.p, c->d_rec.p,
+                       c->d_ovf_rec.p, c->ovf_cap, c->d_starts.p, c->d_ends.p, c->d_runit.p, ns);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->d_nreg.p, &c->nreg, 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    StatParams P = stat_params(c);
+    dispatch_stats(c, P, nreg);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    hipLaunchKernelGGL(unit_last_kernel, dim3((unsigned)c->units.size()), dim3(256), 0, c->stream,
+                       c->d_units.p, c->d_lastnz.p, c->d_unit_last.p);
+    HIPCHK(hipGetLastError());
+    c->unit_last.resize(c->units.size());
+    HIPCHK(hipMemcpyAsync(c->unit_last.data(), c->d_unit_last.p, c->units.size() * 4,
+                          hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float a = 0, b = 0, d = 0;
+    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+    (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+    (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+    c->times[0] = a;
+    c->times[1] = b;
+    c->times[2] = d;
+    c->times[3] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->ran = true;
+    if (n_regions) *n_regions = nreg;
+    return UP_OK;
+}
+
+int up_get_regions(up_ctx *c, up_region *out, uint32_t *counts, size_t cap) {
+    if (!c) return UP_E_ARG;
+    if (!c->ran) return UP_E_STATE;
+    const size_t n = c->nreg < cap ? (size_t)c->nreg : cap;
+    HIPCHK(hipSetDevice(c->dev));
+    if (n && out)
+        HIPCHK(hipMemcpyAsync(out, c->d_regions.p, n * sizeof(up_region), hipMemcpyDeviceToHost, c->stream));
+    if (n && counts)
+        HIPCHK(hipMemcpyAsync(counts, c->d_counts.p, n * c->p.n_samples * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return UP_OK;
+}
+
+int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, double *out) {
+    if (!c || (n && (!idx || !out))) return UP_E_ARG;
+    if (!c->ran) return UP_E_STATE;
+    if (!c->p.nondir) return UP_E_UNSUPPORTED;
+    if (n == 0) return UP_OK;
+    HIPCHK(hipSetDevice(c->dev));
+    std::vector<uint32_t> st(c->nreg), en(c->nreg);
+    HIPCHK(hipMemcpy(st.data(), c->d_starts.p, c->nreg * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(en.data(), c->d_ends.p, c->nreg * 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> off(n);
+    uint64_t tot = 0;
+    for (size_t j = 0; j < n; ++j) {
+        if (idx[j] >= c->nreg) return UP_E_ARG;
+        off[j] = tot;
+        tot += 2ull * (en[idx[j]] - st[idx[j]] + 1);
+    }
+    uint64_t *d_idx = nullptr, *d_off = nullptr;
+    double *d_slab = nullptr, *d_out = nullptr;
+    HIPCHK(hipMalloc(&d_idx, n * 8));
+    HIPCHK(hipMalloc(&d_off, n * 8));
+    HIPCHK(hipMalloc(&d_slab, (tot + 1) * 8));
+    HIPCHK(hipMalloc(&d_out, n * ((size_t)max_shift + 1) * 8));
+    HIPCHK(hipMemcpy(d_idx, idx, n * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_off, off.data(), n * 8, hipMemcpyHostToDevice));
+    StatParams P = stat_params(c);
+    const int nh = P.bw <= 63 ? 1 : 2;
+    const int pool = pool_mode(c);
+    const size_t lds = (2 * (size_t)P.bw + 1) * sizeof(double);
+    const unsigned blocks = (unsigned)std::min<size_t>(n, 8192);
+#define UPK_SH(NH, PL)                                                                        \
+    if (nh == NH && pool == PL)                                                               \
+        hipLaunchKernelGGL((shift_kernel<NH, PL>), dim3(blocks), dim3(64), lds, c->stream, P, \
+                           d_idx, (uint32_t)n, (int)max_shift, d_off, d_slab, d_out);
+    UPK_SH(1, 0) UPK_SH(1, 1) UPK_SH(1, 2) UPK_SH(2, 0) UPK_SH(2, 1) UPK_SH(2, 2)
+#undef UPK_SH
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(out, d_out, n * ((size_t)max_shift + 1) * 8, hipMemcpyDeviceToHost));
+    (void)hipFree(d_idx);
+    (void)hipFree(d_off);
+    (void)hipFree(d_slab);
+    (void)hipFree(d_out);
+    return UP_OK;
+}
+
+int up_timings(up_ctx *c, double *ms, int n) {
+    if (!c || !ms) return UP_E_ARG;
+    for (int i = 0; i < n && i < 5; ++i) ms[i] = c->times[i];
+    return UP_OK;
+}
+
+int up_unit_profile(up_ctx *c, uint32_t unit, double *out_f, double *out_r, uint32_t len) {
+    int r = check_runnable(c);
+    if (r) return r;
+    if (unit >= c->units.size() || !out_f || !out_r) return UP_E_ARG;
+    HIPCHK(hipSetDevice(c->dev));
+    if ((r = sync_units(c))) return r;
+    double *d = nullptr;
+    HIPCHK(hipMalloc(&d, 2 * (size_t)len * sizeof(double) + 16));
+    HIPCHK(hipMemsetAsync(d, 0, 2 * (size_t)len * sizeof(double), c->stream));
+    ScanParams P = scan_params(c);
+    P.prof_f = d;
+    P.prof_r = d + len;
+    P.prof_len = len;
+    P.prof_unit = unit;
+    const Unit &u = c->units[unit];
+    dispatch_scan<true>(c, P, u.strip0, u.strip0 + u.nstrips);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(out_f, d, (size_t)len * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out_r, d + len, (size_t)len * sizeof(double), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return UP_OK;
+}

@@ -1,0 +1,79 @@
+// unipeak_amd/csrc/kernels.h -- device data layout shared by the gfx950
+// kernels (kernels.hip) and the C-ABI implementation (api.hip).
+//
+// HBM layout (DESIGN.md "Data layout"): every (unit, strand, sample) track is
+// a dense uint32 array; position p (1-based) of a track lives at element
+// kPad + p - 1, with kPad zero elements in front and at least kPad behind
+// the unit's scan domain [1, len + bw], so every halo load is in bounds and
+// reads zeros outside the contig.  Tracks of one unit are contiguous:
+// track(s, k) = base + (s * S + k) * stride.
+#pragma once
+#include <stdint.h>
+
+namespace upk {
+
+constexpr int kWave = 64;           // CDNA wavefront
+constexpr int kStripWords = 16;     // one strip = 16 words of 64 positions
+constexpr int kStrip = kStripWords * kWave;  // 1024 positions per wave task
+constexpr int kPad = 2112;          // 33 words: covers bw <= 2047 halos
+constexpr int kMaxBw = 127;         // register-resident halo: NH <= 2 words
+constexpr int kCap = 8;             // inline run records per strip
+constexpr int kOvfStride = 2 * (kStrip / 2 + 1);  // starts + ends of one strip
+
+struct UnitDesc {
+    uint64_t base;      // device address of track (0, 0)
+    uint64_t stride;    // elements per track
+    uint32_t len;       // contig length
+    uint32_t strip0;    // first global strip index
+    uint32_t nstrips;   // strips covering [1, len + bw]
+    int32_t nstrands;   // 1 or 2
+};
+
+// packed per-strip summary written by the scan kernel
+//   bits  0- 9 interior run starts, 10-19 interior run ends,
+//   bit  20 flag(first position), 21 flag(last position),
+//   bit  22 first strip of its unit, 23 last strip of its unit,
+//   bit  24 records spilled to the overflow area
+__host__ __device__ inline uint32_t si_starts(uint32_t v) { return v & 0x3FFu; }
+__host__ __device__ inline uint32_t si_ends(uint32_t v) { return (v >> 10) & 0x3FFu; }
+
+struct ScanParams {
+    const UnitDesc *units;
+    uint32_t nunits;
+    uint32_t nstrips;
+    int32_t S;          // all samples
+    int32_t nnc;        // non-control samples
+    const int32_t *nc;  // indices of non-control samples, in sample order
+    const double *coef; // per non-control sample (pool mode 2) or null
+    const double *kern; // 2*bw+1 weights
+    int32_t bw;
+    double thr;
+    uint32_t *strip_info;
+    uint32_t *rec;          // [nstrips][2*kCap]: starts then ends
+    uint32_t *strip_lastnz; // last position with a pooled hit, 0 if none
+    uint32_t *ovf_count;
+    uint32_t *ovf_rec;      // [ovf_cap][kOvfStride]
+    uint32_t ovf_cap;
+    double *prof_f, *prof_r;  // optional dense profile of one unit
+    uint32_t prof_unit, prof_len;
+};
+
+struct StatParams {
+    const UnitDesc *units;
+    int32_t S, nnc;
+    const int32_t *nc;
+    const uint8_t *is_control;
+    const double *coef;
+    const double *kern;
+    int32_t bw;
+    int32_t nondir;
+    int32_t want_corr;
+    double region_thr, kurt_thr, corr_thr, hit_thr;
+    const uint32_t *starts, *ends, *reg_unit;
+    const uint64_t *nreg;
+    void *out;            // up_region records
+    uint32_t *out_counts; // [n][S]
+    uint32_t *scratch;    // per-wave exptSums accumulators [waves][S]
+};
+
+}  // namespace upk

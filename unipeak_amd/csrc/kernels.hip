@@ -1,0 +1,658 @@
+// unipeak_amd/csrc/kernels.hip -- gfx950 kernels of the KDE smoothing +
+// enriched-region scan (reference: misc/peakcall.cpp:33-231,
+// misc/kernel.cpp:12-35, misc/data.cpp:22-193).
+//
+// Exactness contract: every score is the FP64 left-to-right sum, over the
+// hits h of the window in ascending order, of kernel[x-h+bw] * countSum[h]
+// (one multiply, one add -- the order ProfileBuffer::add accumulates into
+// its deque cells, peakcall.cpp:203-209).  Built with -ffp-contract=off so
+// no FMA fuses the pair; zero-count positions are skipped exactly as the
+// reference skips countSum == 0 adds.  The work is proportional to hits, not
+// taps: a wave owns 64 consecutive positions per step and walks the hit
+// bitmaps (wave ballots) of the neighbouring words in ascending order,
+// broadcasting each hit's pooled count with v_readlane.
+//
+// Kernels
+//   K1 scan_kernel     pool + KDE + threshold flags + run boundaries per strip
+//   K2 finalize/scatter  strip-boundary fix-up, scan, compaction to regions
+//   K3 stats_kernel    per-region peak, exptSums, kurtosis, strandCorr, filter
+//   K4 shift_kernel    strandCorr(shift) table for bin/strand_shift
+//   aux: scatter, synthetic input, unit last-add reduction
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "../../include/unipeak_hip.h"
+#include "kernels.h"
+
+namespace upk {
+
+__device__ __forceinline__ double rl_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ uint32_t rl_u(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// bits b of a word at offset d words from the output word whose hits can
+// reach some lane of the output word: 64d + b in [-bw, 63 + bw]
+__device__ __forceinline__ uint64_t win_mask(int d, int bw) {
+    int lo = -bw - 64 * d, hi = 63 + bw - 64 * d;
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > 63 ? 63 : hi;
+    if (lo > hi) return 0;
+    const uint64_t up = hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1);
+    return up & ~((1ull << lo) - 1);
+}
+
+// ---- pooled count (ProfileBuffer::add countSum, peakcall.cpp:186-200) ----
+// POOL 0: one non-control sample, no coefficients; 1: several, unscaled;
+// 2: scaled by coefficients plus the unscaled second loop (quirk Q5).
+template <int NWT, int POOL>
+__device__ __forceinline__ void load_pool(double (&cs)[NWT], const uint32_t *strand_base,
+                                          uint64_t stride, int64_t idx0, int lane, int nnc,
+                                          const int32_t *nc, const double *coef) {
+    if (POOL == 0) {
+        const uint32_t *t = strand_base + (uint64_t)nc[0] * stride + idx0 + lane;
+        uint32_t c[NWT];
+#pragma unroll
+        for (int w = 0; w < NWT; ++w) c[w] = __builtin_nontemporal_load(t + 64 * w);
+#pragma unroll
+        for (int w = 0; w < NWT; ++w) cs[w] = (double)c[w];
+    } else {
+#pragma unroll
+        for (int w = 0; w < NWT; ++w) cs[w] = 0.0;
+        for (int k = 0; k < nnc; ++k) {
+            const uint32_t *t = strand_base + (uint64_t)nc[k] * stride + idx0 + lane;
+            uint32_t c[NWT];
+#pragma unroll
+            for (int w = 0; w < NWT; ++w) c[w] = __builtin_nontemporal_load(t + 64 * w);
+            if (POOL == 1) {
+#pragma unroll
+                for (int w = 0; w < NWT; ++w) cs[w] = cs[w] + (double)c[w];
+            } else {
+                const double q = coef[k];
+#pragma unroll
+                for (int w = 0; w < NWT; ++w) cs[w] = cs[w] + (double)c[w] * q;
+            }
+        }
+        if (POOL == 2) {
+            for (int k = 0; k < nnc; ++k) {
+                const uint32_t *t = strand_base + (uint64_t)nc[k] * stride + idx0 + lane;
+#pragma unroll
+                for (int w = 0; w < NWT; ++w) cs[w] = cs[w] + (double)t[64 * w];
+            }
+        }
+    }
+}
+
+// KDE value of lane's position in output word K: ascending walk over the
+// hits of words K-NH..K+NH (window-masked).  K must be a compile-time index.
+template <int NWT, int NH, int K>
+__device__ __forceinline__ double kde_word(const double (&cs)[NWT], const uint64_t (&hm)[NWT],
+                                           const uint64_t (&wm)[2 * NH + 1], int lane, int bw,
+                                           const double *ktab) {
+    double f = 0.0;
+#pragma unroll
+    for (int d = -NH; d <= NH; ++d) {
+        uint64_t m = hm[K + d] & wm[d + NH];
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            const double c = rl_d(cs[K + d], b);
+            const int idx = lane + (bw - 64 * d - b);
+            if ((unsigned)idx <= (unsigned)(2 * bw)) f = f + ktab[idx] * c;
+        }
+    }
+    return f;
+}
+
+template <int NWT, int NH, int K>
+struct WordLoop {
+    template <typename F>
+    __device__ __forceinline__ static void run(F &&fn) {
+        WordLoop<NWT, NH, K - 1>::run(fn);
+        fn(std::integral_constant<int, K>());
+    }
+};
+template <int NWT, int NH>
+struct WordLoop<NWT, NH, NH - 1> {
+    template <typename F>
+    __device__ __forceinline__ static void run(F &&) {}
+};
+
+__device__ __forceinline__ uint32_t find_unit(const UnitDesc *units, uint32_t nunits,
+                                              uint32_t strip) {
+    uint32_t lo = 0, hi = nunits;  // first unit with strip0 > strip, minus one
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (units[mid].strip0 <= strip) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// ------------------------------------------------------------------------
+// K1: one wave per 1024-position strip (grid-stride).
+// ------------------------------------------------------------------------
+template <int NH, int POOL, bool NONDIR, bool PROF>
+__global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_begin,
+                                                   uint32_t strip_end) {
+    extern __shared__ double ktab[];
+    const int bw = P.bw;
+    for (int i = threadIdx.x; i <= 2 * bw; i += blockDim.x) ktab[i] = P.kern[i];
+    __syncthreads();
+
+    constexpr int NW = kStripWords;
+    constexpr int NWT = NW + 2 * NH;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+
+    uint64_t wm[2 * NH + 1];
+#pragma unroll
+    for (int d = -NH; d <= NH; ++d) wm[d + NH] = win_mask(d, bw);
+
+    uint32_t cur = 0;
+    bool have = false;
+    for (uint32_t strip = strip_begin + wave; strip < strip_end; strip += nwaves) {
+        if (!have) { cur = find_unit(P.units, P.nunits, strip); have = true; }
+        while (strip >= P.units[cur].strip0 + P.units[cur].nstrips) ++cur;
+        const UnitDesc U = P.units[cur];
+        const uint32_t local = strip - U.strip0;
+        const int64_t p0 = 1 + (int64_t)local * kStrip;  // first position of the strip
+        const int64_t idx0 = kPad + p0 - 1 - 64 * NH;     // element of word 0 (halo)
+        const uint32_t *base = (const uint32_t *)U.base;
+        const uint64_t sstride = (uint64_t)P.S * U.stride;
+
+        double cf[NWT];
+        uint64_t hf[NWT];
+        load_pool<NWT, POOL>(cf, base, U.stride, idx0, lane, P.nnc, P.nc, P.coef);
+#pragma unroll
+        for (int w = 0; w < NWT; ++w) hf[w] = __ballot(cf[w] != 0.0);
+        double cr[NONDIR ? NWT : 1];
+        uint64_t hr[NONDIR ? NWT : 1];
+        if constexpr (NONDIR) {
+            load_pool<NWT, POOL>(cr, base + sstride, U.stride, idx0, lane, P.nnc, P.nc, P.coef);
+#pragma unroll
+            for (int w = 0; w < NWT; ++w) hr[w] = __ballot(cr[w] != 0.0);
+        }
+
+        uint64_t F[NW];
+        WordLoop<NWT, NH, NH + NW - 1>::run([&](auto kc) {
+            constexpr int K = decltype(kc)::value;
+            double s = kde_word<NWT, NH, K>(cf, hf, wm, lane, bw, ktab);
+            double r = 0.0;
+            if constexpr (NONDIR) {
+                r = kde_word<NWT, NH, K>(cr, hr, wm, lane, bw, ktab);
+                if constexpr (PROF) {
+                    const int64_t p = p0 + 64 * (K - NH) + lane;
+                    if (p <= P.prof_len) { P.prof_f[p - 1] = s; P.prof_r[p - 1] = r; }
+                }
+                s = s + r;  // processPosition: forwardScore + reverseScore
+            } else if constexpr (PROF) {
+                const int64_t p = p0 + 64 * (K - NH) + lane;
+                if (p <= P.prof_len) { P.prof_f[p - 1] = s; P.prof_r[p - 1] = 0.0; }
+            }
+            F[K - NH] = __ballot(s >= P.thr);
+        });
+        if constexpr (PROF) continue;
+
+        // interior run boundaries (a start at p0 / an end at p0+1023 depends
+        // on the neighbour strip and is resolved in K2)
+        uint32_t ns = 0, ne = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const uint64_t prevb = k == 0 ? 1ull : (F[k - 1] >> 63);
+            const uint64_t nextb = k == NW - 1 ? 1ull : (F[k + 1] & 1ull);
+            ns += __builtin_popcountll(F[k] & ~((F[k] << 1) | prevb));
+            ne += __builtin_popcountll(F[k] & ~((F[k] >> 1) | (nextb << 63)));
+        }
+        uint32_t info = ns | (ne << 10) | ((uint32_t)(F[0] & 1ull) << 20) |
+                        ((uint32_t)(F[NW - 1] >> 63) << 21) | ((local == 0) << 22) |
+                        ((local + 1 == U.nstrips) << 23);
+        uint32_t *dst = P.rec + (uint64_t)strip * (2 * kCap);
+        uint32_t so = 0, eo = kCap;
+        if (ns > kCap || ne > kCap) {
+            uint32_t slot = 0;
+            if (lane == 0) slot = atomicAdd(P.ovf_count, 1u);
+            slot = rl_u(slot, 0);
+            if (lane == 0) dst[0] = slot;
+            info |= 1u << 24;
+            dst = slot < P.ovf_cap ? P.ovf_rec + (uint64_t)slot * kOvfStride : nullptr;
+            eo = kStrip / 2 + 1;
+        }
+        if ((ns | ne) && dst) {
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                const uint64_t prevb = k == 0 ? 1ull : (F[k - 1] >> 63);
+                const uint64_t nextb = k == NW - 1 ? 1ull : (F[k + 1] & 1ull);
+                uint64_t st = F[k] & ~((F[k] << 1) | prevb);
+                uint64_t en = F[k] & ~((F[k] >> 1) | (nextb << 63));
+                while (st) {
+                    const int b = __builtin_ctzll(st);
+                    st &= st - 1;
+                    if (lane == 0) dst[so] = (uint32_t)(p0 + 64 * k + b);
+                    ++so;
+                }
+                while (en) {
+                    const int b = __builtin_ctzll(en);
+                    en &= en - 1;
+                    if (lane == 0) dst[eo] = (uint32_t)(p0 + 64 * k + b);
+                    ++eo;
+                }
+            }
+        }
+        // last position with a pooled hit (an add() with countSum != 0)
+        uint32_t lastnz = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            uint64_t h = hf[NH + k];
+            if constexpr (NONDIR) h |= hr[NH + k];
+            if (h) lastnz = (uint32_t)(p0 + 64 * k + 63 - __builtin_clzll(h));
+        }
+        if (lane == 0) {
+            P.strip_info[strip] = info;
+            P.strip_lastnz[strip] = lastnz;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// K2a: resolve strip-boundary starts/ends, pack (starts, ends) as uint64
+// ------------------------------------------------------------------------
+__global__ void finalize_kernel(const uint32_t *__restrict__ info, uint64_t *__restrict__ cnt,
+                                uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t v = info[i];
+    const uint32_t prev_last = (v >> 22) & 1 ? 0 : (info[i - 1] >> 21) & 1;
+    const uint32_t next_first = (v >> 23) & 1 ? 0 : (info[i + 1] >> 20) & 1;
+    const uint32_t xs = ((v >> 20) & 1) & !prev_last;
+    const uint32_t xe = ((v >> 21) & 1) & !next_first;
+    cnt[i] = (uint64_t)(si_starts(v) + xs) | ((uint64_t)(si_ends(v) + xe) << 32);
+}
+
+// K2c: compaction of run boundaries into region lists
+__global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
+                               const uint32_t *__restrict__ info, const uint64_t *__restrict__ cnt,
+                               const uint64_t *__restrict__ off, const uint32_t *__restrict__ rec,
+                               const uint32_t *__restrict__ ovf_rec, uint32_t ovf_cap,
+                               uint32_t *__restrict__ starts, uint32_t *__restrict__ ends,
+                               uint32_t *__restrict__ reg_unit, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t c = cnt[i];
+    if (c == 0) return;
+    const uint32_t v = info[i];
+    const uint32_t ns = (uint32_t)c, ne = (uint32_t)(c >> 32);
+    const uint32_t xs = ns - si_starts(v), xe = ne - si_ends(v);
+    const uint64_t o = off[i];
+    uint32_t os = (uint32_t)o, oe = (uint32_t)(o >> 32);
+    const uint32_t u = find_unit(units, nunits, i);
+    const int64_t p0 = 1 + (int64_t)(i - units[u].strip0) * kStrip;
+    const uint32_t *src = rec + (uint64_t)i * (2 * kCap);
+    uint32_t eoff = kCap;
+    if ((v >> 24) & 1) {
+        const uint32_t slot = src[0];
+        if (slot >= ovf_cap) return;  // reported by the host as overflow
+        src = ovf_rec + (uint64_t)slot * kOvfStride;
+        eoff = kStrip / 2 + 1;
+    }
+    if (xs) { starts[os] = (uint32_t)p0; reg_unit[os] = u; ++os; }
+    for (uint32_t k = 0; k < si_starts(v); ++k) { starts[os] = src[k]; reg_unit[os] = u; ++os; }
+    for (uint32_t k = 0; k < si_ends(v); ++k) ends[oe++] = src[eoff + k];
+    if (xe) ends[oe++] = (uint32_t)(p0 + kStrip - 1);
+}
+
+// per-unit last add: max over the unit's strips
+__global__ void unit_last_kernel(const UnitDesc *units, const uint32_t *__restrict__ lastnz,
+                                 uint32_t *__restrict__ out) {
+    const UnitDesc U = units[blockIdx.x];
+    uint32_t m = 0;
+    for (uint32_t s = threadIdx.x; s < U.nstrips; s += blockDim.x) {
+        const uint32_t v = lastnz[U.strip0 + s];
+        m = v > m ? v : m;
+    }
+    __shared__ uint32_t red[256];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k && red[threadIdx.x + k] > red[threadIdx.x])
+            red[threadIdx.x] = red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+// ------------------------------------------------------------------------
+// K3: region statistics, one wave per region (grid-stride).
+// ------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+
+// pooled counts of the 2NH+1 words around block start x0 for one strand
+template <int NH, int POOL>
+__device__ __forceinline__ void region_words(double (&cs)[2 * NH + 1], uint64_t (&hm)[2 * NH + 1],
+                                             const uint32_t *strand_base, uint64_t stride,
+                                             int64_t x0, int lane, const StatParams &P) {
+    const int64_t idx0 = kPad + x0 - 1 - 64 * NH;
+    load_pool<2 * NH + 1, POOL>(cs, strand_base, stride, idx0, lane, P.nnc, P.nc, P.coef);
+#pragma unroll
+    for (int w = 0; w < 2 * NH + 1; ++w) hm[w] = __ballot(cs[w] != 0.0);
+}
+
+template <int NH, int POOL, bool NONDIR>
+__global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
+    extern __shared__ double ktab[];
+    const int bw = P.bw;
+    for (int i = threadIdx.x; i <= 2 * bw; i += blockDim.x) ktab[i] = P.kern[i];
+    __syncthreads();
+    constexpr int NWT = 2 * NH + 1;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    const uint64_t nreg = *P.nreg;
+    uint64_t wm[2 * NH + 1];
+#pragma unroll
+    for (int d = -NH; d <= NH; ++d) wm[d + NH] = win_mask(d, bw);
+    const int S = P.S;  // <= 256 (checked by the host)
+
+    for (uint64_t ri = wave; ri < nreg; ri += nwaves) {
+        const uint32_t left = P.starts[ri], right = P.ends[ri], u = P.reg_unit[ri];
+        const UnitDesc U = P.units[u];
+        const uint32_t *base = (const uint32_t *)U.base;
+        const uint64_t sstride = (uint64_t)S * U.stride;
+        uint32_t esum[4] = {0, 0, 0, 0};  // exptSums[s] lives in lane s%64, slot s/64
+
+        uint32_t cnt_acc = 0, sum_acc = 0;
+        double best = 0.0;
+        int64_t best_x = -1;
+        double sf = 0.0, sr = 0.0;  // sequential sums of f and r (corr means)
+        // ---- pass 1: scores, peak, exptSums, kurtosis first moments ----
+        for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
+            const int64_t x = x0 + lane;
+            const bool valid = x <= (int64_t)right;
+            const int nvalid = (int)(((int64_t)right - x0 + 1) < 64 ? ((int64_t)right - x0 + 1) : 64);
+            double cf[NWT];
+            uint64_t hf[NWT];
+            region_words<NH, POOL>(cf, hf, base, U.stride, x0, lane, P);
+            double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
+            double r = 0.0;
+            uint64_t hr_c = 0;
+            double cr[NONDIR ? NWT : 1];
+            uint64_t hr[NONDIR ? NWT : 1];
+            if constexpr (NONDIR) {
+                region_words<NH, POOL>(cr, hr, base + sstride, U.stride, x0, lane, P);
+                r = kde_word<NWT, NH, NH>(cr, hr, wm, lane, bw, ktab);
+                hr_c = hr[NH];
+            }
+            const double score = NONDIR ? f + r : f;
+            if (valid && (best_x < 0 || score > best)) { best = score; best_x = x; }
+            if (NONDIR && P.want_corr) {
+                for (int l = 0; l < nvalid; ++l) {
+                    sf = sf + rl_d(f, l);
+                    sr = sr + rl_d(r, l);
+                }
+            }
+            // stored hit vectors (peakcall.cpp:210-219; quirk Q7)
+            const bool sf_hit = (hf[NH] >> lane) & 1, sr_hit = (hr_c >> lane) & 1;
+            const int64_t idx = kPad + x - 1;
+            uint32_t pc = 0;
+            for (int s = 0; s < S; ++s) {
+                uint32_t c = 0;
+                if (valid) {
+                    if (sf_hit) c += base[(uint64_t)s * U.stride + idx];
+                    if (NONDIR && sr_hit) c += base[sstride + (uint64_t)s * U.stride + idx];
+                }
+                pc += c;
+                const uint32_t t = wave_sum_u32(c);
+                if (lane == (s & 63)) {
+                    const int slot = s >> 6;
+                    esum[0] += slot == 0 ? t : 0u;
+                    esum[1] += slot == 1 ? t : 0u;
+                    esum[2] += slot == 2 ? t : 0u;
+                    esum[3] += slot == 3 ? t : 0u;
+                }
+            }
+            cnt_acc += pc;
+            sum_acc += pc * (uint32_t)(uint16_t)(x - left);
+        }
+        // peak: first maximum (Region::addPos, data.cpp:98-101)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double ob = __shfl_xor(best, o);
+            const long long ox = __shfl_xor((long long)best_x, o);
+            if (ox >= 0 && (best_x < 0 || ob > best || (ob == best && ox < best_x))) {
+                best = ob;
+                best_x = ox;
+            }
+        }
+        const uint32_t count = wave_sum_u32(cnt_acc);
+        const uint32_t psum = wave_sum_u32(sum_acc);
+
+        // ---- pass 2: kurtosis (data.cpp:164-182; powi semantics) ----
+        const double x_bar = (double)psum / (double)count;
+        double sum2 = 0.0, sum4 = 0.0;
+        for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
+            const int64_t x = x0 + lane;
+            const bool valid = x <= (int64_t)right;
+            const int64_t idx = kPad + x - 1;
+            double c0 = 0.0, c1 = 0.0;
+            // pooled count at x itself, per strand, to know what was stored
+            if (valid) {
+                if (POOL == 0) {
+                    c0 = (double)base[(uint64_t)P.nc[0] * U.stride + idx];
+                    if (NONDIR) c1 = (double)base[sstride + (uint64_t)P.nc[0] * U.stride + idx];
+                } else {
+                    for (int k = 0; k < P.nnc; ++k) {
+                        const double q = POOL == 2 ? P.coef[k] : 1.0;
+                        const uint32_t a = base[(uint64_t)P.nc[k] * U.stride + idx];
+                        c0 = POOL == 2 ? c0 + (double)a * q : c0 + (double)a;
+                        if (NONDIR) {
+                            const uint32_t b = base[sstride + (uint64_t)P.nc[k] * U.stride + idx];
+                            c1 = POOL == 2 ? c1 + (double)b * q : c1 + (double)b;
+                        }
+                    }
+                    if (POOL == 2) {
+                        for (int k = 0; k < P.nnc; ++k) {
+                            c0 = c0 + (double)base[(uint64_t)P.nc[k] * U.stride + idx];
+                            if (NONDIR) c1 = c1 + (double)base[sstride + (uint64_t)P.nc[k] * U.stride + idx];
+                        }
+                    }
+                }
+            }
+            const bool h0 = valid && c0 != 0.0, h1 = valid && NONDIR && c1 != 0.0;
+            uint32_t pc = 0;
+            for (int s = 0; s < S; ++s) {
+                if (h0) pc += base[(uint64_t)s * U.stride + idx];
+                if (h1) pc += base[sstride + (uint64_t)s * U.stride + idx];
+            }
+            uint64_t m = __ballot(h0 || h1);
+            while (m) {
+                const int l = __builtin_ctzll(m);
+                m &= m - 1;
+                const uint32_t q = rl_u(pc, l);
+                const double d = (double)(uint16_t)(x0 + l - left) - x_bar;
+                const double d2 = d * d;
+                sum2 = sum2 + (double)q * d2;
+                sum4 = sum4 + (double)q * (d2 * d2);
+            }
+        }
+        const double kurt = ((double)count - 1) * sum4 / (sum2 * sum2);
+
+        // ---- pass 3: strandCorr(0) (data.cpp:38-58, 184-193) ----
+        const uint32_t n = right - left + 1;
+        double corr = __builtin_nan("");
+        if (NONDIR && P.want_corr && n > 3) {
+            const double m1 = sf / (double)n, m2 = sr / (double)n;
+            double ss1 = 0.0, ss2 = 0.0, ssr = 0.0;
+            for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
+                const int nvalid = (int)(((int64_t)right - x0 + 1) < 64 ? ((int64_t)right - x0 + 1) : 64);
+                double cf[NWT], cr[NWT];
+                uint64_t hf[NWT], hr[NWT];
+                region_words<NH, POOL>(cf, hf, base, U.stride, x0, lane, P);
+                region_words<NH, POOL>(cr, hr, base + sstride, U.stride, x0, lane, P);
+                const double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
+                const double r = kde_word<NWT, NH, NH>(cr, hr, wm, lane, bw, ktab);
+                const double d1 = f - m1, d2 = r - m2;
+                const double p1 = d1 * d1, p2 = d2 * d2, p3 = d1 * d2;
+                for (int l = 0; l < nvalid; ++l) {
+                    ss1 = ss1 + rl_d(p1, l);
+                    ss2 = ss2 + rl_d(p2, l);
+                    ssr = ssr + rl_d(p3, l);
+                }
+            }
+            const double sd1 = sqrt(ss1 / ((double)n - 1));
+            const double sd2 = sqrt(ss2 / ((double)n - 1));
+            corr = ssr / (((double)n - 1) * sd1 * sd2);
+        }
+
+        // ---- processRegion filters (peakcall.cpp:33-53) ----
+        uint32_t nonctl = 0;
+        for (int s = 0; s < S; ++s) {
+            const int slot = s >> 6;
+            const uint32_t mine = slot == 0 ? esum[0] : slot == 1 ? esum[1] : slot == 2 ? esum[2] : esum[3];
+            const uint32_t v = rl_u(mine, s & 63);
+            if (!P.is_control[s]) nonctl += v;
+            if (lane == 0) P.out_counts[ri * S + s] = v;
+        }
+        bool acc = (double)nonctl >= P.hit_thr;
+        if (acc) acc = P.kurt_thr == 0 || (n > 1 && kurt <= P.kurt_thr);
+        if (acc) acc = P.corr_thr <= -1 || corr >= P.corr_thr;
+        if (lane == 0) {
+            up_region *o = (up_region *)P.out + ri;
+            o->unit = u;
+            o->left = left;
+            o->right = right;
+            o->peak = (uint32_t)best_x;
+            o->sum = count;
+            o->nonctl_sum = nonctl;
+            o->accepted = acc;
+            o->reserved = 0;
+            o->peak_score = best;
+            o->kurtosis = kurt;
+            o->corr = corr;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// K4: strandCorr(shift) for shift = 0..max_shift; one wave per region,
+// lanes = shifts.  f/r of the region are first materialised by the wave
+// into a scratch slab (same KDE as K3), then each lane runs the reference's
+// five sequential passes (mean, mean, sd, sd, cross) for its shift.
+// ------------------------------------------------------------------------
+template <int NH, int POOL>
+__global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t *idx, uint32_t n,
+                                                   int max_shift, const uint64_t *slab_off,
+                                                   double *slab, double *out) {
+    extern __shared__ double ktab[];
+    const int bw = P.bw;
+    for (int i = threadIdx.x; i <= 2 * bw; i += blockDim.x) ktab[i] = P.kern[i];
+    __syncthreads();
+    constexpr int NWT = 2 * NH + 1;
+    const int lane = threadIdx.x & 63;
+    uint64_t wm[2 * NH + 1];
+#pragma unroll
+    for (int d = -NH; d <= NH; ++d) wm[d + NH] = win_mask(d, bw);
+    for (uint32_t j = blockIdx.x; j < n; j += gridDim.x) {
+        const uint64_t ri = idx[j];
+        const uint32_t left = P.starts[ri], right = P.ends[ri], u = P.reg_unit[ri];
+        const UnitDesc U = P.units[u];
+        const uint32_t *base = (const uint32_t *)U.base;
+        const uint64_t sstride = (uint64_t)P.S * U.stride;
+        const uint32_t len = right - left + 1;
+        double *fs = slab + slab_off[j], *rs = fs + len;
+        for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
+            double cf[NWT], cr[NWT];
+            uint64_t hf[NWT], hr[NWT];
+            region_words<NH, POOL>(cf, hf, base, U.stride, x0, lane, P);
+            region_words<NH, POOL>(cr, hr, base + sstride, U.stride, x0, lane, P);
+            const double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
+            const double r = kde_word<NWT, NH, NH>(cr, hr, wm, lane, bw, ktab);
+            const int64_t x = x0 + lane;
+            if (x <= (int64_t)right) { fs[x - left] = f; rs[x - left] = r; }
+        }
+        __syncthreads();
+        for (int sh = lane; sh <= max_shift; sh += 64) {
+            double c = __builtin_nan("");
+            if (len > (uint32_t)(2 * sh + 3)) {
+                const uint32_t m = len - 2 * sh;
+                const double *a = fs, *b = rs + 2 * sh;
+                double s1 = 0.0, s2 = 0.0;
+                for (uint32_t i = 0; i < m; ++i) s1 = s1 + a[i];
+                for (uint32_t i = 0; i < m; ++i) s2 = s2 + b[i];
+                const double m1 = s1 / (double)m, m2 = s2 / (double)m;
+                double q1 = 0.0, q2 = 0.0, q3 = 0.0;
+                for (uint32_t i = 0; i < m; ++i) { const double d = a[i] - m1; q1 = q1 + d * d; }
+                for (uint32_t i = 0; i < m; ++i) { const double d = b[i] - m2; q2 = q2 + d * d; }
+                const double sd1 = sqrt(q1 / ((double)m - 1)), sd2 = sqrt(q2 / ((double)m - 1));
+                for (uint32_t i = 0; i < m; ++i) q3 = q3 + (a[i] - m1) * (b[i] - m2);
+                c = q3 / (((double)m - 1) * sd1 * sd2);
+            }
+            out[(uint64_t)j * (max_shift + 1) + sh] = c;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------
+// aux kernels
+// ------------------------------------------------------------------------
+__global__ void scatter_kernel(uint32_t *track, const uint32_t *__restrict__ pos,
+                               const uint32_t *__restrict__ cnt, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) track[kPad + pos[i] - 1] = cnt[i];
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct SynthThr {
+    uint64_t t[6];
+};
+
+__global__ void synth_bg_kernel(uint32_t *track, uint64_t tkey, int64_t lo, int64_t hi,
+                                SynthThr thr) {
+    const int64_t x = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x > hi) return;
+    const uint64_t u = mix64(tkey ^ mix64((uint64_t)x));
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) c += u >= thr.t[k];
+    track[kPad + x - 1] = c;
+}
+
+__global__ void track_sum_kernel(const uint32_t *__restrict__ t, uint64_t n,
+                                 unsigned long long *out) {
+    uint64_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        acc += t[i];
+    __shared__ unsigned long long red[256];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicAdd(out, red[0]);
+}
+
+__global__ void synth_peak_kernel(uint32_t *track, const uint32_t *__restrict__ pos, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&track[kPad + pos[i] - 1], 1u);
+}
+
+}  // namespace upk
