@@ -71,12 +71,13 @@ struct up_ctx {
     DevBuf<UnitDesc> d_units;
     uint32_t nstrips = 0;
     int bw_layout = -1;  // bw the strip layout was computed for
-    DevBuf<uint32_t> d_info, d_rec, d_lastnz, d_ovf_count, d_ovf_rec, d_unit_last;
+    DevBuf<uint64_t> d_info;
+    DevBuf<uint32_t> d_rec, d_lastnz, d_ovf_count, d_ovf_rec, d_unit_last;
     DevBuf<uint64_t> d_cnt, d_off, d_nreg;
     DevBuf<unsigned char> d_tmp;
     DevBuf<uint32_t> d_starts, d_ends, d_runit, d_counts;
     DevBuf<up_region> d_regions;
-    uint32_t ovf_cap = 4096;
+    uint32_t ovf_cap = 256;
     uint64_t nreg = 0;
     bool ran = false;
     std::vector<uint32_t> unit_last;
@@ -179,35 +180,46 @@ int up_set_params(up_ctx *c, const up_params *p) {
     if (!c || !p) return UP_E_ARG;
     if (p->n_samples == 0 || p->bw == 0) return UP_E_ARG;
     HIPCHK(hipSetDevice(c->dev));
-    c->p = *p;
     const int S = p->n_samples;
-    c->ctl.assign(S, 0);
+    std::vector<uint8_t> ctl(S, 0);
     if (p->is_control)
-        for (int s = 0; s < S; ++s) c->ctl[s] = p->is_control[s] ? 1 : 0;
-    c->nc.clear();
+        for (int s = 0; s < S; ++s) ctl[s] = p->is_control[s] ? 1 : 0;
+    std::vector<int32_t> nc;
     for (int s = 0; s < S; ++s)
-        if (!c->ctl[s]) c->nc.push_back(s);
-    c->coef.clear();
+        if (!ctl[s]) nc.push_back(s);
+    std::vector<double> coef;
     if (p->n_coeffs) {
-        if (!p->coeffs || p->n_coeffs != c->nc.size()) return UP_E_ARG;
-        c->coef.assign(p->coeffs, p->coeffs + p->n_coeffs);
+        if (!p->coeffs || p->n_coeffs != nc.size()) return UP_E_ARG;
+        coef.assign(p->coeffs, p->coeffs + p->n_coeffs);
     }
+    std::vector<double> kern(2 * p->bw + 1, 0.0);
+    up_kernel_weights(p->bw, 1 / p->background, kern.data());
+    // upload only what changed (a bench step re-sets identical parameters)
+    const bool same = c->have_params && ctl == c->ctl && nc == c->nc && coef == c->coef &&
+                      kern.size() == c->kern.size() &&
+                      std::memcmp(kern.data(), c->kern.data(), kern.size() * sizeof(double)) == 0;
+    const int old_bw = c->have_params ? c->p.bw : -1;
+    c->p = *p;
     c->p.is_control = nullptr;
     c->p.coeffs = nullptr;
-    c->kern.assign(2 * p->bw + 1, 0.0);
-    up_kernel_weights(p->bw, 1 / p->background, c->kern.data());
-    HIPCHK(c->d_kern.ensure(c->kern.size()));
-    HIPCHK(hipMemcpy(c->d_kern.p, c->kern.data(), c->kern.size() * sizeof(double), hipMemcpyHostToDevice));
-    HIPCHK(c->d_nc.ensure(c->nc.size() + 1));
-    if (!c->nc.empty())
-        HIPCHK(hipMemcpy(c->d_nc.p, c->nc.data(), c->nc.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    HIPCHK(c->d_ctl.ensure(S));
-    HIPCHK(hipMemcpy(c->d_ctl.p, c->ctl.data(), S, hipMemcpyHostToDevice));
-    HIPCHK(c->d_coef.ensure(c->coef.size() + 1));
-    if (!c->coef.empty())
-        HIPCHK(hipMemcpy(c->d_coef.p, c->coef.data(), c->coef.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (!same) {
+        c->ctl = ctl;
+        c->nc = nc;
+        c->coef = coef;
+        c->kern = kern;
+        HIPCHK(c->d_kern.ensure(c->kern.size()));
+        HIPCHK(hipMemcpy(c->d_kern.p, c->kern.data(), c->kern.size() * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(c->d_nc.ensure(c->nc.size() + 1));
+        if (!c->nc.empty())
+            HIPCHK(hipMemcpy(c->d_nc.p, c->nc.data(), c->nc.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        HIPCHK(c->d_ctl.ensure(S));
+        HIPCHK(hipMemcpy(c->d_ctl.p, c->ctl.data(), S, hipMemcpyHostToDevice));
+        HIPCHK(c->d_coef.ensure(c->coef.size() + 1));
+        if (!c->coef.empty())
+            HIPCHK(hipMemcpy(c->d_coef.p, c->coef.data(), c->coef.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
     c->have_params = true;
-    c->units_dirty = true;
+    if (old_bw != p->bw) c->units_dirty = true;
     return UP_OK;
 }
 
@@ -444,7 +456,6 @@ static ScanParams scan_params(up_ctx *c) {
     P.thr = c->p.region_thr;
     P.strip_info = c->d_info.p;
     P.rec = c->d_rec.p;
-    P.strip_lastnz = c->d_lastnz.p;
     P.ovf_count = c->d_ovf_count.p;
     P.ovf_rec = c->d_ovf_rec.p;
     P.ovf_cap = c->ovf_cap;
@@ -545,7 +556,6 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     if ((r = sync_units(c))) return r;
     const uint32_t ns = c->nstrips;
     HIPCHK(c->d_info.ensure(ns));
-    HIPCHK(c->d_lastnz.ensure(ns));
     HIPCHK(c->d_rec.ensure((size_t)ns * 2 * kCap));
     HIPCHK(c->d_cnt.ensure(ns));
     HIPCHK(c->d_off.ensure(ns));
@@ -602,7 +612,8 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     hipLaunchKernelGGL(unit_last_kernel, dim3((unsigned)c->units.size()), dim3(256), 0, c->stream,
-                       c->d_units.p, c->d_lastnz.p, c->d_unit_last.p);
+                       c->d_units.p, (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p,
+                       c->d_unit_last.p);
     HIPCHK(hipGetLastError());
     c->unit_last.resize(c->units.size());
     HIPCHK(hipMemcpyAsync(c->unit_last.data(), c->d_unit_last.p, c->units.size() * 4,

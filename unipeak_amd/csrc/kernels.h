@@ -13,12 +13,14 @@
 namespace upk {
 
 constexpr int kWave = 64;           // CDNA wavefront
-constexpr int kStripWords = 16;     // one strip = 16 words of 64 positions
-constexpr int kStrip = kStripWords * kWave;  // 1024 positions per wave task
+constexpr int kStripWords = 256;    // one strip (wave task) = 256 words of 64 positions
+constexpr int kStrip = kStripWords * kWave;  // 16384 positions per wave task
+constexpr int kStepWords = 16;      // words per register step inside a strip
 constexpr int kPad = 2112;          // 33 words: covers bw <= 2047 halos
 constexpr int kMaxBw = 127;         // register-resident halo: NH <= 2 words
-constexpr int kCap = 8;             // inline run records per strip
-constexpr int kOvfStride = 2 * (kStrip / 2 + 1);  // starts + ends of one strip
+constexpr int kCap = 32;            // inline run records per strip (starts, ends each)
+constexpr int kOvfHalf = kStrip / 2 + 1;  // max starts (= max ends) of one strip
+constexpr int kOvfStride = 2 * kOvfHalf;  // starts + ends of one spilled strip
 
 struct UnitDesc {
     uint64_t base;      // device address of track (0, 0)
@@ -29,13 +31,14 @@ struct UnitDesc {
     int32_t nstrands;   // 1 or 2
 };
 
-// packed per-strip summary written by the scan kernel
-//   bits  0- 9 interior run starts, 10-19 interior run ends,
-//   bit  20 flag(first position), 21 flag(last position),
-//   bit  22 first strip of its unit, 23 last strip of its unit,
-//   bit  24 records spilled to the overflow area
-__host__ __device__ inline uint32_t si_starts(uint32_t v) { return v & 0x3FFu; }
-__host__ __device__ inline uint32_t si_ends(uint32_t v) { return (v >> 10) & 0x3FFu; }
+// packed per-strip summary written by the scan kernel (uint64):
+//   bits  0-15 interior run starts, 16-31 interior run ends,
+//   bit  32 flag(first position), 33 flag(last position),
+//   bit  34 first strip of its unit, 35 last strip of its unit,
+//   bit  36 records spilled to the overflow area
+__host__ __device__ inline uint32_t si_starts(uint64_t v) { return (uint32_t)(v & 0xFFFFu); }
+__host__ __device__ inline uint32_t si_ends(uint64_t v) { return (uint32_t)((v >> 16) & 0xFFFFu); }
+__host__ __device__ inline uint32_t si_bit(uint64_t v, int b) { return (uint32_t)((v >> b) & 1u); }
 
 struct ScanParams {
     const UnitDesc *units;
@@ -48,9 +51,8 @@ struct ScanParams {
     const double *kern; // 2*bw+1 weights
     int32_t bw;
     double thr;
-    uint32_t *strip_info;
+    uint64_t *strip_info;
     uint32_t *rec;          // [nstrips][2*kCap]: starts then ends
-    uint32_t *strip_lastnz; // last position with a pooled hit, 0 if none
     uint32_t *ovf_count;
     uint32_t *ovf_rec;      // [ovf_cap][kOvfStride]
     uint32_t ovf_cap;
@@ -73,7 +75,6 @@ struct StatParams {
     const uint64_t *nreg;
     void *out;            // up_region records
     uint32_t *out_counts; // [n][S]
-    uint32_t *scratch;    // per-wave exptSums accumulators [waves][S]
 };
 
 }  // namespace upk

@@ -49,42 +49,54 @@ __device__ __forceinline__ uint64_t win_mask(int d, int bw) {
     return up & ~((1ull << lo) - 1);
 }
 
+// global-address-space view of a track (plain pointers from the unit table
+// would otherwise compile to flat loads)
+typedef const __attribute__((address_space(1))) uint32_t gu32;
+
+// window word storage: raw counts when the pooled count is the single
+// non-control sample's count, otherwise the FP64 pooled count
+template <int POOL>
+using WinT = typename std::conditional<POOL == 0, uint32_t, double>::type;
+
+__device__ __forceinline__ double rl_cs(uint32_t v, int l) { return (double)rl_u(v, l); }
+__device__ __forceinline__ double rl_cs(double v, int l) { return rl_d(v, l); }
+__device__ __forceinline__ bool nz(uint32_t v) { return v != 0u; }
+__device__ __forceinline__ bool nz(double v) { return v != 0.0; }
+
 // ---- pooled count (ProfileBuffer::add countSum, peakcall.cpp:186-200) ----
 // POOL 0: one non-control sample, no coefficients; 1: several, unscaled;
 // 2: scaled by coefficients plus the unscaled second loop (quirk Q5).
-template <int NWT, int POOL>
-__device__ __forceinline__ void load_pool(double (&cs)[NWT], const uint32_t *strand_base,
-                                          uint64_t stride, int64_t idx0, int lane, int nnc,
-                                          const int32_t *nc, const double *coef) {
-    if (POOL == 0) {
-        const uint32_t *t = strand_base + (uint64_t)nc[0] * stride + idx0 + lane;
-        uint32_t c[NWT];
+// e0 = element index of lane 0 of the first word.
+template <int N, int POOL>
+__device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], gu32 *strand_base, uint64_t stride,
+                                           int64_t e0, int lane, int nnc, const int32_t *nc,
+                                           const double *coef) {
+    if constexpr (POOL == 0) {
+        gu32 *t = strand_base + (uint64_t)nc[0] * stride + e0 + lane;
 #pragma unroll
-        for (int w = 0; w < NWT; ++w) c[w] = __builtin_nontemporal_load(t + 64 * w);
-#pragma unroll
-        for (int w = 0; w < NWT; ++w) cs[w] = (double)c[w];
+        for (int w = 0; w < N; ++w) cs[w] = __builtin_nontemporal_load(t + 64 * w);
     } else {
 #pragma unroll
-        for (int w = 0; w < NWT; ++w) cs[w] = 0.0;
+        for (int w = 0; w < N; ++w) cs[w] = 0.0;
         for (int k = 0; k < nnc; ++k) {
-            const uint32_t *t = strand_base + (uint64_t)nc[k] * stride + idx0 + lane;
-            uint32_t c[NWT];
+            gu32 *t = strand_base + (uint64_t)nc[k] * stride + e0 + lane;
+            uint32_t c[N];
 #pragma unroll
-            for (int w = 0; w < NWT; ++w) c[w] = __builtin_nontemporal_load(t + 64 * w);
-            if (POOL == 1) {
+            for (int w = 0; w < N; ++w) c[w] = __builtin_nontemporal_load(t + 64 * w);
+            if constexpr (POOL == 1) {
 #pragma unroll
-                for (int w = 0; w < NWT; ++w) cs[w] = cs[w] + (double)c[w];
+                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w];
             } else {
                 const double q = coef[k];
 #pragma unroll
-                for (int w = 0; w < NWT; ++w) cs[w] = cs[w] + (double)c[w] * q;
+                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w] * q;
             }
         }
-        if (POOL == 2) {
+        if constexpr (POOL == 2) {
             for (int k = 0; k < nnc; ++k) {
-                const uint32_t *t = strand_base + (uint64_t)nc[k] * stride + idx0 + lane;
+                gu32 *t = strand_base + (uint64_t)nc[k] * stride + e0 + lane;
 #pragma unroll
-                for (int w = 0; w < NWT; ++w) cs[w] = cs[w] + (double)t[64 * w];
+                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)t[64 * w];
             }
         }
     }
@@ -92,8 +104,8 @@ __device__ __forceinline__ void load_pool(double (&cs)[NWT], const uint32_t *str
 
 // KDE value of lane's position in output word K: ascending walk over the
 // hits of words K-NH..K+NH (window-masked).  K must be a compile-time index.
-template <int NWT, int NH, int K>
-__device__ __forceinline__ double kde_word(const double (&cs)[NWT], const uint64_t (&hm)[NWT],
+template <int NWT, int NH, int K, typename T>
+__device__ __forceinline__ double kde_word(const T (&cs)[NWT], const uint64_t (&hm)[NWT],
                                            const uint64_t (&wm)[2 * NH + 1], int lane, int bw,
                                            const double *ktab) {
     double f = 0.0;
@@ -103,7 +115,7 @@ __device__ __forceinline__ double kde_word(const double (&cs)[NWT], const uint64
         while (m) {
             const int b = __builtin_ctzll(m);
             m &= m - 1;
-            const double c = rl_d(cs[K + d], b);
+            const double c = rl_cs(cs[K + d], b);
             const int idx = lane + (bw - 64 * d - b);
             if ((unsigned)idx <= (unsigned)(2 * bw)) f = f + ktab[idx] * c;
         }
@@ -112,22 +124,30 @@ __device__ __forceinline__ double kde_word(const double (&cs)[NWT], const uint64
 }
 
 template <int NWT, int NH, int K>
+__device__ __forceinline__ uint64_t any_hits(const uint64_t (&hm)[NWT], const uint64_t (&wm)[2 * NH + 1]) {
+    uint64_t a = 0;
+#pragma unroll
+    for (int d = -NH; d <= NH; ++d) a |= hm[K + d] & wm[d + NH];
+    return a;
+}
+
+template <int K0, int K1>
 struct WordLoop {
     template <typename F>
     __device__ __forceinline__ static void run(F &&fn) {
-        WordLoop<NWT, NH, K - 1>::run(fn);
-        fn(std::integral_constant<int, K>());
+        fn(std::integral_constant<int, K0>());
+        WordLoop<K0 + 1, K1>::run(fn);
     }
 };
-template <int NWT, int NH>
-struct WordLoop<NWT, NH, NH - 1> {
+template <int K1>
+struct WordLoop<K1, K1> {
     template <typename F>
     __device__ __forceinline__ static void run(F &&) {}
 };
 
 __device__ __forceinline__ uint32_t find_unit(const UnitDesc *units, uint32_t nunits,
                                               uint32_t strip) {
-    uint32_t lo = 0, hi = nunits;  // first unit with strip0 > strip, minus one
+    uint32_t lo = 0, hi = nunits;  // last unit with strip0 <= strip
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (units[mid].strip0 <= strip) lo = mid; else hi = mid;
@@ -135,8 +155,73 @@ __device__ __forceinline__ uint32_t find_unit(const UnitDesc *units, uint32_t nu
     return lo;
 }
 
+// run-boundary record list of one strip: kCap inline starts/ends, spilled
+// to an overflow slot (kOvfHalf each) by lane 0 when either list fills
+struct RecList {
+    uint32_t *st, *en;
+    uint32_t ns, ne, cap;
+    bool spilled, lost;
+};
+
+__device__ __forceinline__ void rec_spill(RecList &R, const ScanParams &P, uint32_t *inline_base,
+                                          int lane) {
+    uint32_t slot = 0;
+    if (lane == 0) slot = atomicAdd(P.ovf_count, 1u);
+    slot = rl_u(slot, 0);
+    R.spilled = true;
+    if (slot >= P.ovf_cap) {  // host grows the area and reruns
+        R.lost = true;
+        if (lane == 0) inline_base[0] = slot;
+        return;
+    }
+    uint32_t *dst = P.ovf_rec + (uint64_t)slot * kOvfStride;
+    if (lane == 0) {  // same lane wrote the inline records: program order suffices
+        for (uint32_t i = 0; i < R.ns; ++i) dst[i] = R.st[i];
+        for (uint32_t i = 0; i < R.ne; ++i) dst[kOvfHalf + i] = R.en[i];
+        inline_base[0] = slot;
+    }
+    R.st = dst;
+    R.en = dst + kOvfHalf;
+    R.cap = kOvfHalf;
+}
+
+__device__ __forceinline__ void rec_push(RecList &R, bool start, uint32_t pos, const ScanParams &P,
+                                         uint32_t *inline_base, int lane) {
+    uint32_t &n = start ? R.ns : R.ne;
+    if (n == R.cap && !R.spilled) rec_spill(R, P, inline_base, lane);
+    if (!R.lost && lane == 0) (start ? R.st : R.en)[n] = pos;
+    ++n;
+}
+
+// scatter one hit (window word W, bit b, pooled count c) into the register
+// accumulators of the output words it can reach: branch-free, predicated
+// per lane, so the only scalar work per hit is the bit walk itself
+template <int NH, int SW, int W, typename A>
+__device__ __forceinline__ void scatter_hit(A (&acc)[SW], int b, double c, int lane, int bw,
+                                            const double *ktab) {
+    WordLoop<W - NH, W + NH + 1>::run([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        if constexpr (t >= NH && t < NH + SW) {
+            // output word t-NH, lane position 64(t-NH)+lane; hit at 64(W-NH)+b
+            const int idx = lane + bw - b + 64 * (t - W);
+            const bool in = (unsigned)idx <= (unsigned)(2 * bw);
+            const int ci = in ? idx : 0;
+            const double v = acc[t - NH] + ktab[ci] * c;
+            acc[t - NH] = in ? v : acc[t - NH];
+        }
+    });
+}
+
 // ------------------------------------------------------------------------
-// K1: one wave per 1024-position strip (grid-stride).
+// K1: one wave streams one 16384-position strip of a unit through a
+// register window of 16 + 2*NH words (64 positions each), one step of 16
+// words at a time, with the next step's counts prefetched (POOL 0) while
+// the current step is scored.  Halo words are carried between steps, so
+// every count is read from HBM once (plus 2*NH words per strip).
+// Scalar work per step is the walk over hit bits plus one flag test: each
+// hit is scattered (in ascending position order, so every position's sum
+// keeps the reference's order) into FP64 accumulators of the words it
+// reaches; run boundaries are only derived for steps holding a flag.
 // ------------------------------------------------------------------------
 template <int NH, int POOL, bool NONDIR, bool PROF>
 __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_begin,
@@ -146,15 +231,20 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
     for (int i = threadIdx.x; i <= 2 * bw; i += blockDim.x) ktab[i] = P.kern[i];
     __syncthreads();
 
-    constexpr int NW = kStripWords;
-    constexpr int NWT = NW + 2 * NH;
+    constexpr int SW = kStepWords;
+    constexpr int NWIN = SW + 2 * NH;
+    constexpr int NSTEP = kStripWords / SW;
+    using T = WinT<POOL>;
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-
-    uint64_t wm[2 * NH + 1];
+    // halo words only matter where they reach an output word
+    uint64_t edge_lo[NH], edge_hi[NH];
 #pragma unroll
-    for (int d = -NH; d <= NH; ++d) wm[d + NH] = win_mask(d, bw);
+    for (int i = 0; i < NH; ++i) {
+        edge_lo[i] = win_mask(i - NH, bw);  // window word i vs output word 0
+        edge_hi[i] = win_mask(i + 1, bw);   // window word NH+SW+i vs output word SW-1
+    }
 
     uint32_t cur = 0;
     bool have = false;
@@ -164,121 +254,178 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
         const UnitDesc U = P.units[cur];
         const uint32_t local = strip - U.strip0;
         const int64_t p0 = 1 + (int64_t)local * kStrip;  // first position of the strip
-        const int64_t idx0 = kPad + p0 - 1 - 64 * NH;     // element of word 0 (halo)
-        const uint32_t *base = (const uint32_t *)U.base;
-        const uint64_t sstride = (uint64_t)P.S * U.stride;
+        const int64_t e0 = kPad + p0 - 1;                 // element of strip word 0, lane 0
+        gu32 *fb = (gu32 *)U.base;
+        gu32 *rb = fb + (uint64_t)P.S * U.stride;
 
-        double cf[NWT];
-        uint64_t hf[NWT];
-        load_pool<NWT, POOL>(cf, base, U.stride, idx0, lane, P.nnc, P.nc, P.coef);
+        T wf[NWIN], wr[NONDIR ? NWIN : 1];
+        uint64_t hf[NWIN], hr[NONDIR ? NWIN : 1];
+        load_words<NWIN, POOL>(wf, fb, U.stride, e0 - 64 * NH, lane, P.nnc, P.nc, P.coef);
+        if constexpr (NONDIR)
+            load_words<NWIN, POOL>(wr, rb, U.stride, e0 - 64 * NH, lane, P.nnc, P.nc, P.coef);
 #pragma unroll
-        for (int w = 0; w < NWT; ++w) hf[w] = __ballot(cf[w] != 0.0);
-        double cr[NONDIR ? NWT : 1];
-        uint64_t hr[NONDIR ? NWT : 1];
-        if constexpr (NONDIR) {
-            load_pool<NWT, POOL>(cr, base + sstride, U.stride, idx0, lane, P.nnc, P.nc, P.coef);
-#pragma unroll
-            for (int w = 0; w < NWT; ++w) hr[w] = __ballot(cr[w] != 0.0);
+        for (int w = 0; w < NWIN; ++w) {
+            hf[w] = __ballot(nz(wf[w]));
+            if constexpr (NONDIR) hr[w] = __ballot(nz(wr[w]));
         }
 
-        uint64_t F[NW];
-        WordLoop<NWT, NH, NH + NW - 1>::run([&](auto kc) {
-            constexpr int K = decltype(kc)::value;
-            double s = kde_word<NWT, NH, K>(cf, hf, wm, lane, bw, ktab);
-            double r = 0.0;
-            if constexpr (NONDIR) {
-                r = kde_word<NWT, NH, K>(cr, hr, wm, lane, bw, ktab);
-                if constexpr (PROF) {
-                    const int64_t p = p0 + 64 * (K - NH) + lane;
-                    if (p <= P.prof_len) { P.prof_f[p - 1] = s; P.prof_r[p - 1] = r; }
+        uint32_t *inl = P.rec + (uint64_t)strip * (2 * kCap);
+        RecList R{inl, inl + kCap, 0, 0, (uint32_t)kCap, false, false};
+        uint64_t prevF = 0, F0 = 0;
+
+        for (int j = 0; j < NSTEP; ++j) {
+            const bool more = j + 1 < NSTEP;
+            const int64_t enext = e0 + 64 * ((j + 1) * SW + NH);  // first new word of step j+1
+            T nf[POOL == 0 ? SW : 1], nr[(POOL == 0 && NONDIR) ? SW : 1];
+            if constexpr (POOL == 0) {
+                if (more) {
+                    load_words<SW, 0>(nf, fb, U.stride, enext, lane, P.nnc, P.nc, P.coef);
+                    if constexpr (NONDIR)
+                        load_words<SW, 0>(nr, rb, U.stride, enext, lane, P.nnc, P.nc, P.coef);
                 }
-                s = s + r;  // processPosition: forwardScore + reverseScore
-            } else if constexpr (PROF) {
-                const int64_t p = p0 + 64 * (K - NH) + lane;
-                if (p <= P.prof_len) { P.prof_f[p - 1] = s; P.prof_r[p - 1] = 0.0; }
             }
-            F[K - NH] = __ballot(s >= P.thr);
-        });
+            // ---- KDE: scatter every hit of the window, ascending ----
+            double af[SW], ar[NONDIR ? SW : 1];
+#pragma unroll
+            for (int k = 0; k < SW; ++k) {
+                af[k] = 0.0;
+                if constexpr (NONDIR) ar[k] = 0.0;
+            }
+            WordLoop<0, NWIN>::run([&](auto wc) {
+                constexpr int W = decltype(wc)::value;
+                uint64_t m = hf[W];
+                if constexpr (W < NH) m &= edge_lo[W];
+                if constexpr (W >= NH + SW) m &= edge_hi[W - NH - SW];
+                while (m) {
+                    const int b = __builtin_ctzll(m);
+                    m &= m - 1;
+                    scatter_hit<NH, SW, W>(af, b, rl_cs(wf[W], b), lane, bw, ktab);
+                }
+                if constexpr (NONDIR) {
+                    uint64_t q = hr[W];
+                    if constexpr (W < NH) q &= edge_lo[W];
+                    if constexpr (W >= NH + SW) q &= edge_hi[W - NH - SW];
+                    while (q) {
+                        const int b = __builtin_ctzll(q);
+                        q &= q - 1;
+                        scatter_hit<NH, SW, W>(ar, b, rl_cs(wr[W], b), lane, bw, ktab);
+                    }
+                }
+            });
+            double sc[SW];
+            double mx = -__builtin_inf();
+#pragma unroll
+            for (int k = 0; k < SW; ++k) {
+                if constexpr (NONDIR) sc[k] = af[k] + ar[k];  // forwardScore + reverseScore
+                else sc[k] = af[k];
+                mx = __builtin_fmax(mx, sc[k]);
+            }
+            if constexpr (PROF) {
+#pragma unroll
+                for (int k = 0; k < SW; ++k) {
+                    const int64_t p = p0 + 64 * (j * SW + k) + lane;
+                    if (p <= P.prof_len) {
+                        P.prof_f[p - 1] = af[k];
+                        if constexpr (NONDIR) P.prof_r[p - 1] = ar[k];
+                    }
+                }
+            } else {
+                // ---- flags and run boundaries (only steps touching a run) ----
+                const uint64_t anyflag = __ballot(mx >= P.thr);
+                if (anyflag | prevF) {
+#pragma unroll
+                    for (int k = 0; k < SW; ++k) {
+                        const uint64_t F = __ballot(sc[k] >= P.thr);
+                        const int64_t wpos = p0 + 64 * (j * SW + k);
+                        uint64_t st;
+                        if (j == 0 && k == 0) {
+                            F0 = F;
+                            st = F & ~((F << 1) | 1ull);  // no interior start at p0
+                        } else {
+                            st = F & ~((F << 1) | (prevF >> 63));
+                            uint64_t en = prevF & ~((prevF >> 1) | ((F & 1ull) << 63));
+                            while (en) {
+                                const int b = __builtin_ctzll(en);
+                                en &= en - 1;
+                                rec_push(R, false, (uint32_t)(wpos - 64 + b), P, inl, lane);
+                            }
+                        }
+                        while (st) {
+                            const int b = __builtin_ctzll(st);
+                            st &= st - 1;
+                            rec_push(R, true, (uint32_t)(wpos + b), P, inl, lane);
+                        }
+                        prevF = F;
+                    }
+                }
+            }
+            if (more) {
+#pragma unroll
+                for (int w = 0; w < 2 * NH; ++w) {
+                    wf[w] = wf[SW + w];
+                    hf[w] = hf[SW + w];
+                    if constexpr (NONDIR) { wr[w] = wr[SW + w]; hr[w] = hr[SW + w]; }
+                }
+                if constexpr (POOL == 0) {
+#pragma unroll
+                    for (int w = 0; w < SW; ++w) {
+                        wf[2 * NH + w] = nf[w];
+                        if constexpr (NONDIR) wr[2 * NH + w] = nr[w];
+                    }
+                } else {
+                    T t[SW];
+                    load_words<SW, POOL>(t, fb, U.stride, enext, lane, P.nnc, P.nc, P.coef);
+#pragma unroll
+                    for (int w = 0; w < SW; ++w) wf[2 * NH + w] = t[w];
+                    if constexpr (NONDIR) {
+                        load_words<SW, POOL>(t, rb, U.stride, enext, lane, P.nnc, P.nc, P.coef);
+#pragma unroll
+                        for (int w = 0; w < SW; ++w) wr[2 * NH + w] = t[w];
+                    }
+                }
+#pragma unroll
+                for (int w = 2 * NH; w < NWIN; ++w) {
+                    hf[w] = __ballot(nz(wf[w]));
+                    if constexpr (NONDIR) hr[w] = __ballot(nz(wr[w]));
+                }
+            }
+        }
         if constexpr (PROF) continue;
-
-        // interior run boundaries (a start at p0 / an end at p0+1023 depends
-        // on the neighbour strip and is resolved in K2)
-        uint32_t ns = 0, ne = 0;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-            const uint64_t prevb = k == 0 ? 1ull : (F[k - 1] >> 63);
-            const uint64_t nextb = k == NW - 1 ? 1ull : (F[k + 1] & 1ull);
-            ns += __builtin_popcountll(F[k] & ~((F[k] << 1) | prevb));
-            ne += __builtin_popcountll(F[k] & ~((F[k] >> 1) | (nextb << 63)));
-        }
-        uint32_t info = ns | (ne << 10) | ((uint32_t)(F[0] & 1ull) << 20) |
-                        ((uint32_t)(F[NW - 1] >> 63) << 21) | ((local == 0) << 22) |
-                        ((local + 1 == U.nstrips) << 23);
-        uint32_t *dst = P.rec + (uint64_t)strip * (2 * kCap);
-        uint32_t so = 0, eo = kCap;
-        if (ns > kCap || ne > kCap) {
-            uint32_t slot = 0;
-            if (lane == 0) slot = atomicAdd(P.ovf_count, 1u);
-            slot = rl_u(slot, 0);
-            if (lane == 0) dst[0] = slot;
-            info |= 1u << 24;
-            dst = slot < P.ovf_cap ? P.ovf_rec + (uint64_t)slot * kOvfStride : nullptr;
-            eo = kStrip / 2 + 1;
-        }
-        if ((ns | ne) && dst) {
-#pragma unroll
-            for (int k = 0; k < NW; ++k) {
-                const uint64_t prevb = k == 0 ? 1ull : (F[k - 1] >> 63);
-                const uint64_t nextb = k == NW - 1 ? 1ull : (F[k + 1] & 1ull);
-                uint64_t st = F[k] & ~((F[k] << 1) | prevb);
-                uint64_t en = F[k] & ~((F[k] >> 1) | (nextb << 63));
-                while (st) {
-                    const int b = __builtin_ctzll(st);
-                    st &= st - 1;
-                    if (lane == 0) dst[so] = (uint32_t)(p0 + 64 * k + b);
-                    ++so;
-                }
-                while (en) {
-                    const int b = __builtin_ctzll(en);
-                    en &= en - 1;
-                    if (lane == 0) dst[eo] = (uint32_t)(p0 + 64 * k + b);
-                    ++eo;
-                }
+        {   // ends of the last word (no interior end at the strip's last position)
+            uint64_t en = prevF & ~((prevF >> 1) | (1ull << 63));
+            const int64_t wpos = p0 + kStrip - 64;
+            while (en) {
+                const int b = __builtin_ctzll(en);
+                en &= en - 1;
+                rec_push(R, false, (uint32_t)(wpos + b), P, inl, lane);
             }
         }
-        // last position with a pooled hit (an add() with countSum != 0)
-        uint32_t lastnz = 0;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-            uint64_t h = hf[NH + k];
-            if constexpr (NONDIR) h |= hr[NH + k];
-            if (h) lastnz = (uint32_t)(p0 + 64 * k + 63 - __builtin_clzll(h));
-        }
-        if (lane == 0) {
-            P.strip_info[strip] = info;
-            P.strip_lastnz[strip] = lastnz;
-        }
+        const uint64_t info = (uint64_t)R.ns | ((uint64_t)R.ne << 16) | ((F0 & 1ull) << 32) |
+                              ((prevF >> 63) << 33) | ((uint64_t)(local == 0) << 34) |
+                              ((uint64_t)(local + 1 == U.nstrips) << 35) |
+                              ((uint64_t)R.spilled << 36);
+        if (lane == 0) P.strip_info[strip] = info;
     }
 }
 
 // ------------------------------------------------------------------------
 // K2a: resolve strip-boundary starts/ends, pack (starts, ends) as uint64
 // ------------------------------------------------------------------------
-__global__ void finalize_kernel(const uint32_t *__restrict__ info, uint64_t *__restrict__ cnt,
+__global__ void finalize_kernel(const uint64_t *__restrict__ info, uint64_t *__restrict__ cnt,
                                 uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t v = info[i];
-    const uint32_t prev_last = (v >> 22) & 1 ? 0 : (info[i - 1] >> 21) & 1;
-    const uint32_t next_first = (v >> 23) & 1 ? 0 : (info[i + 1] >> 20) & 1;
-    const uint32_t xs = ((v >> 20) & 1) & !prev_last;
-    const uint32_t xe = ((v >> 21) & 1) & !next_first;
+    const uint64_t v = info[i];
+    const uint32_t prev_last = si_bit(v, 34) ? 0u : si_bit(info[i - 1], 33);
+    const uint32_t next_first = si_bit(v, 35) ? 0u : si_bit(info[i + 1], 32);
+    const uint32_t xs = si_bit(v, 32) & (prev_last ^ 1u);
+    const uint32_t xe = si_bit(v, 33) & (next_first ^ 1u);
     cnt[i] = (uint64_t)(si_starts(v) + xs) | ((uint64_t)(si_ends(v) + xe) << 32);
 }
 
 // K2c: compaction of run boundaries into region lists
 __global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
-                               const uint32_t *__restrict__ info, const uint64_t *__restrict__ cnt,
+                               const uint64_t *__restrict__ info, const uint64_t *__restrict__ cnt,
                                const uint64_t *__restrict__ off, const uint32_t *__restrict__ rec,
                                const uint32_t *__restrict__ ovf_rec, uint32_t ovf_cap,
                                uint32_t *__restrict__ starts, uint32_t *__restrict__ ends,
@@ -287,7 +434,7 @@ __global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
     if (i >= n) return;
     const uint64_t c = cnt[i];
     if (c == 0) return;
-    const uint32_t v = info[i];
+    const uint64_t v = info[i];
     const uint32_t ns = (uint32_t)c, ne = (uint32_t)(c >> 32);
     const uint32_t xs = ns - si_starts(v), xe = ne - si_ends(v);
     const uint64_t o = off[i];
@@ -296,11 +443,11 @@ __global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
     const int64_t p0 = 1 + (int64_t)(i - units[u].strip0) * kStrip;
     const uint32_t *src = rec + (uint64_t)i * (2 * kCap);
     uint32_t eoff = kCap;
-    if ((v >> 24) & 1) {
+    if (si_bit(v, 36)) {
         const uint32_t slot = src[0];
-        if (slot >= ovf_cap) return;  // reported by the host as overflow
+        if (slot >= ovf_cap) return;  // host grows the area and reruns
         src = ovf_rec + (uint64_t)slot * kOvfStride;
-        eoff = kStrip / 2 + 1;
+        eoff = kOvfHalf;
     }
     if (xs) { starts[os] = (uint32_t)p0; reg_unit[os] = u; ++os; }
     for (uint32_t k = 0; k < si_starts(v); ++k) { starts[os] = src[k]; reg_unit[os] = u; ++os; }
@@ -308,24 +455,27 @@ __global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
     if (xe) ends[oe++] = (uint32_t)(p0 + kStrip - 1);
 }
 
-// per-unit last add: max over the unit's strips
-__global__ void unit_last_kernel(const UnitDesc *units, const uint32_t *__restrict__ lastnz,
+// per-unit last add (the last position whose pooled count is nonzero):
+// one workgroup per unit scans its tracks backwards from the contig end
+__global__ void unit_last_kernel(const UnitDesc *units, int S, int nnc, const int32_t *nc,
                                  uint32_t *__restrict__ out) {
     const UnitDesc U = units[blockIdx.x];
-    uint32_t m = 0;
-    for (uint32_t s = threadIdx.x; s < U.nstrips; s += blockDim.x) {
-        const uint32_t v = lastnz[U.strip0 + s];
-        m = v > m ? v : m;
-    }
-    __shared__ uint32_t red[256];
-    red[threadIdx.x] = m;
+    __shared__ uint32_t found;
+    if (threadIdx.x == 0) found = 0;
     __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-        if ((int)threadIdx.x < k && red[threadIdx.x + k] > red[threadIdx.x])
-            red[threadIdx.x] = red[threadIdx.x + k];
+    for (int64_t hi = U.len; hi >= 1; hi -= blockDim.x) {
+        const int64_t p = hi - threadIdx.x;
+        uint32_t any = 0;
+        if (p >= 1)
+            for (int st = 0; st < U.nstrands; ++st)
+                for (int k = 0; k < nnc; ++k)
+                    any |= ((const uint32_t *)U.base)[((uint64_t)st * S + nc[k]) * U.stride + kPad + p - 1];
+        if (any) atomicMax(&found, (uint32_t)p);
+        __syncthreads();
+        if (found) break;
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+    if (threadIdx.x == 0) out[blockIdx.x] = found;
 }
 
 // ------------------------------------------------------------------------
@@ -339,13 +489,13 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 
 // pooled counts of the 2NH+1 words around block start x0 for one strand
 template <int NH, int POOL>
-__device__ __forceinline__ void region_words(double (&cs)[2 * NH + 1], uint64_t (&hm)[2 * NH + 1],
+__device__ __forceinline__ void region_words(WinT<POOL> (&cs)[2 * NH + 1], uint64_t (&hm)[2 * NH + 1],
                                              const uint32_t *strand_base, uint64_t stride,
                                              int64_t x0, int lane, const StatParams &P) {
     const int64_t idx0 = kPad + x0 - 1 - 64 * NH;
-    load_pool<2 * NH + 1, POOL>(cs, strand_base, stride, idx0, lane, P.nnc, P.nc, P.coef);
+    load_words<2 * NH + 1, POOL>(cs, (gu32 *)strand_base, stride, idx0, lane, P.nnc, P.nc, P.coef);
 #pragma unroll
-    for (int w = 0; w < 2 * NH + 1; ++w) hm[w] = __ballot(cs[w] != 0.0);
+    for (int w = 0; w < 2 * NH + 1; ++w) hm[w] = __ballot(nz(cs[w]));
 }
 
 template <int NH, int POOL, bool NONDIR>
@@ -380,13 +530,13 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             const int64_t x = x0 + lane;
             const bool valid = x <= (int64_t)right;
             const int nvalid = (int)(((int64_t)right - x0 + 1) < 64 ? ((int64_t)right - x0 + 1) : 64);
-            double cf[NWT];
+            WinT<POOL> cf[NWT];
             uint64_t hf[NWT];
             region_words<NH, POOL>(cf, hf, base, U.stride, x0, lane, P);
             double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
             double r = 0.0;
             uint64_t hr_c = 0;
-            double cr[NONDIR ? NWT : 1];
+            WinT<POOL> cr[NONDIR ? NWT : 1];
             uint64_t hr[NONDIR ? NWT : 1];
             if constexpr (NONDIR) {
                 region_words<NH, POOL>(cr, hr, base + sstride, U.stride, x0, lane, P);
@@ -495,7 +645,7 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             double ss1 = 0.0, ss2 = 0.0, ssr = 0.0;
             for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
                 const int nvalid = (int)(((int64_t)right - x0 + 1) < 64 ? ((int64_t)right - x0 + 1) : 64);
-                double cf[NWT], cr[NWT];
+                WinT<POOL> cf[NWT], cr[NWT];
                 uint64_t hf[NWT], hr[NWT];
                 region_words<NH, POOL>(cf, hf, base, U.stride, x0, lane, P);
                 region_words<NH, POOL>(cr, hr, base + sstride, U.stride, x0, lane, P);
@@ -571,7 +721,7 @@ __global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t 
         const uint32_t len = right - left + 1;
         double *fs = slab + slab_off[j], *rs = fs + len;
         for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
-            double cf[NWT], cr[NWT];
+            WinT<POOL> cf[NWT], cr[NWT];
             uint64_t hf[NWT], hr[NWT];
             region_words<NH, POOL>(cf, hf, base, U.stride, x0, lane, P);
             region_words<NH, POOL>(cr, hr, base + sstride, U.stride, x0, lane, P);
