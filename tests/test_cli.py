@@ -1,0 +1,152 @@
+"""Drop-in parity of the C++ CLIs (bin/) with the oracle's restatement of the
+reference CLIs: byte-identical region tables, strand_shift reports and
+tags_in_regions tables on seeded synthetic wiggle inputs.
+
+bin/regions and bin/strand_shift need the GPU (gpu marker);
+bin/tags_in_regions is host-only and runs on CPU."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.wig import write_contigs, write_wig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "bin")
+
+
+def gen_sample(rng, contigs, lo=300, n_bg=None, n_cl=None, shift_rev=0, sd=60):
+    """{contig: [(pos, count)]} for both strands, positions >= lo."""
+    fwd, rev = {}, {}
+    for name, L in contigs:
+        for strand, d in ((0, fwd), (1, rev)):
+            hi = L - 300
+            dense = {}
+            nb = max(1, (hi - lo) // 400) if n_bg is None else n_bg
+            for p in rng.integers(lo, hi, nb):
+                dense[int(p)] = dense.get(int(p), 0) + int(rng.integers(1, 3))
+            nc = max(1, (hi - lo) // 6000) if n_cl is None else n_cl
+            for _ in range(nc):
+                c = int(rng.integers(lo + 200, hi - 200)) + (shift_rev if strand else 0)
+                for o in np.rint(rng.normal(0, sd, int(rng.integers(20, 150)))).astype(int):
+                    p = c + int(o)
+                    if lo <= p <= hi:
+                        dense[p] = dense.get(p, 0) + 1
+            if dense:
+                d[name] = sorted(dense.items())
+    return fwd, rev
+
+
+def make_inputs(tmp_path, seed, contigs, nsamples, **kw):
+    rng = np.random.default_rng(seed)
+    ct = tmp_path / "contigs.txt"
+    write_contigs(ct, contigs)
+    files = []
+    for i in range(nsamples):
+        fwd, rev = gen_sample(rng, contigs, **kw)
+        p = tmp_path / f"s{i}.wig"
+        write_wig(p, f"s{i}", fwd, rev)
+        files.append(str(p))
+    return str(ct), files
+
+
+def run(cmd, cwd):
+    r = subprocess.run(cmd, cwd=cwd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise AssertionError(f"{cmd[0]} failed ({r.returncode}):\n{r.stderr[-2000:]}")
+    return r
+
+
+def compare_tool(orc_bin, tmp_path, tool, args, outname="out.txt"):
+    ref = tmp_path / ("ref_" + outname)
+    got = tmp_path / ("got_" + outname)
+    run([orc_bin, tool] + args + ["-o", str(ref)], tmp_path)
+    run([os.path.join(BIN, tool)] + args + ["-o", str(got)], tmp_path)
+    a, b = ref.read_bytes(), got.read_bytes()
+    assert a == b, f"{tool} output differs\n--- oracle\n{a[:3000].decode()}\n--- bin\n{b[:3000].decode()}"
+    return a.decode()
+
+
+HG_LIKE = [("chrA", 60_000), ("chrB", 45_000), ("chrC", 30_000)]
+
+REGION_CASES = [
+    ("directional_basic", HG_LIKE, 1, ["-f"], {}),
+    ("directional_k5_r10", HG_LIKE, 1, ["-f", "-k", "5", "-r", "10", "-t", "3"], {}),
+    ("one_contig_interleave_q4", [("chrX", 80_000)], 1, ["-f"], {}),
+    ("controls_prop_coeffs", HG_LIKE, 3, ["-f", "-e", "3", "-z", "p"], {}),
+    ("explicit_coeffs_q6", HG_LIKE, 3, ["-e", "2", "-z", "0.7,1.3"], {}),
+    ("bandwidth_20", HG_LIKE, 2, ["-f", "-b", "20"], {}),
+    ("bandwidth_100", HG_LIKE, 1, ["-f", "-b", "100", "-k", "0"], {}),
+    ("nondir_corr", HG_LIKE, 1, ["-D", "-y", "-f", "-s", "60"], {"shift_rev": 120}),
+    ("nondir_two_samples", HG_LIKE, 2, ["-D", "-y", "-u", "0.5"], {"shift_rev": 100}),
+    ("mappable_override", HG_LIKE, 1, ["-f", "-m", "3095693983"], {}),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", REGION_CASES, ids=lambda c: c[0])
+def test_regions_cli_matches_oracle(orc_bin, gpu_lib, tmp_path, case):
+    name, contigs, ns, args, kw = case
+    ct, files = make_inputs(tmp_path, abs(hash(name)) % 10_000, contigs, ns, **kw)
+    out = compare_tool(orc_bin, tmp_path, "regions", ["-q", "-c", ct] + args + files)
+    assert out.count("\n") > 15
+
+
+@pytest.mark.gpu
+def test_regions_cli_survey_kat(orc_bin, gpu_lib, tmp_path):
+    """Q7 known answer (reference run recorded in SURVEY.md) through bin/regions."""
+    write_contigs(tmp_path / "ct.txt", [("chrA", 10000)])
+    write_wig(tmp_path / "s1.wig", "s1", {"chrA": [(1000, 10)]}, {})
+    write_wig(tmp_path / "c1.wig", "c1", {"chrA": [(1005, 7)]}, {})
+    out = compare_tool(orc_bin, tmp_path, "regions",
+                       ["-q", "-f", "-k", "0", "-e", "2", "-m", "1000", "-c", "ct.txt",
+                        "s1.wig", "c1.wig"])
+    assert out.rstrip().split("\n")[-1] == "chrA:980-1020\t1000\t-nan\t10\t0"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+def test_strand_shift_cli_matches_oracle(orc_bin, gpu_lib, tmp_path, seed):
+    contigs = [("chrA", 200_000), ("chrB", 150_000)]
+    ct, files = make_inputs(tmp_path, seed, contigs, 1, shift_rev=150, n_cl=40, sd=90)
+    out = compare_tool(orc_bin, tmp_path, "strand_shift",
+                       ["-c", ct, "-x", "100", "-n", "10", "-u", "0", "-g", "50"] + files)
+    assert "# best_shift=" in out
+
+
+def test_tags_in_regions_cli_matches_oracle(orc_bin, tmp_path):
+    """host-only: build a region table with the oracle, then count 2 extra samples."""
+    ct, files = make_inputs(tmp_path, 5, HG_LIKE, 3)
+    regions = tmp_path / "regions.txt"
+    run([orc_bin, "regions", "-q", "-f", "-c", ct, "-o", str(regions), files[0]], tmp_path)
+    for extra in (["-e", "30"], []):
+        compare_tool(orc_bin, tmp_path, "tags_in_regions",
+                     ["-c", ct, "-f", str(regions)] + extra + files[1:])
+    # nondirectional input table
+    nd = tmp_path / "nd.txt"
+    run([orc_bin, "regions", "-q", "-D", "-c", ct, "-o", str(nd), files[0]], tmp_path)
+    compare_tool(orc_bin, tmp_path, "tags_in_regions", ["-D", "-c", ct, "-f", str(nd)] + files[1:],
+                 outname="nd_out.txt")
+
+
+def test_tags_in_regions_q12_reverse_mislabel(orc_bin, tmp_path):
+    """Q12: a forward-labelled reverse region counts 0 (no strand check in the
+    count loop; survey probe `chrA:5011-5162 55 0`)."""
+    write_contigs(tmp_path / "ct.txt", [("chrA", 20000)])
+    write_wig(tmp_path / "a.wig", "a", {}, {"chrA": [(5100, 30), (8000, 30)]})
+    (tmp_path / "r.txt").write_text("# x\n\tkurtosis\ta\nchrA:5011-5162\t1.00\t30\n"
+                                    "chrA:8060-7940\t1.00\t30\n")
+    out = compare_tool(orc_bin, tmp_path, "tags_in_regions",
+                       ["-c", "ct.txt", "-f", "r.txt", "a.wig"])
+    rows = [l.split("\t") for l in out.strip().split("\n") if not l.startswith(("#", "\t"))]
+    # the forward-labelled region skips (and so consumes) the reverse tags
+    assert rows[0][-1] == "0" and rows[1][-1] == "0"
+
+
+def test_cli_usage_errors(tmp_path):
+    for tool in ("regions", "strand_shift", "tags_in_regions"):
+        r = subprocess.run([os.path.join(BIN, tool)], capture_output=True, text=True)
+        assert r.returncode == 1 and r.stderr.startswith("error: ")
+    r = subprocess.run([os.path.join(BIN, "regions"), "--version"], capture_output=True, text=True)
+    assert r.returncode == 0 and "1.0" in r.stdout

@@ -1,0 +1,44 @@
+// unipeak_amd/host/cli.hpp -- the reference CLIs' flag tables (TCLAP in the
+// reference: src/regions.cpp:53-75, src/strand_shift.cpp:52-68,
+// src/tags_in_regions.cpp:36-46).  Accepts "-x value", "--long value",
+// combined short switches ("-qD"), "--" and trailing positional files;
+// parse errors print "error: <msg> for arg <id>" and exit 1 like
+// src/regions.cpp:99-101.  --help / --version print and exit 0.
+#pragma once
+
+#include <cstdint>
+
+#include <string>
+#include <vector>
+
+namespace unipeak {
+
+struct Flag {
+    std::string s, l;   // short and long names
+    bool is_switch;
+    bool required;
+    bool seen = false;
+    std::string value;
+};
+
+class ArgParser {
+  public:
+    explicit ArgParser(std::vector<Flag> flags) : flags_(std::move(flags)) {}
+    void parse(int argc, char **argv);
+    const Flag &get(const std::string &s) const;
+    bool on(const std::string &s) const { return get(s).seen; }
+    std::string str(const std::string &s, const std::string &dflt = "") const;
+    double dbl(const std::string &s, double dflt) const;
+    uint64_t uint(const std::string &s, uint64_t dflt, uint64_t maxv) const;
+    const std::vector<std::string> &files() const { return files_; }
+
+  private:
+    [[noreturn]] void fail(const std::string &msg, const std::string &id) const;
+    std::vector<Flag> flags_;
+    std::vector<std::string> files_;
+};
+
+// GPU count for the engine: UNIPEAK_GPUS (0 or unset = every visible device)
+int env_gpus();
+
+}  // namespace unipeak

@@ -1,0 +1,271 @@
+// unipeak_amd/host/engine.cpp -- see engine.hpp.
+#include "engine.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <iostream>
+#include <mutex>
+#include <thread>
+
+namespace unipeak {
+
+// countSum of one add (peakcall.cpp:186-200, quirk Q5): only used here to
+// spot head hits; the device recomputes it bit-exactly from the tracks
+static double count_sum(const uint32_t *c, size_t S, const std::vector<uint8_t> &control,
+                        const std::vector<double> &coeffs) {
+    double s = 0;
+    if (coeffs.empty()) {
+        for (size_t i = 0; i < S; ++i)
+            if (!control[i]) s += (double)c[i];
+    } else {
+        size_t k = 0;
+        for (size_t i = 0; i < S && k < coeffs.size(); ++i)
+            if (!control[i]) s += (double)c[i] * coeffs[k++];
+        for (size_t i = 0; i < S; ++i)
+            if (!control[i]) s += (double)c[i];
+    }
+    return s;
+}
+
+void build_units(std::vector<SampleStream *> &streams, const ContigTable &ct, bool directional,
+                 uint16_t bw, const std::vector<uint8_t> &control, const std::vector<double> &coeffs,
+                 bool quiet, PassResult &out) {
+    (void)quiet;
+    const size_t S = streams.size();
+    std::vector<uint32_t> fh(S), rh(S);
+    uint64_t clock = 0;
+    int cur[2] = {-1, -1};  // unit index per buffer for the current iteration
+    uint32_t contig = 0, iteration = 0;
+    bool forward = true;
+
+    auto add = [&](int buffer, int strand, const std::vector<uint32_t> &counts, uint32_t pos) {
+        if (cur[buffer] < 0) {
+            UnitBuild u;
+            u.buffer = buffer;
+            u.contig = contig;
+            u.len = ct.length(contig);
+            u.iteration = iteration;
+            out.units.push_back(std::move(u));
+            cur[buffer] = (int)out.units.size() - 1;
+        }
+        UnitBuild &u = out.units[cur[buffer]];
+        const int track = directional ? 0 : strand;
+        u.pos[track].push_back(pos);
+        u.cnt[track].insert(u.cnt[track].end(), counts.begin(), counts.end());
+        u.add_pos.push_back(pos);
+        u.add_time.push_back(++clock);
+        if (pos <= bw && count_sum(counts.data(), S, control, coeffs) != 0) u.head_hit = true;
+    };
+
+    // src/regions.cpp:311-391 (and src/strand_shift.cpp:144-190)
+    while (contig < ct.size()) {
+        const uint32_t lim = ct.length(contig);
+        uint32_t pos = 1;
+        while (pos <= lim) {
+            bool ff = false, fr = false;
+            uint32_t next = lim + 1;
+            for (size_t i = 0; i < S; ++i) {
+                fh[i] = 0;
+                rh[i] = 0;
+                const Align *a = &streams[i]->last();
+                while (a->count != 0 && a->first == pos && a->contig == contig) {
+                    if (a->forward) { fh[i] += a->count; ff = true; }
+                    else { rh[i] += a->count; fr = true; }
+                    a = &streams[i]->read_align();
+                }
+                if (a->count != 0 && a->contig == contig && a->first < next) next = a->first;
+            }
+            if (ff) add(0, 0, fh, pos);
+            if (fr) add(directional ? 1 : 0, 1, rh, pos);
+            out.write_times.push_back(clock);  // pending regions are written here
+            pos = next;
+        }
+        // flushContig(): forward buffer, then reverse buffer
+        for (int b = 0; b < 2; ++b) {
+            ++clock;
+            if (cur[b] >= 0) out.units[cur[b]].flush_time = clock;
+            cur[b] = -1;
+        }
+        ++contig;
+        ++iteration;
+        if (directional && contig == ct.size() && forward) {
+            contig = 0;
+            forward = false;
+        }
+    }
+}
+
+namespace {
+
+struct DeviceJob {
+    int dev;
+    std::vector<uint32_t> units;  // global unit indices
+    up_ctx *ctx = nullptr;
+    std::vector<uint32_t> dev_unit;  // device unit id -> global unit index
+    std::vector<uint64_t> cand_idx;  // candidate list index of each device region
+    int rc = UP_OK;
+    std::string err;
+};
+
+std::vector<DeviceJob> g_jobs;  // kept alive for shift_scan
+
+void check(int rc, const char *what) {
+    if (rc != UP_OK) fatal(std::string(what) + ": " + up_strerror(rc));
+}
+
+}  // namespace
+
+void run_units(const EngineParams &ep, PassResult &out) {
+    int ndev = 0;
+    up_device_count(&ndev);
+    if (ndev < 1) fatal("no HIP device available (the GPU path has no CPU fallback)");
+    if (ep.ngpus > 0 && ep.ngpus < ndev) ndev = ep.ngpus;
+    const size_t S = ep.p.n_samples;
+    for (const UnitBuild &u : out.units)
+        if (u.head_hit)
+            fatal("tags within the first bandwidth positions of a contig (quirk Q1) are not "
+                  "supported on the GPU path yet");
+    // LPT assignment of units to devices by track bytes
+    const int nstr = ep.p.nondir ? 2 : 1;
+    std::vector<uint32_t> order(out.units.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (uint32_t)i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return out.units[a].len > out.units[b].len;
+    });
+    std::vector<uint64_t> load(ndev, 0);
+    g_jobs.assign(ndev, DeviceJob());
+    for (int d = 0; d < ndev; ++d) g_jobs[d].dev = d;
+    for (uint32_t i : order) {
+        int best = 0;
+        for (int d = 1; d < ndev; ++d)
+            if (load[d] < load[best]) best = d;
+        load[best] += (uint64_t)out.units[i].len * nstr * S;
+        g_jobs[best].units.push_back(i);
+    }
+    for (auto &j : g_jobs) std::sort(j.units.begin(), j.units.end());  // buffer order kept
+
+    std::mutex mu;
+    auto work = [&](DeviceJob &job) {
+        auto fail = [&](int rc, const char *what) {
+            job.rc = rc;
+            job.err = std::string(what) + ": " + up_strerror(rc);
+        };
+        if (job.units.empty()) return;
+        int rc = up_open(job.dev, &job.ctx);
+        if (rc) return fail(rc, "up_open");
+        up_params p = ep.p;
+        p.is_control = ep.control.data();
+        p.coeffs = ep.coeffs.empty() ? nullptr : ep.coeffs.data();
+        p.n_coeffs = (uint32_t)ep.coeffs.size();
+        if ((rc = up_set_params(job.ctx, &p))) return fail(rc, "up_set_params");
+        std::vector<uint32_t> tp, tc;
+        for (uint32_t gi : job.units) {
+            const UnitBuild &u = out.units[gi];
+            uint32_t id = 0;
+            if ((rc = up_add_unit(job.ctx, u.len, nstr, u.buffer, &id))) return fail(rc, "up_add_unit");
+            job.dev_unit.push_back(gi);
+            for (int st = 0; st < nstr; ++st) {
+                const size_t n = u.pos[st].size();
+                for (size_t s = 0; s < S; ++s) {
+                    tp.clear();
+                    tc.clear();
+                    for (size_t k = 0; k < n; ++k) {
+                        const uint32_t c = u.cnt[st][k * S + s];
+                        if (c) {
+                            tp.push_back(u.pos[st][k]);
+                            tc.push_back(c);
+                        }
+                    }
+                    if (!tp.empty() &&
+                        (rc = up_unit_scatter(job.ctx, id, st, (uint16_t)s, tp.size(), tp.data(), tc.data())))
+                        return fail(rc, "up_unit_scatter");
+                }
+            }
+            if (!u.add_pos.empty()) up_unit_set_last_add(job.ctx, id, u.add_pos.back());
+        }
+        uint64_t n = 0;
+        if ((rc = up_run(job.ctx, &n))) return fail(rc, "up_run");
+        std::vector<up_region> regs(n);
+        std::vector<uint32_t> cnt(n * S);
+        if (n && (rc = up_get_regions(job.ctx, regs.data(), cnt.data(), n))) return fail(rc, "up_get_regions");
+        std::lock_guard<std::mutex> lk(mu);
+        for (uint64_t i = 0; i < n; ++i) {
+            Candidate c;
+            c.r = regs[i];
+            c.unit_index = job.dev_unit[regs[i].unit];
+            c.counts.assign(cnt.begin() + i * S, cnt.begin() + (i + 1) * S);
+            job.cand_idx.push_back(out.cands.size());
+            out.cands.push_back(std::move(c));
+        }
+    };
+    std::vector<std::thread> th;
+    for (auto &j : g_jobs) th.emplace_back(work, std::ref(j));
+    for (auto &t : th) t.join();
+    for (auto &j : g_jobs)
+        if (j.rc != UP_OK) fatal("GPU device " + std::to_string(j.dev) + ": " + j.err);
+}
+
+std::vector<Emitted> order_candidates(const PassResult &out, uint16_t bw, bool accepted_only) {
+    std::vector<Emitted> v;
+    v.reserve(out.cands.size());
+    const uint64_t last_write = out.write_times.empty() ? 0 : out.write_times.back();
+    for (const Candidate &c : out.cands) {
+        const UnitBuild &u = out.units[c.unit_index];
+        // closed by the first add at pos >= right + bw + 2, else by the flush
+        const uint64_t key = (uint64_t)c.r.right + bw + 2;
+        auto it = std::lower_bound(u.add_pos.begin(), u.add_pos.end(), key,
+                                   [](uint32_t a, uint64_t k) { return (uint64_t)a < k; });
+        const uint64_t t = it != u.add_pos.end() ? u.add_time[it - u.add_pos.begin()] : u.flush_time;
+        v.push_back(Emitted{&c, t, false, u.buffer == 0});
+    }
+    std::stable_sort(v.begin(), v.end(), [](const Emitted &a, const Emitted &b) {
+        if (a.close_time != b.close_time) return a.close_time < b.close_time;
+        return a.c->r.left < b.c->r.left;
+    });
+    // Q2: the reverse buffer's first candidate keeps the ctor's forward label
+    for (Emitted &e : v)
+        if (out.units[e.c->unit_index].buffer == 1) {
+            e.forward_label = true;
+            break;
+        }
+    for (Emitted &e : v) e.written = e.c->r.accepted && e.close_time <= last_write;  // Q3
+    if (accepted_only) {
+        std::vector<Emitted> a;
+        for (const Emitted &e : v)
+            if (e.c->r.accepted) a.push_back(e);
+        return a;
+    }
+    return v;
+}
+
+void shift_scan(const EngineParams &ep, PassResult &out, const std::vector<const Candidate *> &regs,
+                uint16_t max_shift, std::vector<double> &table) {
+    (void)ep;
+    const size_t W = (size_t)max_shift + 1;
+    table.assign(regs.size() * W, 0.0);
+    for (DeviceJob &job : g_jobs) {
+        if (!job.ctx) continue;
+        std::vector<uint64_t> idx;
+        std::vector<size_t> where;
+        for (size_t k = 0; k < regs.size(); ++k) {
+            const size_t ci = (size_t)(regs[k] - out.cands.data());
+            auto it = std::find(job.cand_idx.begin(), job.cand_idx.end(), (uint64_t)ci);
+            if (it == job.cand_idx.end()) continue;
+            idx.push_back((uint64_t)(it - job.cand_idx.begin()));
+            where.push_back(k);
+        }
+        if (idx.empty()) continue;
+        std::vector<double> t(idx.size() * W);
+        check(up_shift_scan(job.ctx, idx.data(), idx.size(), max_shift, t.data()), "up_shift_scan");
+        for (size_t j = 0; j < idx.size(); ++j)
+            std::copy(t.begin() + j * W, t.begin() + (j + 1) * W, table.begin() + where[j] * W);
+    }
+}
+
+void release_devices() {
+    for (DeviceJob &j : g_jobs)
+        if (j.ctx) up_close(j.ctx);
+    g_jobs.clear();
+}
+
+}  // namespace unipeak

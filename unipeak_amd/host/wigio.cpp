@@ -1,0 +1,452 @@
+// unipeak_amd/host/wigio.cpp -- see wigio.hpp.
+#include "wigio.hpp"
+
+#include <cctype>
+#include <cerrno>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+
+namespace unipeak {
+
+void fatal(const std::string &msg) {
+    std::cerr << "error: " << msg << "\n" << std::endl;
+    std::exit(1);
+}
+
+// ---------------------------------------------------------------------------
+// number parsing / formatting
+// ---------------------------------------------------------------------------
+bool lex_uint(const std::string &s, uint64_t maxv, uint64_t *out) {
+    size_t i = 0;
+    bool neg = false;
+    if (s.empty()) return false;
+    if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; i = 1; }
+    if (i == s.size()) return false;
+    uint64_t v = 0;
+    for (; i < s.size(); ++i) {
+        if (s[i] < '0' || s[i] > '9') return false;
+        const uint64_t d = (uint64_t)(s[i] - '0');
+        if (v > (maxv - d) / 10) return false;
+        v = v * 10 + d;
+    }
+    if (neg) v = (uint64_t)(0 - v) & maxv;  // lexical_cast<unsigned>("-1") wraps
+    *out = v;
+    return true;
+}
+
+bool lex_short(const std::string &s, int16_t *out) {
+    if (s.empty() || std::isspace((unsigned char)s[0])) return false;
+    char *e = nullptr;
+    errno = 0;
+    const long v = std::strtol(s.c_str(), &e, 10);
+    if (*e || errno || v < -32768 || v > 32767) return false;
+    *out = (int16_t)v;
+    return true;
+}
+
+bool lex_double(const std::string &s, double *out) {
+    if (s.empty() || std::isspace((unsigned char)s[0])) return false;
+    char *e = nullptr;
+    const double v = std::strtod(s.c_str(), &e);
+    if (*e) return false;
+    *out = v;
+    return true;
+}
+
+std::string fmt_lexical(double v) {
+    char b[64];
+    std::snprintf(b, sizeof b, "%.17g", v);
+    return b;
+}
+
+std::string fmt_ostream(double v) {
+    char b[64];
+    std::snprintf(b, sizeof b, "%g", v);
+    return b;
+}
+
+std::string fmt_fixed2(double v) {
+    char b[64];
+    std::snprintf(b, sizeof b, "%.2f", v);
+    return b;
+}
+
+std::vector<std::string> split_csv(const std::string &s) {
+    std::vector<std::string> out;
+    size_t p = 0;
+    while (p <= s.size()) {
+        size_t q = s.find(',', p);
+        if (q == std::string::npos) q = s.size();
+        if (q > p) out.push_back(s.substr(p, q - p));
+        p = q + 1;
+    }
+    return out;
+}
+
+std::string fname_prefix(const std::string &path) {
+    std::string r = path;
+    const size_t sl = r.rfind('/');
+    if (sl != std::string::npos) r = r.substr(sl + 1);
+    const size_t dot = r.find('.');
+    if (dot != std::string::npos) r = r.substr(0, dot);
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// LineReader
+// ---------------------------------------------------------------------------
+LineReader::LineReader(const std::string &fname) {
+    if (fname == "stdin") {
+        fp_ = stdin;
+        shown_ = "standard input stream";
+    } else {
+        fp_ = std::fopen(fname.c_str(), "rb");
+        if (!fp_) {
+            std::cerr << "error: could not read " << fname << std::endl << std::endl;
+            std::exit(1);
+        }
+        owned_ = true;
+        shown_ = fname;
+    }
+    open_ = true;
+}
+
+LineReader::~LineReader() {
+    close();
+    std::free(buf_);
+}
+
+void LineReader::close() {
+    if (open_ && owned_ && fp_) std::fclose(fp_);
+    open_ = false;
+    fp_ = nullptr;
+}
+
+const std::string &LineReader::read() {
+    ++line_no_;
+    const ssize_t n = getline(&buf_, &cap_, fp_);
+    if (n < 0) {
+        eof_ = true;
+        line_.clear();
+        return line_;
+    }
+    size_t len = (size_t)n;
+    if (len && buf_[len - 1] == '\n') --len;
+    else eof_ = true;  // a last line without '\n' sets eofbit
+    line_.assign(buf_, len);
+    return line_;
+}
+
+// ---------------------------------------------------------------------------
+// ContigTable (regex ^(\w+)\W+(\d+), '#' comments, duplicate names fatal)
+// ---------------------------------------------------------------------------
+uint32_t ContigTable::index(const std::string &name) const {
+    auto it = index_.find(name);
+    return it == index_.end() ? size() : it->second;
+}
+
+void ContigTable::add(const std::string &name, uint32_t len) {
+    if (index_.count(name)) fatal(name + " defined twice in contig table");
+    index_[name] = (uint32_t)names_.size();
+    names_.push_back(name);
+    lens_.push_back(len);
+    genome_ += len;
+}
+
+static bool word_char(int c) { return std::isalnum(c) || c == '_'; }
+
+ContigTable ContigTable::parse(const std::string &fname) {
+    std::cerr << "reading " << fname << "... " << std::flush;
+    ContigTable t;
+    LineReader in(fname);
+    while (in.good()) {
+        const std::string &l = in.read();
+        if (l.empty() || l[0] == '#') continue;
+        size_t i = 0;
+        while (i < l.size() && word_char((unsigned char)l[i])) ++i;
+        if (i == 0) continue;
+        size_t j = i;
+        while (j < l.size() && !word_char((unsigned char)l[j])) ++j;
+        if (j == i) continue;
+        size_t k = j;
+        while (k < l.size() && std::isdigit((unsigned char)l[k])) ++k;
+        if (k == j) continue;
+        uint64_t v;
+        if (!lex_uint(l.substr(j, k - j), 0xFFFFFFFFull, &v)) {
+            std::cerr << "terminate called after throwing an instance of 'boost::bad_lexical_cast'" << std::endl;
+            std::abort();
+        }
+        const std::string name = l.substr(0, i);
+        if (t.index(name) != t.size()) {
+            std::cerr << "error: " << name << " defined twice in contig table\n" << std::endl;
+            std::exit(1);
+        }
+        t.add(name, (uint32_t)v);
+    }
+    if (t.size() == 0) {
+        std::cerr << "error: no contigs in table" << std::endl << std::endl;
+        std::exit(1);
+    }
+    std::cerr << t.size() << " contigs" << std::endl;
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// WigStream
+// ---------------------------------------------------------------------------
+WigStream::WigStream(const std::string &fname, const ContigTable *ct, int16_t offset,
+                     uint16_t use_length, int strand_filter)
+    : in_(fname), fname_(fname), ct_(ct), offset_(offset), use_length_(use_length),
+      filter_(strand_filter) {
+    name_ = fname_prefix(fname);
+    a_.forward = true;
+    a_.contig = 0;  // ParseAlignStream::open resets the contig to 0
+}
+
+void WigStream::bad(const char *what) const {
+    std::cerr << "error: " << what << " in " << in_.display_name() << " line " << in_.line_no()
+              << "\n" << std::endl;
+    std::exit(1);
+}
+
+// name="(.+?)"
+static bool name_quoted(const std::string &l, std::string *out) {
+    for (size_t p = l.find("name=\""); p != std::string::npos; p = l.find("name=\"", p + 1)) {
+        const size_t q = p + 6;
+        if (q >= l.size()) continue;
+        const size_t e = l.find('"', q + 1);
+        if (e == std::string::npos) continue;
+        *out = l.substr(q, e - q);
+        return true;
+    }
+    return false;
+}
+
+// name=(.+?)<space>
+static bool name_bare(const std::string &l, std::string *out) {
+    for (size_t p = l.find("name="); p != std::string::npos; p = l.find("name=", p + 1)) {
+        const size_t q = p + 5;
+        if (q >= l.size()) continue;
+        const size_t e = l.find(' ', q + 1);
+        if (e == std::string::npos) continue;
+        *out = l.substr(q, e - q);
+        return true;
+    }
+    return false;
+}
+
+// "(.+) ([+-])" with a greedy first group
+static bool strand_suffix(const std::string &name, std::string *expt, bool *fwd) {
+    if (name.size() < 3) {
+        if (name.size() < 3) return false;
+    }
+    for (size_t i = name.size() - 2; i >= 1; --i) {
+        if (name[i] == ' ' && (name[i + 1] == '+' || name[i + 1] == '-')) {
+            *expt = name.substr(0, i);
+            *fwd = name[i + 1] == '+';
+            return true;
+        }
+    }
+    return false;
+}
+
+static bool starts(const std::string &l, const char *p) { return l.compare(0, std::strlen(p), p) == 0; }
+
+void WigStream::parse(const std::string &l) {
+    a_.count = 0;
+    if (l.empty() || l[0] == '#') return;
+    if (format_ == 0) {
+        if (!starts(l, "track"))
+            fatal("unsupported input format in " + fname_ + " (wiggle files only)");
+        std::string nm;
+        const bool has = name_quoted(l, &nm) || name_bare(l, &nm);
+        if (has) name_ = nm;
+        if (l.find("type=wiggle_0") == std::string::npos)
+            fatal("unsupported input format in " + fname_ + " (wiggle files only)");
+        std::string e;
+        bool f;
+        if (strand_suffix(name_, &e, &f)) {
+            format_ = 6;
+            name_ = e;
+            a_.forward = f;
+        } else {
+            format_ = 7;
+            name_ = has ? nm : std::string();
+            a_.forward = true;
+        }
+        return;
+    }
+    if (std::isdigit((unsigned char)l[0])) {
+        if (a_.contig == ct_->size()) return;
+        const size_t d = l.find_last_of("\t ");
+        if (d == std::string::npos) bad("bad format");
+        uint64_t pos, cnt;
+        if (!lex_uint(l.substr(0, d), 0xFFFFFFFFull, &pos)) bad("bad format");
+        const size_t cs = d + (d + 1 < l.size() && l[d + 1] == '-' ? 2 : 1);
+        if (!lex_uint(cs <= l.size() ? l.substr(cs) : std::string(), 0xFFFFFFFFull, &cnt)) bad("bad format");
+        a_.first = (uint32_t)pos;
+        a_.count = (uint32_t)cnt;
+        const uint32_t ext = use_length_ == 0 ? 0u : (uint32_t)(use_length_ - 1);
+        if (format_ == 6) a_.last = a_.first + (a_.forward ? ext : (uint32_t)(0u - ext));
+        else a_.last = a_.first + ext;
+        total_ += a_.count;
+    } else if (starts(l, "variableStep chrom=") && l.size() > 19) {
+        a_.contig = ct_->index(l.substr(19));
+        return;
+    } else if (starts(l, "track")) {
+        std::string nm;
+        if (!name_quoted(l, &nm)) bad("bad format");
+        a_.contig = ct_->size();
+        name_ = nm;
+        if (format_ == 6) {
+            std::string e;
+            bool f;
+            if (!strand_suffix(name_, &e, &f)) bad("strand not defined");
+            name_ = e;
+            a_.forward = f;
+        }
+        return;
+    } else {
+        bad("bad format");
+    }
+    // offset and bounds (format.cpp:654-678)
+    if (a_.count != 0 && a_.contig != ct_->size()) {
+        if (use_length_ != 0) {
+            const uint32_t ext = (uint32_t)(use_length_ - 1);
+            a_.last = a_.first + (a_.forward ? ext : (uint32_t)(0u - ext));
+        }
+        if (offset_ != 0) {
+            if ((a_.forward && (int)a_.first > -offset_) || (!a_.forward && (int)a_.last > offset_)) {
+                const uint32_t sh = (uint32_t)(a_.forward ? (int)offset_ : -(int)offset_);
+                a_.first += sh;
+                a_.last += sh;
+            } else {
+                oob_ += a_.count;
+                a_.count = 0;
+                return;
+            }
+        }
+        const uint32_t size = ct_->length(a_.contig);
+        if (a_.first == 0 || a_.first > size || a_.last == 0 || a_.last > size) {
+            oob_ += a_.count;
+            a_.count = 0;
+            return;
+        }
+        confident_ += a_.count;
+    }
+}
+
+void WigStream::read_plain() {
+    if (in_.good()) {
+        parse(in_.read());
+    } else {
+        a_.count = 0;
+        a_.contig = ct_->size();
+    }
+    while ((a_.count == 0 || a_.contig == ct_->size()) && in_.good()) parse(in_.read());
+}
+
+const Align &WigStream::read_align() {
+    read_plain();
+    if (filter_ == 0) return a_;
+    const bool want = filter_ == 1;
+    if (format_ == 6 && want && !a_.forward && a_.count > 0) {  // forward handle is done
+        a_.count = 0;
+        in_.close();
+    }
+    while (in_.good() && a_.forward != want) read_plain();
+    return a_;
+}
+
+uint64_t WigStream::expected_tags() {
+    if (expected_ != 0) return expected_;
+    while (in_.good()) {
+        const std::string l = in_.read();
+        if (!l.empty() && l[0] == '#') {
+            const size_t m = l.find("# tags=");
+            if (m != std::string::npos && m + 7 < l.size() && std::isdigit((unsigned char)l[m + 7])) {
+                size_t k = m + 7;
+                while (k < l.size() && std::isdigit((unsigned char)l[k])) ++k;
+                uint64_t v;
+                if (!lex_uint(l.substr(m + 7, k - m - 7), ~0ull, &v)) std::abort();
+                if (expected_ == 0) expected_ = v;
+                else bad("multiple tag count headers");
+                if (expected_ == 0) bad("zero tag count");
+            }
+        } else {
+            parse(l);
+            if (expected_ == 0) {  // count the hard way
+                WigStream t(fname_, ct_, offset_, use_length_, 0);
+                while (t.in_.good()) t.read_plain();
+                expected_ = t.confident_;
+            }
+            break;
+        }
+    }
+    return expected_;
+}
+
+// ---------------------------------------------------------------------------
+// SampleStream
+// ---------------------------------------------------------------------------
+SampleStream::SampleStream(const std::string &fname, const ContigTable *ct, int16_t offset,
+                           uint16_t use_length, bool nondirectional)
+    : nondir_(nondirectional) {
+    if (!nondir_) {
+        plain_.reset(new WigStream(fname, ct, offset, use_length, 0));
+    } else {
+        fwd_.reset(new WigStream(fname, ct, offset, use_length, 1));
+        rev_.reset(new WigStream(fname, ct, offset, use_length, 2));
+        // quirk Q18: the reference leaves this flag uninitialised; the
+        // intended two-handle merge starts from the forward handle
+        merged_.forward = true;
+        merged_.contig = ct->size();
+    }
+}
+
+const WigStream &SampleStream::further() const {
+    return fwd_->line_no() >= rev_->line_no() ? *fwd_ : *rev_;
+}
+
+uint64_t SampleStream::expected_tags() {
+    if (!nondir_) return plain_->expected_tags();
+    if (expected_ == 0)
+        expected_ = fwd_->line_no() >= rev_->line_no() ? fwd_->expected_tags() : rev_->expected_tags();
+    return expected_;
+}
+
+const std::string &SampleStream::expt_name() const { return nondir_ ? further().expt_name() : plain_->expt_name(); }
+uint64_t SampleStream::confident() const { return nondir_ ? further().confident() : plain_->confident(); }
+uint64_t SampleStream::out_of_bounds() const { return nondir_ ? further().out_of_bounds() : plain_->out_of_bounds(); }
+
+// NondirParseAlignStream::readAlign (format.cpp:873-895)
+const Align &SampleStream::read_align() {
+    if (!nondir_) return plain_->read_align();
+    if (merged_.forward) {
+        const Align &f = fwd_->read_align();
+        if (f.forward && f.contig == merged_.contig && f.first < merged_.first) {
+            std::cerr << f.first << "\t" << merged_.first << "\n";
+            fatal("alignments out of order");
+        }
+    } else {
+        const Align &r = rev_->read_align();
+        if (!r.forward && r.contig == merged_.contig && r.first < merged_.first)
+            fatal("alignments out of order");
+    }
+    if (fwd_->line_no() == 0) fwd_->read_align();
+    if (rev_->line_no() == 0) rev_->read_align();
+    const Align &a1 = fwd_->last(), &a2 = rev_->last();
+    bool lower;
+    switch (2 * (a1.count == 0) + (a2.count == 0)) {
+    case 0: lower = a1.contig == a2.contig ? a1.first <= a2.first : a1.contig < a2.contig; break;
+    case 1: lower = true; break;
+    case 2: lower = false; break;
+    default: lower = true; break;
+    }
+    merged_ = lower ? a1 : a2;
+    return merged_;
+}
+
+}  // namespace unipeak
