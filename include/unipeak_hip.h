@@ -73,6 +73,8 @@ typedef struct {
     int32_t want_corr;        /* evaluate strandCorr(0) for every region */
 } up_params;
 
+#define UP_CLOSE_RULE 0xFFFFFFFFu
+
 /* One candidate region (accepted or rejected by processRegion). */
 typedef struct {
     uint32_t unit;            /* unit the region was closed in */
@@ -81,7 +83,11 @@ typedef struct {
     uint32_t sum;             /* Region::sum() (uint32, wraps) */
     uint32_t nonctl_sum;      /* sum over non-control samples of exptSums */
     int32_t accepted;         /* passed the hit/kurtosis/correlation filters */
-    int32_t reserved;
+    uint32_t close_pos;       /* UP_CLOSE_RULE: closed by the unit's first add at
+                                 pos >= right + bw + 2, else by its flush;
+                                 0: closed by the unit's flush; otherwise the
+                                 position of the add whose retirement closed it
+                                 (head-hit units replayed by the emulator, Q1) */
     double peak_score;        /* f+r at peak */
     double kurtosis;          /* Region::posKurtosis() */
     double corr;              /* Region::strandCorr(0) or NaN when not evaluated */
@@ -103,7 +109,11 @@ int up_set_params(up_ctx *ctx, const up_params *p);
  * reverse buffer) over one contig pass; units of one buffer must be added in
  * the order the buffer sees them.  nstrands is 1 (directional) or 2
  * (nondirectional: strand 0 forward, 1 reverse).  Count tracks are zeroed
- * uint32 arrays covering positions 1..contig_len. */
+ * uint32 arrays covering positions 1..contig_len.
+ * Quirk Q1 (misc/peakcall.cpp:177-183): a unit with pooled tags at a position
+ * <= bw is replayed by the exact state machine; if all of its adds sit at
+ * positions <= bw its leftover state leaks into the buffer's NEXT unit, which
+ * must then be in the same context (the reference driver's chain). */
 int up_add_unit(up_ctx *ctx, uint32_t contig_len, int32_t nstrands,
                 int32_t buffer_id, uint32_t *unit_id);
 int up_unit_count(up_ctx *ctx, uint32_t *n);

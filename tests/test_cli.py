@@ -154,3 +154,62 @@ def test_cli_usage_errors(tmp_path):
         assert r.returncode == 1 and r.stderr.startswith("error: ")
     r = subprocess.run([os.path.join(BIN, "regions"), "--version"], capture_output=True, text=True)
     assert r.returncode == 0 and "1.0" in r.stdout
+
+
+# ---- quirk Q1: tags within the first bw positions of a contig ----
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", __import__("tests.test_oracle_kat", fromlist=["KAT"]).KAT["cases"],
+                         ids=lambda c: c["name"])
+def test_regions_cli_survey_kats(orc_bin, gpu_lib, tmp_path, case):
+    """Every recorded reference answer (incl. both Q1 probes) through bin/regions."""
+    from tests.test_oracle_kat import run_case
+    _, _, rows = run_case([os.path.join(BIN, "regions")], case, tmp_path)
+    got = [[r[0], int(r[1]), [int(x) for x in r[3:]]] for r in rows]
+    assert got == case["expect"]
+
+
+def gen_head_sample(rng, contigs, bw, tiny=()):
+    """Clusters plus tags inside the first bw positions of most contigs;
+    contigs named in `tiny` get tags only at positions <= bw (their buffer
+    state leaks into the next contig pass)."""
+    fwd, rev = gen_sample(rng, [c for c in contigs if c[1] >= 2000], lo=bw + 1, n_cl=3, sd=40)
+    for d in (fwd, rev):
+        for name, L in contigs:
+            dense = dict(d.get(name, [])) if name not in tiny else {}
+            if name in tiny or rng.random() < 0.8:
+                for p in rng.integers(1, bw + 1, int(rng.integers(1, 12))):
+                    dense[int(p)] = dense.get(int(p), 0) + int(rng.integers(1, 9))
+            if dense:
+                d[name] = sorted(dense.items())
+    return fwd, rev
+
+
+Q1_CASES = [
+    ("dir_bw50", 50, 1, ["-f", "-k", "0"], ()),
+    ("dir_bw50_leak", 50, 1, ["-f", "-k", "0"], ("c1", "c3")),
+    ("dir_bw20_controls", 20, 2, ["-f", "-e", "2"], ("c2",)),
+    ("dir_bw100_coeffs", 100, 3, ["-e", "3", "-z", "0.5,2", "-k", "0"], ("c1",)),
+    ("nondir_bw50_corr", 50, 1, ["-D", "-y", "-f", "-k", "0"], ("c2",)),
+    ("nondir_bw90_two", 90, 2, ["-D", "-f", "-k", "0"], ("c1", "c2")),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", Q1_CASES, ids=lambda c: c[0])
+@pytest.mark.parametrize("thr_m", ["3000", "100000"])
+def test_regions_cli_q1_head_hits(orc_bin, gpu_lib, tmp_path, case, thr_m):
+    name, bw, ns, args, tiny = case
+    rng = np.random.default_rng(zlib.crc32((name + thr_m).encode()))
+    contigs = [("c0", 9000), ("c1", 4000), ("c2", 400), ("c3", 7000), ("c4", 5000)]
+    ct = tmp_path / "contigs.txt"
+    write_contigs(ct, contigs)
+    files = []
+    for i in range(ns):
+        fwd, rev = gen_head_sample(rng, contigs, bw, tiny)
+        p = tmp_path / f"s{i}.wig"
+        write_wig(p, f"s{i}", fwd, rev)
+        files.append(str(p))
+    out = compare_tool(orc_bin, tmp_path, "regions",
+                       ["-q", "-c", str(ct), "-b", str(bw), "-m", thr_m] + args + files)
+    assert out.count("\n") > 3

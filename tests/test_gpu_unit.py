@@ -149,3 +149,43 @@ def test_synthetic_track_matches_oracle_spec(gpu_lib, oracle):
         f, _ = g.profile(u, length)
     ref = oracle.profile(bw, 0.003, length, pos, cnt.reshape(-1, 1))
     assert ref.tobytes() == f.tobytes()
+
+
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("bw", [50, 13, 120])
+def test_head_hits_replayed_q1(gpu_lib, oracle, seed, bw):
+    """Quirk Q1: tags at positions <= bw misalign the reference's window; the
+    library replays the state machine there and resyncs to the parallel scan."""
+    rng = np.random.default_rng(900 + seed)
+    length = int(rng.integers(3_000, 60_000))
+    pos, cnt = random_unit(rng, length, bw, lo=1, n_clusters=int(rng.integers(1, 6)))
+    head = rng.integers(1, bw + 1, int(rng.integers(1, 6)))
+    dense = {int(p): int(c) for p, c in zip(pos, cnt[:, 0])}
+    for p in head:
+        dense[int(p)] = dense.get(int(p), 0) + int(rng.integers(5, 40))
+    if seed % 2:  # a cluster right at the start keeps a region open across the resync horizon
+        for o in np.rint(rng.normal(bw, bw / 2, 80)).astype(int):
+            if 1 <= o <= length:
+                dense[int(o)] = dense.get(int(o), 0) + 1
+    pos = np.array(sorted(dense), np.uint32)
+    cnt = np.array([[dense[int(p)]] for p in pos], np.uint32)
+    bg = 0.003
+    thr = float(rng.choice([5.0, 25.0]))
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, region_thr=thr, kurt_thr=0.0)
+    regs, gcnt, f, r, last = run_gpu(gpu_lib, bw, bg, length, pos, cnt, region_thr=thr, kurt_thr=0.0)
+    compare(ref, ref_sums, regs, gcnt)
+    assert len(regs) > 0
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_head_hits_nondir_with_corr(gpu_lib, oracle, seed):
+    rng = np.random.default_rng(950 + seed)
+    length, bw, bg = 20_000, 50, 0.003
+    pos, cf = random_unit(rng, length, bw, lo=1)
+    cr = np.roll(cf, 3, axis=0)
+    cf[:3] += 7
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cf, cr, nondir=True, corr_thr=0.1, kurt_thr=0.0)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cf, cr, nondir=True, corr_thr=0.1,
+                             kurt_thr=0.0, want_corr=True)
+    compare(ref, ref_sums, regs, gcnt)
+    assert close(ref["corr"], regs["corr"])

@@ -47,7 +47,7 @@ class Region(ctypes.Structure):
         ("sum", ctypes.c_uint32),
         ("nonctl_sum", ctypes.c_uint32),
         ("accepted", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("close_pos", ctypes.c_uint32),
         ("peak_score", ctypes.c_double),
         ("kurtosis", ctypes.c_double),
         ("corr", ctypes.c_double),
@@ -56,7 +56,7 @@ class Region(ctypes.Structure):
 
 REGION_DTYPE = np.dtype([
     ("unit", "<u4"), ("left", "<u4"), ("right", "<u4"), ("peak", "<u4"),
-    ("sum", "<u4"), ("nonctl_sum", "<u4"), ("accepted", "<i4"), ("reserved", "<i4"),
+    ("sum", "<u4"), ("nonctl_sum", "<u4"), ("accepted", "<i4"), ("close_pos", "<u4"),
     ("peak_score", "<f8"), ("kurtosis", "<f8"), ("corr", "<f8")])
 assert REGION_DTYPE.itemsize == ctypes.sizeof(Region)
 

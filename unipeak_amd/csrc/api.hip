@@ -15,6 +15,7 @@
 #include "kernels.h"
 
 #include "kernels.hip"  // single translation unit: kernels + C-ABI
+#include "emulate.hip"
 
 using namespace upk;
 
@@ -83,6 +84,16 @@ struct up_ctx {
     std::vector<uint32_t> unit_last;
     hipEvent_t ev[8] = {};
     double times[5] = {0, 0, 0, 0, 0};
+    // head-hit (quirk Q1) replay
+    DevBuf<uint32_t> d_head, d_resync, d_emu_n, d_emu_err, d_emu_counts, d_ring_hits, d_reg_hit, d_reg_hits;
+    DevBuf<int32_t> d_unit_buffer;
+    DevBuf<double> d_reg_f, d_reg_r;
+    DevBuf<up_region> d_emu_out;
+    bool host_regions = false;  // merged list lives on the host
+    std::vector<up_region> h_regions;
+    std::vector<uint32_t> h_counts;
+    std::vector<uint8_t> h_emulated;
+    std::vector<uint32_t> h_head;
 };
 
 #define HIPCHK(x)                                                                   \
@@ -171,6 +182,9 @@ void up_close(up_ctx *c) {
     c->d_cnt.release(); c->d_off.release(); c->d_nreg.release(); c->d_tmp.release();
     c->d_starts.release(); c->d_ends.release(); c->d_runit.release(); c->d_counts.release();
     c->d_regions.release();
+    c->d_head.release(); c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
+    c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
+    c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -497,7 +511,7 @@ static StatParams stat_params(up_ctx *c) {
     P.kern = c->d_kern.p;
     P.bw = c->p.bw;
     P.nondir = c->p.nondir;
-    P.want_corr = c->p.want_corr;
+    P.want_corr = c->p.want_corr || c->p.corr_thr > -1;
     P.region_thr = c->p.region_thr;
     P.kurt_thr = c->p.kurt_thr;
     P.corr_thr = c->p.corr_thr;
@@ -541,6 +555,141 @@ static int check_runnable(up_ctx *c) {
     return UP_OK;
 }
 
+// Quirk Q1: units whose pooled hits include a position <= bw are replayed
+// by the exact state machine (emulate.hip); their early regions replace the
+// parallel path's, and the merged list moves to the host.
+static int launch_head_detect(up_ctx *c) {
+    const uint32_t nu = (uint32_t)c->units.size();
+    HIPCHK(c->d_head.ensure(nu));
+    HIPCHK(hipMemsetAsync(c->d_head.p, 0, nu * sizeof(uint32_t), c->stream));
+    if (pool_mode(c) == 2)
+        hipLaunchKernelGGL(head_detect_kernel<2>, dim3(nu), dim3(128), 0, c->stream, c->d_units.p,
+                           (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw, c->d_head.p);
+    else
+        hipLaunchKernelGGL(head_detect_kernel<1>, dim3(nu), dim3(128), 0, c->stream, c->d_units.p,
+                           (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw, c->d_head.p);
+    HIPCHK(hipGetLastError());
+    c->h_head.resize(nu);
+    HIPCHK(hipMemcpyAsync(c->h_head.data(), c->d_head.p, nu * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    return UP_OK;
+}
+
+// after launch_head_detect's copy has landed
+static int replay_head_hits(up_ctx *c) {
+    c->host_regions = false;
+    const uint32_t nu = (uint32_t)c->units.size();
+    const std::vector<uint32_t> &head = c->h_head;
+    bool any = false;
+    for (uint32_t h : head) any |= h != 0;
+    if (!any) return UP_OK;
+
+    const int S = c->p.n_samples;
+    const uint32_t W = 2u * c->p.bw + 1;
+    const uint32_t reg_cap = 1u << 18, out_cap = 1u << 16;
+    std::vector<int32_t> ub(nu);
+    for (uint32_t i = 0; i < nu; ++i) ub[i] = c->units[i].buffer;
+    HIPCHK(c->d_unit_buffer.ensure(nu));
+    HIPCHK(hipMemcpy(c->d_unit_buffer.p, ub.data(), nu * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(c->d_resync.ensure(nu));
+    HIPCHK(hipMemsetAsync(c->d_resync.p, 0, nu * sizeof(uint32_t), c->stream));
+    HIPCHK(c->d_emu_n.ensure(1));
+    HIPCHK(c->d_emu_err.ensure(1));
+    HIPCHK(hipMemsetAsync(c->d_emu_n.p, 0, 4, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_emu_err.p, 0, 4, c->stream));
+    HIPCHK(c->d_emu_out.ensure(out_cap));
+    HIPCHK(c->d_emu_counts.ensure((size_t)out_cap * S));
+    HIPCHK(c->d_ring_hits.ensure(2ull * W * S));
+    HIPCHK(c->d_reg_f.ensure(2ull * reg_cap));
+    HIPCHK(c->d_reg_r.ensure(2ull * reg_cap));
+    HIPCHK(c->d_reg_hit.ensure(2ull * reg_cap));
+    HIPCHK(c->d_reg_hits.ensure(2ull * reg_cap * S));
+    EmuParams E{};
+    E.units = c->d_units.p;
+    E.nunits = nu;
+    E.unit_buffer = c->d_unit_buffer.p;
+    E.unit_head = c->d_head.p;
+    E.S = S;
+    E.nnc = (int32_t)c->nc.size();
+    E.nc = c->d_nc.p;
+    E.is_control = c->d_ctl.p;
+    E.coef = c->d_coef.p;
+    E.ncoef = (int32_t)c->coef.size();
+    E.kern = c->d_kern.p;
+    E.bw = c->p.bw;
+    E.nondir = c->p.nondir;
+    E.region_thr = c->p.region_thr;
+    E.kurt_thr = c->p.kurt_thr;
+    E.corr_thr = c->p.corr_thr;
+    E.hit_thr = c->p.hit_thr;
+    E.want_corr = c->p.want_corr || c->p.corr_thr > -1;
+    E.resync = c->d_resync.p;
+    E.out = c->d_emu_out.p;
+    E.out_counts = c->d_emu_counts.p;
+    E.nout = c->d_emu_n.p;
+    E.out_cap = out_cap;
+    E.ring_hits = c->d_ring_hits.p;
+    E.reg_f = c->d_reg_f.p;
+    E.reg_r = c->d_reg_r.p;
+    E.reg_hit = c->d_reg_hit.p;
+    E.reg_hits = c->d_reg_hits.p;
+    E.reg_cap = reg_cap;
+    E.err = c->d_emu_err.p;
+    hipLaunchKernelGGL(emulate_kernel, dim3(2), dim3(64), 0, c->stream, E);
+    HIPCHK(hipGetLastError());
+    uint32_t nemu = 0, err = 0;
+    std::vector<uint32_t> resync(nu);
+    HIPCHK(hipMemcpyAsync(&nemu, c->d_emu_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&err, c->d_emu_err.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(resync.data(), c->d_resync.p, nu * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (err) {
+        fprintf(stderr, "unipeak_hip: head-hit replay failed (flags %u)\n", err);
+        return err & 4u ? UP_E_ARG : UP_E_NOMEM;
+    }
+    std::vector<up_region> emu(nemu), par(c->nreg);
+    std::vector<uint32_t> ecnt((size_t)nemu * S), pcnt((size_t)c->nreg * S);
+    if (nemu) {
+        HIPCHK(hipMemcpy(emu.data(), c->d_emu_out.p, nemu * sizeof(up_region), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(ecnt.data(), c->d_emu_counts.p, ecnt.size() * 4, hipMemcpyDeviceToHost));
+    }
+    if (c->nreg) {
+        HIPCHK(hipMemcpy(par.data(), c->d_regions.p, c->nreg * sizeof(up_region), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(pcnt.data(), c->d_counts.p, pcnt.size() * 4, hipMemcpyDeviceToHost));
+    }
+    // merge: unit-major; within a unit the replayed regions, then the
+    // parallel ones that start at or after the resync position
+    std::vector<std::pair<uint64_t, int64_t>> keys;  // (unit<<32 | order, +par idx / -emu idx-1)
+    for (uint32_t i = 0; i < nemu; ++i) keys.push_back({((uint64_t)emu[i].unit << 32) | i, -(int64_t)i - 1});
+    for (uint64_t i = 0; i < c->nreg; ++i) {
+        const uint32_t x = resync[par[i].unit];
+        if (x != 0 && par[i].left < x) continue;
+        keys.push_back({((uint64_t)par[i].unit << 32) | (0x80000000u + par[i].left / 2), (int64_t)i});
+    }
+    std::stable_sort(keys.begin(), keys.end(),
+                     [](const std::pair<uint64_t, int64_t> &a, const std::pair<uint64_t, int64_t> &b) {
+                         return (a.first >> 32) < (b.first >> 32);
+                     });
+    c->h_regions.clear();
+    c->h_counts.clear();
+    c->h_emulated.clear();
+    for (auto &k : keys) {
+        if (k.second < 0) {
+            const uint32_t i = (uint32_t)(-k.second - 1);
+            c->h_regions.push_back(emu[i]);
+            c->h_counts.insert(c->h_counts.end(), ecnt.begin() + (size_t)i * S, ecnt.begin() + (size_t)(i + 1) * S);
+            c->h_emulated.push_back(1);
+        } else {
+            const uint64_t i = (uint64_t)k.second;
+            c->h_regions.push_back(par[i]);
+            c->h_counts.insert(c->h_counts.end(), pcnt.begin() + i * S, pcnt.begin() + (i + 1) * S);
+            c->h_emulated.push_back(0);
+        }
+    }
+    c->host_regions = true;
+    c->nreg = c->h_regions.size();
+    return UP_OK;
+}
+
 int up_run(up_ctx *c, uint64_t *n_regions) {
     int r = check_runnable(c);
     if (r) return r;
@@ -548,6 +697,7 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     HIPCHK(hipSetDevice(c->dev));
     c->ran = false;
     c->nreg = 0;
+    c->host_regions = false;
     if (c->units.empty()) {
         if (n_regions) *n_regions = 0;
         c->ran = true;
@@ -611,6 +761,7 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     dispatch_stats(c, P, nreg);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    if ((r = launch_head_detect(c))) return r;
     hipLaunchKernelGGL(unit_last_kernel, dim3((unsigned)c->units.size()), dim3(256), 0, c->stream,
                        c->d_units.p, (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p,
                        c->d_unit_last.p);
@@ -619,6 +770,7 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     HIPCHK(hipMemcpyAsync(c->unit_last.data(), c->d_unit_last.p, c->units.size() * 4,
                           hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if ((r = replay_head_hits(c))) return r;
     float a = 0, b = 0, d = 0;
     (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
     (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
@@ -628,7 +780,7 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     c->times[2] = d;
     c->times[3] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->ran = true;
-    if (n_regions) *n_regions = nreg;
+    if (n_regions) *n_regions = c->nreg;
     return UP_OK;
 }
 
@@ -636,6 +788,11 @@ int up_get_regions(up_ctx *c, up_region *out, uint32_t *counts, size_t cap) {
     if (!c) return UP_E_ARG;
     if (!c->ran) return UP_E_STATE;
     const size_t n = c->nreg < cap ? (size_t)c->nreg : cap;
+    if (c->host_regions) {
+        if (n && out) std::memcpy(out, c->h_regions.data(), n * sizeof(up_region));
+        if (n && counts) std::memcpy(counts, c->h_counts.data(), n * c->p.n_samples * sizeof(uint32_t));
+        return UP_OK;
+    }
     HIPCHK(hipSetDevice(c->dev));
     if (n && out)
         HIPCHK(hipMemcpyAsync(out, c->d_regions.p, n * sizeof(up_region), hipMemcpyDeviceToHost, c->stream));
@@ -653,8 +810,27 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
     if (n == 0) return UP_OK;
     HIPCHK(hipSetDevice(c->dev));
     std::vector<uint32_t> st(c->nreg), en(c->nreg);
-    HIPCHK(hipMemcpy(st.data(), c->d_starts.p, c->nreg * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(en.data(), c->d_ends.p, c->nreg * 4, hipMemcpyDeviceToHost));
+    if (c->host_regions) {
+        // replayed (Q1) regions carry state-machine scores the dense KDE
+        // cannot reproduce; refuse rather than return something else
+        std::vector<uint32_t> un(c->nreg);
+        for (uint64_t i = 0; i < c->nreg; ++i) {
+            st[i] = c->h_regions[i].left;
+            en[i] = c->h_regions[i].right;
+            un[i] = c->h_regions[i].unit;
+        }
+        for (size_t j = 0; j < n; ++j)
+            if (idx[j] < c->nreg && c->h_emulated[idx[j]]) return UP_E_UNSUPPORTED;
+        HIPCHK(c->d_starts.ensure(c->nreg + 1));
+        HIPCHK(c->d_ends.ensure(c->nreg + 1));
+        HIPCHK(c->d_runit.ensure(c->nreg + 1));
+        HIPCHK(hipMemcpy(c->d_starts.p, st.data(), c->nreg * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->d_ends.p, en.data(), c->nreg * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->d_runit.p, un.data(), c->nreg * 4, hipMemcpyHostToDevice));
+    } else {
+        HIPCHK(hipMemcpy(st.data(), c->d_starts.p, c->nreg * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(en.data(), c->d_ends.p, c->nreg * 4, hipMemcpyDeviceToHost));
+    }
     std::vector<uint64_t> off(n);
     uint64_t tot = 0;
     for (size_t j = 0; j < n; ++j) {

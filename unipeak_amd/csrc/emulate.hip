@@ -1,0 +1,379 @@
+// unipeak_amd/csrc/emulate.hip -- K0: exact replay of the ProfileBuffer
+// state machine (misc/peakcall.cpp:33-231, Region stats misc/data.cpp:92-193)
+// for the units the parallel scan cannot represent: a contig pass whose
+// pooled hits include a position <= bw (quirk Q1: the deque window does not
+// shift there, peakcall.cpp:177-183, and leftover density / an open region
+// can leak into the buffer's next contig pass, peakcall.cpp:164-168,
+// 224-231).  #included by api.hip.
+//
+// One workgroup (one wave) per ProfileBuffer walks that buffer's units in
+// order.  A chain starts at a unit with a head hit and replays add() for
+// every position with tags on the buffer's strand(s) (control samples
+// included: control-only adds move the window too).  It stops as soon as the
+// replayed state is the one the parallel path assumes -- the buffer is
+// aligned (an add past bw happened in this unit), every position that could
+// hold misaligned leftovers (<= first aligned add + bw) has been retired and
+// no region is open -- and records the resync position X: regions of that
+// unit starting at or after X come from K1-K3 unchanged, earlier ones from
+// here.  A chain that ends a unit dirty continues into the buffer's next unit.
+// Lane 0 runs the state machine; the wave scans for adds 64 positions at a
+// time.  Everything is sequential FP64 in the reference's order.
+
+namespace upk {
+
+struct EmuParams {
+    const UnitDesc *units;
+    uint32_t nunits;
+    const int32_t *unit_buffer;
+    const uint32_t *unit_head;   // 1: unit has a head hit
+    int32_t S, nnc;
+    const int32_t *nc;
+    const uint8_t *is_control;
+    const double *coef;
+    int32_t ncoef;
+    const double *kern;
+    int32_t bw;
+    int32_t nondir;
+    double region_thr, kurt_thr, corr_thr, hit_thr;
+    int32_t want_corr;
+    uint32_t *resync;            // per unit: 0 untouched, X, or 0xFFFFFFFF
+    up_region *out;
+    uint32_t *out_counts;
+    uint32_t *nout;
+    uint32_t out_cap;
+    // scratch per buffer (index = buffer id)
+    uint32_t *ring_hits;         // [2][W][S]
+    double *reg_f, *reg_r;       // [2][reg_cap]
+    uint32_t *reg_hit;           // [2][reg_cap] index into reg_hits or 0xFFFFFFFF
+    uint32_t *reg_hits;          // [2][reg_cap][S]
+    uint32_t reg_cap;
+    uint32_t *err;               // nonzero: capacity exceeded / contract violated
+};
+
+struct EmuState {
+    // window: deque[j] = cell (head + j) % W
+    double *rf, *rr;      // LDS
+    uint8_t *rhas;        // LDS
+    uint32_t *rhits;      // global [W][S]
+    uint32_t W, head;
+    uint32_t buffer_pos, last_pos;
+    // open Region
+    uint32_t left, n, peak_pos;
+    double peak_score;
+    double *gf, *gr;
+    uint32_t *ghit, *ghits;
+    uint32_t nhits;
+    uint32_t cur_unit;
+    uint32_t close_pos;   // position of the add being processed, 0 during a flush
+    bool aligned;
+    uint64_t horizon;     // positions <= horizon may hold misaligned leftovers
+    bool resynced;
+};
+
+__device__ static const uint32_t *trk(const EmuParams &P, uint32_t u, int strand, int s) {
+    const UnitDesc &U = P.units[u];
+    return (const uint32_t *)U.base + ((uint64_t)strand * P.S + s) * U.stride + kPad;
+}
+
+// processRegion (peakcall.cpp:33-53) + Region statistics, appended to out
+__device__ static void emu_region(const EmuParams &P, EmuState &E) {
+    const int S = P.S;
+    uint32_t slot = atomicAdd(P.nout, 1u);
+    uint32_t sums_local[1];
+    (void)sums_local;
+    const bool keep = slot < P.out_cap;
+    if (!keep) atomicOr(P.err, 2u);
+    uint32_t nonctl = 0, total = 0;
+    for (int s = 0; s < S; ++s) {
+        uint32_t acc = 0;
+        for (uint32_t i = 0; i < E.n; ++i)
+            if (E.ghit[i] != 0xFFFFFFFFu) acc += E.ghits[(uint64_t)E.ghit[i] * S + s];
+        if (!P.is_control[s]) nonctl += acc;
+        total += acc;
+        if (keep) P.out_counts[(uint64_t)slot * S + s] = acc;
+    }
+    // posMean / posKurtosis with a UShort position index (data.cpp:133-182)
+    uint32_t count = 0, psum = 0;
+    uint16_t pos = 0;
+    for (uint32_t i = 0; i < E.n; ++i, ++pos)
+        if (E.ghit[i] != 0xFFFFFFFFu) {
+            uint32_t pc = 0;
+            for (int s = 0; s < S; ++s) pc += E.ghits[(uint64_t)E.ghit[i] * S + s];
+            count += pc;
+            psum += pc * (uint32_t)pos;
+        }
+    const double x_bar = (double)psum / (double)count;
+    double sum2 = 0.0, sum4 = 0.0;
+    pos = 0;
+    for (uint32_t i = 0; i < E.n; ++i, ++pos)
+        if (E.ghit[i] != 0xFFFFFFFFu) {
+            uint32_t pc = 0;
+            for (int s = 0; s < S; ++s) pc += E.ghits[(uint64_t)E.ghit[i] * S + s];
+            const double d = (double)pos - x_bar;
+            const double d2 = d * d;
+            sum2 = sum2 + (double)pc * d2;
+            sum4 = sum4 + (double)pc * (d2 * d2);
+        }
+    const double kurt = ((double)count - 1) * sum4 / (sum2 * sum2);
+    double corr = __builtin_nan("");
+    if (P.want_corr && E.n > 3) {
+        const uint32_t m = E.n;
+        double s1 = 0.0, s2 = 0.0;
+        for (uint32_t i = 0; i < m; ++i) s1 = s1 + E.gf[i];
+        for (uint32_t i = 0; i < m; ++i) s2 = s2 + E.gr[i];
+        const double m1 = s1 / (double)m, m2 = s2 / (double)m;
+        double q1 = 0.0, q2 = 0.0, q3 = 0.0;
+        for (uint32_t i = 0; i < m; ++i) { const double d = E.gf[i] - m1; q1 = q1 + d * d; }
+        for (uint32_t i = 0; i < m; ++i) { const double d = E.gr[i] - m2; q2 = q2 + d * d; }
+        const double sd1 = sqrt(q1 / ((double)m - 1)), sd2 = sqrt(q2 / ((double)m - 1));
+        for (uint32_t i = 0; i < m; ++i) q3 = q3 + (E.gf[i] - m1) * (E.gr[i] - m2);
+        corr = q3 / (((double)m - 1) * sd1 * sd2);
+    }
+    bool acc = (double)nonctl >= P.hit_thr;
+    if (acc) acc = P.kurt_thr == 0 || (E.n > 1 && kurt <= P.kurt_thr);
+    if (acc) acc = P.corr_thr <= -1 || corr >= P.corr_thr;
+    if (keep) {
+        up_region &o = P.out[slot];
+        o.unit = E.cur_unit;
+        o.left = E.left;
+        o.right = E.left + E.n - 1;
+        o.peak = E.peak_pos;
+        o.sum = total;
+        o.nonctl_sum = nonctl;
+        o.accepted = acc;
+        o.close_pos = E.close_pos;
+        o.peak_score = E.peak_score;
+        o.kurtosis = kurt;
+        o.corr = corr;
+    }
+    E.left = 0;
+    E.n = 0;
+    E.nhits = 0;
+    E.peak_pos = 0;
+    E.peak_score = 0.0;
+}
+
+// Region::addPos (data.cpp:92-102); hits (cell index or none) are copied
+__device__ static void emu_addpos(const EmuParams &P, EmuState &E, int cell, double f, double r) {
+    if (E.n >= P.reg_cap) {
+        atomicOr(P.err, 1u);
+        return;
+    }
+    E.gf[E.n] = f;
+    E.gr[E.n] = r;
+    if (cell >= 0) {
+        const uint32_t h = E.nhits++;
+        for (int s = 0; s < P.S; ++s) E.ghits[(uint64_t)h * P.S + s] = E.rhits[(uint64_t)cell * P.S + s];
+        E.ghit[E.n] = h;
+    } else {
+        E.ghit[E.n] = 0xFFFFFFFFu;
+    }
+    E.n++;
+    const double score = f + r;
+    if (E.peak_pos == 0 || score > E.peak_score) {
+        E.peak_pos = E.left + E.n - 1;
+        E.peak_score = score;
+    }
+}
+
+// processPosition (peakcall.cpp:55-86) of the front cell
+__device__ static void emu_process(const EmuParams &P, EmuState &E, uint32_t pos, int cell) {
+    if (!(pos > E.last_pos)) atomicOr(P.err, 4u);
+    const double f = E.rf[cell], r = E.rr[cell];
+    const int hc = E.rhas[cell] ? cell : -1;
+    const double score = f + r;
+    if (pos == E.last_pos + 1) {
+        if (E.left != 0) {
+            if (score >= P.region_thr) emu_addpos(P, E, hc, f, r);
+            else emu_region(P, E);
+        } else if (score >= P.region_thr) {
+            E.left = pos;
+            emu_addpos(P, E, hc, f, r);
+        }
+    } else {
+        if (E.left != 0) emu_region(P, E);
+        if (score >= P.region_thr) emu_addpos(P, E, hc, f, r);
+    }
+    E.last_pos = pos;
+    // resync: aligned, leftovers retired, nothing open
+    if (E.aligned && (uint64_t)pos > E.horizon && E.n == 0) E.resynced = true;
+}
+
+// ProfileBuffer::add (peakcall.cpp:161-222) without the contig switch
+__device__ static void emu_add(const EmuParams &P, EmuState &E, const uint32_t *counts,
+                               uint32_t pos, bool forward) {
+    uint16_t n_static = (uint16_t)E.W;
+    if (pos <= E.buffer_pos + 2u * (uint32_t)P.bw) n_static = (uint16_t)(pos - E.buffer_pos);
+    if (E.buffer_pos != 0) {
+        for (uint16_t i = 0; i < n_static && !E.resynced; ++i) {
+            if (E.buffer_pos + i > (uint32_t)P.bw) {
+                const int cell = (int)E.head;
+                emu_process(P, E, E.buffer_pos + i - P.bw, cell);
+                E.rf[cell] = 0.0;
+                E.rr[cell] = 0.0;
+                E.rhas[cell] = 0;
+                E.head = (E.head + 1) % E.W;
+            }
+        }
+    }
+    if (E.resynced) return;
+    double cs = 0.0;
+    if (counts) {
+        if (P.ncoef == 0) {
+            for (int s = 0; s < P.S; ++s)
+                if (!P.is_control[s]) cs = cs + (double)counts[s];
+        } else {
+            int k = 0;
+            for (int s = 0; s < P.S && k < P.ncoef; ++s)
+                if (!P.is_control[s]) { cs = cs + (double)counts[s] * P.coef[k]; ++k; }
+            for (int s = 0; s < P.S; ++s)
+                if (!P.is_control[s]) cs = cs + (double)counts[s];
+        }
+    }
+    if (cs != 0.0) {
+        for (uint32_t j = 0; j < E.W; ++j) {
+            const uint32_t c = (E.head + j) % E.W;
+            if (forward) E.rf[c] = E.rf[c] + P.kern[j] * cs;
+            else E.rr[c] = E.rr[c] + P.kern[j] * cs;
+        }
+        const uint32_t c = (E.head + P.bw) % E.W;
+        if (E.rhas[c]) {
+            for (int s = 0; s < P.S; ++s) E.rhits[(uint64_t)c * P.S + s] += counts[s];
+        } else {
+            for (int s = 0; s < P.S; ++s) E.rhits[(uint64_t)c * P.S + s] = counts[s];
+            E.rhas[c] = 1;
+        }
+    }
+    E.buffer_pos = pos;
+}
+
+__global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
+    __shared__ double rf[2 * kMaxBw + 1], rr[2 * kMaxBw + 1];
+    __shared__ uint8_t rhas[2 * kMaxBw + 1];
+    __shared__ uint32_t cnt_buf[64 * 4];
+    __shared__ int stop_flag;
+    const int lane = threadIdx.x;
+    const int buffer = blockIdx.x;
+    const int S = P.S;
+    EmuState E;
+    E.W = 2 * P.bw + 1;
+    E.rf = rf;
+    E.rr = rr;
+    E.rhas = rhas;
+    E.rhits = P.ring_hits + (uint64_t)buffer * E.W * S;
+    E.gf = P.reg_f + (uint64_t)buffer * P.reg_cap;
+    E.gr = P.reg_r + (uint64_t)buffer * P.reg_cap;
+    E.ghit = P.reg_hit + (uint64_t)buffer * P.reg_cap;
+    E.ghits = P.reg_hits + (uint64_t)buffer * P.reg_cap * S;
+    (void)cnt_buf;
+
+    bool in_chain = false;
+    for (uint32_t u = 0; u < P.nunits; ++u) {
+        if (P.unit_buffer[u] != buffer) continue;
+        if (!in_chain) {
+            if (!P.unit_head[u]) continue;
+            // chain start: fresh buffer state (the previous unit ended clean)
+            if (lane == 0) {
+                for (uint32_t j = 0; j < E.W; ++j) { rf[j] = 0.0; rr[j] = 0.0; rhas[j] = 0; }
+                E.head = 0;
+                E.buffer_pos = 0;
+                E.last_pos = 0;
+                E.left = 0;
+                E.n = 0;
+                E.nhits = 0;
+                E.peak_pos = 0;
+                E.peak_score = 0.0;
+            }
+            in_chain = true;
+        }
+        if (lane == 0) {
+            E.cur_unit = u;  // contig switch relabels the open region (peakcall.cpp:164-168)
+            E.aligned = false;
+            E.horizon = ~0ull;
+            E.resynced = false;
+        }
+        const UnitDesc U = P.units[u];
+        const int nstr = U.nstrands;
+        if (lane == 0) stop_flag = 0;
+        __syncthreads();
+        // walk the unit's add() positions in order, 64 at a time
+        for (uint64_t base = 1; base <= U.len && !stop_flag; base += 64) {
+            const uint64_t p = base + lane;
+            uint32_t any0 = 0, any1 = 0;
+            if (p <= U.len) {
+                for (int s = 0; s < S; ++s) {
+                    any0 |= trk(P, u, 0, s)[p - 1];
+                    if (nstr == 2) any1 |= trk(P, u, 1, s)[p - 1];
+                }
+            }
+            const uint64_t m0 = __ballot(any0 != 0), m1 = __ballot(any1 != 0);
+            uint64_t m = m0 | m1;
+            if (lane == 0) {
+                while (m && !E.resynced) {
+                    const int b = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint32_t pos = (uint32_t)(base + b);
+                    for (int st = 0; st < 2 && !E.resynced; ++st) {
+                        if (!(((st ? m1 : m0) >> b) & 1)) continue;
+                        uint32_t counts[256];
+                        for (int s = 0; s < S; ++s) counts[s] = trk(P, u, nstr == 2 ? st : 0, s)[pos - 1];
+                        E.close_pos = pos;
+                        const bool first_aligned = !E.aligned && pos > (uint32_t)P.bw;
+                        emu_add(P, E, counts, pos, nstr == 2 ? st == 0 : P.unit_buffer[u] == 0);
+                        if (first_aligned) {
+                            E.aligned = true;
+                            E.horizon = (uint64_t)pos + P.bw;
+                        }
+                    }
+                }
+                if (E.resynced) stop_flag = 1;
+            }
+            __syncthreads();
+        }
+        if (lane == 0) {
+            if (E.resynced) {
+                P.resync[u] = E.last_pos + 1;
+            } else {
+                // explicit flushContig() at the end of the unit's pass
+                E.close_pos = 0;
+                emu_add(P, E, nullptr, E.buffer_pos + E.W, true);
+                E.buffer_pos = 0;
+                E.last_pos = 0;
+                P.resync[u] = 0xFFFFFFFFu;
+                bool clean = E.n == 0;
+                for (uint32_t j = 0; j < E.W && clean; ++j)
+                    clean = rf[j] == 0.0 && rr[j] == 0.0 && !rhas[j];
+                stop_flag = clean ? 1 : 0;
+            }
+            if (E.resynced) stop_flag = 1;
+        }
+        __syncthreads();
+        if (stop_flag) in_chain = false;
+        __syncthreads();
+    }
+}
+
+// head-hit detection: any pooled countSum != 0 at positions 1..bw
+template <int POOL>
+__global__ void head_detect_kernel(const UnitDesc *units, int S, int nnc, const int32_t *nc,
+                                   const double *coef, int bw, uint32_t *head) {
+    const UnitDesc U = units[blockIdx.x];
+    const int p = 1 + (int)threadIdx.x;
+    uint32_t hit = 0;
+    if (p <= bw && (uint32_t)p <= U.len) {
+        for (int st = 0; st < U.nstrands; ++st) {
+            const uint32_t *t = (const uint32_t *)U.base + (uint64_t)st * S * U.stride + kPad + p - 1;
+            double cs = 0.0;
+            for (int k = 0; k < nnc; ++k) {
+                const uint32_t c = t[(uint64_t)nc[k] * U.stride];
+                cs = POOL == 2 ? cs + (double)c * coef[k] : cs + (double)c;
+            }
+            if (POOL == 2)
+                for (int k = 0; k < nnc; ++k) cs = cs + (double)t[(uint64_t)nc[k] * U.stride];
+            if (cs != 0.0) hit = 1;
+        }
+    }
+    if (__syncthreads_or(hit) && threadIdx.x == 0) head[blockIdx.x] = 1;
+}
+
+}  // namespace upk

@@ -685,7 +685,7 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             o->sum = count;
             o->nonctl_sum = nonctl;
             o->accepted = acc;
-            o->reserved = 0;
+            o->close_pos = UP_CLOSE_RULE;
             o->peak_score = best;
             o->kurtosis = kurt;
             o->corr = corr;

@@ -121,27 +121,44 @@ void run_units(const EngineParams &ep, PassResult &out) {
     if (ndev < 1) fatal("no HIP device available (the GPU path has no CPU fallback)");
     if (ep.ngpus > 0 && ep.ngpus < ndev) ndev = ep.ngpus;
     const size_t S = ep.p.n_samples;
-    for (const UnitBuild &u : out.units)
-        if (u.head_hit)
-            fatal("tags within the first bandwidth positions of a contig (quirk Q1) are not "
-                  "supported on the GPU path yet");
-    // LPT assignment of units to devices by track bytes
+    // Quirk Q1: a unit whose adds all sit at positions <= bw leaves density
+    // (and maybe an open region) in its buffer after flushContig(); the
+    // library replays such chains, so a chain's units share one device.
+    // group[i] = first unit of the chain unit i belongs to.
+    std::vector<uint32_t> group(out.units.size());
+    {
+        int32_t open_prev[2] = {-1, -1};
+        for (uint32_t i = 0; i < out.units.size(); ++i) {
+            const UnitBuild &u = out.units[i];
+            const int b = u.buffer;
+            const bool linked = open_prev[b] >= 0;
+            group[i] = linked ? group[open_prev[b]] : i;
+            const bool in_chain = u.head_hit || linked;
+            const bool leaks = !u.add_pos.empty() && u.add_pos.back() <= ep.p.bw;
+            open_prev[b] = (in_chain && leaks) ? (int32_t)i : -1;
+        }
+    }
+    // LPT assignment of unit groups to devices by track bytes
     const int nstr = ep.p.nondir ? 2 : 1;
-    std::vector<uint32_t> order(out.units.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = (uint32_t)i;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-        return out.units[a].len > out.units[b].len;
-    });
+    std::vector<uint64_t> gbytes(out.units.size(), 0);
+    for (uint32_t i = 0; i < out.units.size(); ++i)
+        gbytes[group[i]] += (uint64_t)out.units[i].len * nstr * S;
+    std::vector<uint32_t> order;
+    for (uint32_t i = 0; i < out.units.size(); ++i)
+        if (group[i] == i) order.push_back(i);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return gbytes[a] > gbytes[b]; });
     std::vector<uint64_t> load(ndev, 0);
+    std::vector<int> gdev(out.units.size(), 0);
     g_jobs.assign(ndev, DeviceJob());
     for (int d = 0; d < ndev; ++d) g_jobs[d].dev = d;
-    for (uint32_t i : order) {
+    for (uint32_t g : order) {
         int best = 0;
         for (int d = 1; d < ndev; ++d)
             if (load[d] < load[best]) best = d;
-        load[best] += (uint64_t)out.units[i].len * nstr * S;
-        g_jobs[best].units.push_back(i);
+        load[best] += gbytes[g];
+        gdev[g] = best;
     }
+    for (uint32_t i = 0; i < out.units.size(); ++i) g_jobs[gdev[group[i]]].units.push_back(i);
     for (auto &j : g_jobs) std::sort(j.units.begin(), j.units.end());  // buffer order kept
 
     std::mutex mu;
@@ -211,8 +228,10 @@ std::vector<Emitted> order_candidates(const PassResult &out, uint16_t bw, bool a
     const uint64_t last_write = out.write_times.empty() ? 0 : out.write_times.back();
     for (const Candidate &c : out.cands) {
         const UnitBuild &u = out.units[c.unit_index];
-        // closed by the first add at pos >= right + bw + 2, else by the flush
-        const uint64_t key = (uint64_t)c.r.right + bw + 2;
+        // closed by the first add at pos >= right + bw + 2, else by the flush;
+        // regions from the Q1 replay name their closing add (0: the flush)
+        uint64_t key = (uint64_t)c.r.right + bw + 2;
+        if (c.r.close_pos != UP_CLOSE_RULE) key = c.r.close_pos ? c.r.close_pos : ~0ull;
         auto it = std::lower_bound(u.add_pos.begin(), u.add_pos.end(), key,
                                    [](uint32_t a, uint64_t k) { return (uint64_t)a < k; });
         const uint64_t t = it != u.add_pos.end() ? u.add_time[it - u.add_pos.begin()] : u.flush_time;
