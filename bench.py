@@ -9,11 +9,13 @@ the device (DESIGN.md "Synthetic input"), already resident in HBM.
 One step = the whole hot path over the genome: RCCL all-reduce of the tag
 totals -> background -> K1 scan (pool + KDE + flags + run boundaries) ->
 K2 segmentation -> K3 region statistics + filters -> region records on the
-host -> (N>1) gather of the records to rank 0 -> reference emission order.
+host (pinned) -> (N>1) gather of the records to rank 0 -> records concatenated
+in global unit order.
 
 Multi-GPU: one process per GPU (torchrun); the 50 (contig, strand) units are
-LPT-assigned to ranks (strong scaling: the genome is fixed), so there is no
-data-path collective besides the background all-reduce and the record gather.
+LPT-assigned to ranks by unipeak_amd/shard.py (strong scaling: the genome is
+fixed), so there is no data-path collective besides the RCCL background
+all-reduce and the RCCL gather of the fixed-size region records to rank 0.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
 the roofline of the dominant kernel (K1) and the oracle CPU baseline.
@@ -29,7 +31,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from unipeak_amd import capi  # noqa: E402
+from unipeak_amd import capi, shard  # noqa: E402
 
 METRIC = "genome Gbp/s for KDE smoothing + region scan on hg19, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -44,15 +46,17 @@ def read_contigs(path):
     return out
 
 
-def lpt(sizes, n):
-    order = sorted(range(len(sizes)), key=lambda i: -sizes[i])
-    load = [0] * n
-    owner = [0] * len(sizes)
-    for i in order:
-        r = min(range(n), key=lambda k: load[k])
-        owner[i] = r
-        load[r] += sizes[i]
-    return owner
+def pmc_traffic(bytes_per_launch):
+    """HBM bytes per K1 launch from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py) when they were taken on this exact workload."""
+    p = os.path.join(ROOT, "profiles", "r01", "k1_pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        return None, None
+    if int(d.get("algorithmic_bytes_per_launch", -1)) != int(bytes_per_launch):
+        return None, None
+    return round(d["traffic_bytes_per_launch"] / 1e9, 3), os.path.relpath(p, ROOT)
 
 
 def main():
@@ -69,71 +73,62 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    comm = None
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-        gloo = dist.new_group(backend="gloo")
+        dist.init_process_group("nccl")  # RCCL over xGMI
+        comm = shard.Comm(dist, rank, world, f"cuda:{local}")
 
     contigs = read_contigs(os.path.join(ROOT, "unipeak_amd", "data", "hg19.txt"))
     genome = sum(L for _, L in contigs)
-    # directional units: forward buffer over every contig, then reverse
-    units = [(ci, st) for st in (0, 1) for ci in range(len(contigs))]
-    owner = lpt([contigs[ci][1] for ci, _ in units], world)
-    mine = [k for k in range(len(units)) if owner[k] == rank]
+    lens = [L for _, L in contigs]
+    units, owner, mine_all = shard.plan(lens, nondir=False, world=world)
+    mine = mine_all[rank]
 
     g = capi.Lib(local)
     g.set_params(args.bw, 1, 0.0029)  # background is replaced every step
-    uid = {}
     t_gen = time.time()
-    for k in mine:
+    for k in mine:  # ascending global order: records come back unit-major
         ci, st = units[k]
-        u = g.add_unit(contigs[ci][1], buffer_id=st)
+        u = g.add_unit(lens[ci], buffer_id=st)
         g.synth(u, 0, 0, args.seed, ci, st, nondir=False, peaks=True)
-        uid[k] = u
-    local_tags = sum(g.tag_total(uid[k], 0, 0) for k in mine)
+    local_tags = sum(g.tag_total(i, 0, 0) for i in range(len(mine)))
     gen_s = time.time() - t_gen
-    alg_bytes = 4 * 1 * sum(contigs[units[k][0]][1] for k in mine)  # uint32 per bp per strand
+    alg_bytes = 4 * 1 * sum(lens[units[k][0]] for k in mine)  # uint32 per bp per strand
+
+    phase = {"allreduce": 0.0, "run": 0.0, "gather_merge": 0.0}
 
     def step():
-        tags = local_tags
-        if dist is not None:
-            import torch
-            t = torch.tensor([tags], dtype=torch.int64, device=f"cuda:{local}")
-            dist.all_reduce(t)  # RCCL: the global background (regions.cpp:205-213)
-            tags = int(t.item())
-        background = tags / genome / 2  # directional: per strand
+        t0 = time.perf_counter()
+        tags = comm.global_tags(local_tags) if comm else local_tags
+        background = tags / genome / 2  # directional: per strand (regions.cpp:205-213)
         g.set_params(args.bw, 1, background, region_thr=25.0, kurt_thr=50.0,
                      corr_thr=-1.0, hit_thr=10.0)
+        t1 = time.perf_counter()
         n = g.run()
-        regs, cnt = g.regions(n)
-        t = g.timings()
-        if dist is not None:
-            gathered = [None] * world if rank == 0 else None
-            dist.gather_object((regs.tobytes(), [units[k] for k in mine]), gathered, dst=0,
-                               group=gloo)
-        if rank == 0:
-            # reference emission order: forward pass over contigs, then reverse;
-            # ascending within a unit (regions.cpp:311-391)
-            if dist is None:
-                parts = [(regs, np.array([units[k] for k in mine], np.int64).reshape(-1, 2))]
-            else:
-                parts = [(np.frombuffer(blob, capi.REGION_DTYPE),
-                          np.array(ulist, np.int64).reshape(-1, 2)) for blob, ulist in gathered]
-            contig = np.concatenate([u[r["unit"], 0] for r, u in parts])
-            strand = np.concatenate([u[r["unit"], 1] for r, u in parts])
-            left = np.concatenate([r["left"] for r, _ in parts])
-            acc = np.concatenate([r["accepted"] for r, _ in parts])
-            order = np.lexsort((left, contig, strand))
-            npass = int(acc[order].sum())
-            return n, npass, t
-        return n, None, t
+        regs, cnt = g.regions_view()
+        t2 = time.perf_counter()
+        if comm is not None:
+            parts = comm.gather_records(regs, cnt)
+            if parts is not None:
+                parts = [(r, mine_all[i], e) for i, (r, e) in enumerate(parts)]
+        else:
+            parts = [(regs, mine, cnt)]
+        res = None
+        if parts is not None:
+            recs, gid, _ = shard.merge(parts, len(units), capi.REGION_DTYPE)
+            res = (len(recs), int(np.count_nonzero(recs["accepted"])))
+        t3 = time.perf_counter()
+        phase["allreduce"] += t1 - t0
+        phase["run"] += t2 - t1
+        phase["gather_merge"] += t3 - t2
+        return n, res, g.timings()
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        if comm is not None:
+            comm.dist.barrier()
 
     for _ in range(args.warmup):
         st = step()
@@ -141,6 +136,8 @@ def main():
             tt = st[2]
             print(f"[bench] warmup: K1 {tt[0]:.3f} ms, K2 {tt[1]:.3f} ms, K3 {tt[2]:.3f} ms, "
                   f"up_run wall {tt[3]:.3f} ms", file=sys.stderr, flush=True)
+    for k in phase:
+        phase[k] = 0.0
     barrier()
     t0 = time.perf_counter()
     k1 = []
@@ -150,26 +147,20 @@ def main():
         k1.append(last[2][0])
     barrier()
     dt = (time.perf_counter() - t0) / args.steps
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        kk = torch.tensor([float(np.mean(k1)), float(alg_bytes)], dtype=torch.float64,
-                          device=f"cuda:{local}")
-        allk = [torch.zeros_like(kk) for _ in range(world)]
-        dist.all_gather(allk, kk)
-        k1_ms = max(float(a[0]) for a in allk)
-        k1_bytes = sum(float(a[1]) for a in allk)
+    k1_ms = float(np.mean(k1))
+    my_achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
+    if comm is not None:
+        dt = comm.max_over_ranks(dt)
+        achieved = comm.sum_over_ranks(my_achieved) / world  # mean per-GPU K1 GB/s
+        k1_max = comm.max_over_ranks(k1_ms)
     else:
-        k1_ms = float(np.mean(k1))
-        k1_bytes = float(alg_bytes)
+        achieved, k1_max = my_achieved, k1_ms
 
     if rank == 0:
+        print("[bench] per-step phases (ms): " + ", ".join(
+            f"{k} {v / args.steps * 1e3:.3f}" for k, v in phase.items()), file=sys.stderr, flush=True)
         value = genome / dt / 1e9
-        # roofline of K1: algorithmic bytes (4 B per bp per strand per
-        # non-control sample) over the slowest rank's K1 time
-        achieved = k1_bytes / (k1_ms * 1e-3) / 1e9 / world
+        traffic, traffic_src = pmc_traffic(alg_bytes) if world == 1 else (None, None)
         res = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -182,25 +173,29 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (device-generated hg19-shaped tag counts, DESIGN.md)",
+            "data": "synthetic (device-generated hg19-shaped tag counts, DESIGN.md §8)",
             "config": {"workload": "hg19 full genome, 1 directional sample (3SEQ-style), "
                                    "bw 50, -r 25 -k 50 -t 10 (BASELINE configs[1])",
                        "genome_bp": genome, "units": len(units),
                        "parallelism": f"contig-strand units LPT over {world} GPU(s)"},
-            "regions": {"candidates": int(last[0]), "accepted": int(last[1])},
+            "regions": {"candidates": int(last[1][0]), "accepted": int(last[1][1])},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "traffic_unit": "GB per launch (rocprofv3 PMC, gfx950-corrected)",
+                         "traffic_source": traffic_src,
                          "kernel": "scan_kernel (K1)", "k1_ms": round(k1_ms, 4),
-                         "bytes_per_launch": int(k1_bytes / world)},
+                         "k1_ms_max_rank": round(k1_max, 4),
+                         "bytes_per_launch": int(alg_bytes)},
             "setup_s": round(gen_s, 2),
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(contigs, args, value)
         print(json.dumps(res), flush=True)
     g.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.dist.destroy_process_group()
 
 
 def cpu_baseline(contigs, args, gpu_value):

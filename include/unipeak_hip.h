@@ -140,6 +140,10 @@ int up_run(up_ctx *ctx, uint64_t *n_regions);
 /* Copy region records (unit-major, left-ascending) and optionally the
  * per-sample exptSums [n][S]. */
 int up_get_regions(up_ctx *ctx, up_region *out, uint32_t *counts, size_t cap);
+/* Zero-copy view of the same records: host memory owned by the context
+ * (pinned), valid until the next up_run / up_reset_units / up_close. */
+int up_regions_view(up_ctx *ctx, const up_region **regions, const uint32_t **counts,
+                    uint64_t *n);
 
 /* strandCorr(shift) for shift = 0..max_shift of the given regions
  * (indices into up_get_regions order); out is [n][max_shift+1]. */

@@ -1,0 +1,144 @@
+"""Multi-rank layout of the scan (unipeak_amd/shard.py) on CPU: the LPT plan,
+the rank-0 merge, and the two collectives of a step over gloo with
+world_size 2 (the same calls run over RCCL in bench.py on GPUs)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from unipeak_amd import shard
+from unipeak_amd.capi import REGION_DTYPE
+
+HG19 = [int(l.split()[1]) for l in open(os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "unipeak_amd", "data", "hg19.txt"))
+    if l.strip() and not l.startswith("#")]
+
+
+def test_units_follow_reference_pass_order():
+    assert shard.units_for([5, 7], nondir=True) == [(0, 0), (1, 0)]
+    assert shard.units_for([5, 7], nondir=False) == [(0, 0), (1, 0), (0, 1), (1, 1)]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_lpt_plan_covers_every_unit_once(world):
+    units, owner, mine = shard.plan(HG19, nondir=False, world=world)
+    assert len(units) == 2 * len(HG19)
+    assert sorted(k for m in mine for k in m) == list(range(len(units)))
+    for m in mine:
+        assert m == sorted(m)
+    loads = [sum(HG19[units[k][0]] for k in m) for m in mine]
+    # LPT bound: max load <= total/world + largest unit
+    assert max(loads) <= sum(loads) / world + max(HG19)
+    if world == 8:  # static balance bounds the directional speed-up at 7.94x
+        assert sum(loads) / max(loads) > 7.9
+
+
+def fake_records(rng, n_units, per_unit_max=6):
+    recs, counts = [], []
+    for u in range(n_units):
+        k = int(rng.integers(0, per_unit_max))
+        left = np.sort(rng.choice(np.arange(1, 10_000), k, replace=False)).astype(np.uint32)
+        r = np.zeros(k, REGION_DTYPE)
+        r["unit"] = u
+        r["left"] = left
+        r["right"] = left + 10
+        r["sum"] = rng.integers(1, 100, k)
+        r["peak_score"] = rng.random(k)
+        recs.append(r)
+        counts.append(rng.integers(0, 50, (k, 3)).astype(np.uint32))
+    return np.concatenate(recs), np.concatenate(counts)
+
+
+def split_by_owner(recs, counts, mine):
+    parts = []
+    for gids in mine:
+        sel = np.isin(recs["unit"], gids)
+        r = recs[sel].copy()
+        remap = {g: i for i, g in enumerate(gids)}
+        r["unit"] = [remap[int(g)] for g in r["unit"]]
+        parts.append((r, gids, counts[sel]))
+    return parts
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_merge_restores_global_unit_order(world):
+    rng = np.random.default_rng(world)
+    n_units = 50
+    recs, counts = fake_records(rng, n_units)
+    owner, _ = shard.lpt([int(x) for x in rng.integers(1, 1000, n_units)], world)
+    mine = [[k for k in range(n_units) if owner[k] == r] for r in range(world)]
+    got, gid, cnt = shard.merge(split_by_owner(recs, counts, mine), n_units, REGION_DTYPE)
+    assert np.array_equal(gid, recs["unit"].astype(np.int64))
+    for f in ("left", "right", "sum", "peak_score"):
+        assert np.array_equal(got[f], recs[f])
+    assert np.array_equal(cnt, counts)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = shard.Comm(dist, rank, world, "cpu")
+        rng = np.random.default_rng(7)
+        recs, counts = fake_records(rng, 20)
+        tags = [int(x) for x in rng.integers(1, 10**9, 20)]
+        owner, _ = shard.lpt(tags, world)
+        mine = [[k for k in range(20) if owner[k] == r] for r in range(world)]
+        local = sum(tags[k] for k in mine[rank])
+        total = comm.global_tags(local)
+        part = split_by_owner(recs, counts, mine)[rank]
+        gathered = comm.gather_records(part[0], part[2])
+        mx = comm.max_over_ranks(rank + 0.5)
+        if rank == 0:
+            parts = [(r, mine[i], e) for i, (r, e) in enumerate(gathered)]
+            got, gid, cnt = shard.merge(parts, 20, REGION_DTYPE)
+            ok = (total == sum(tags) and mx == world - 0.5
+                  and np.array_equal(gid, recs["unit"].astype(np.int64))
+                  and np.array_equal(got["left"], recs["left"])
+                  and np.array_equal(got["peak_score"], recs["peak_score"])
+                  and np.array_equal(cnt, counts))
+            with open(os.path.join(out_dir, "result"), "w") as f:
+                f.write("ok" if ok else f"mismatch total={total} mx={mx}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_collectives_world2(tmp_path, world):
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert (tmp_path / "result").read_text() == "ok"
+
+
+def test_gloo_empty_rank(tmp_path):
+    """a rank that owns no regions still takes part in both collectives"""
+    import torch.multiprocessing as mp
+    mp.spawn(_empty_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert (tmp_path / "result").read_text() == "ok"
+
+
+def _empty_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = shard.Comm(dist, rank, world, "cpu")
+        recs = np.zeros(3 if rank == 0 else 0, REGION_DTYPE)
+        recs["left"] = [5, 6, 7][:len(recs)]
+        g = comm.gather_records(recs, None)
+        if rank == 0:
+            ok = len(g) == 2 and len(g[1][0]) == 0 and list(g[0][0]["left"]) == [5, 6, 7]
+            with open(os.path.join(out_dir, "result"), "w") as f:
+                f.write("ok" if ok else "bad")
+    finally:
+        dist.destroy_process_group()

@@ -66,8 +66,8 @@ EXPORTS = [
     "up_version", "up_strerror", "up_device_count", "up_kernel_weights", "up_open",
     "up_close", "up_set_params", "up_add_unit", "up_unit_count", "up_unit_ptr",
     "up_unit_scatter", "up_unit_synth", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
-    "up_reset_units", "up_run", "up_get_regions", "up_shift_scan", "up_timings",
-    "up_unit_profile",
+    "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan",
+    "up_timings", "up_unit_profile",
 ]
 
 
@@ -102,6 +102,7 @@ def load_library(path=LIB_PATH):
         "up_reset_units": (c.c_int, [vp]),
         "up_run": (c.c_int, [vp, c.POINTER(c.c_uint64)]),
         "up_get_regions": (c.c_int, [vp, vp, vp, c.c_size_t]),
+        "up_regions_view": (c.c_int, [vp, c.POINTER(vp), c.POINTER(vp), c.POINTER(c.c_uint64)]),
         "up_shift_scan": (c.c_int, [vp, vp, c.c_size_t, c.c_uint16, vp]),
         "up_timings": (c.c_int, [vp, vp, c.c_int]),
         "up_unit_profile": (c.c_int, [vp, c.c_uint32, vp, vp, c.c_uint32]),
@@ -223,6 +224,20 @@ class Lib:
         _ck(self.L.up_get_regions(self.ctx, out.ctypes.data,
                                   cnt.ctypes.data if cnt is not None else None, n))
         return out, cnt
+
+    def regions_view(self):
+        """(records, counts) as numpy views of the context's pinned host copy;
+        valid until the next run()."""
+        r, k, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        _ck(self.L.up_regions_view(self.ctx, ctypes.byref(r), ctypes.byref(k), ctypes.byref(n)))
+        n = n.value
+        if n == 0:
+            return np.zeros(0, REGION_DTYPE), np.zeros((0, self.S), np.uint32)
+        regs = np.frombuffer((ctypes.c_char * (n * REGION_DTYPE.itemsize)).from_address(r.value),
+                             REGION_DTYPE)
+        cnt = np.frombuffer((ctypes.c_char * (n * self.S * 4)).from_address(k.value),
+                            np.uint32).reshape(n, self.S)
+        return regs, cnt
 
     def shift_scan(self, idx, max_shift):
         idx = np.ascontiguousarray(idx, np.uint64)

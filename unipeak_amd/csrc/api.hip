@@ -54,6 +54,28 @@ struct DevBuf {
     }
 };
 
+// pinned host staging (results always end on the host)
+template <typename T>
+struct HostBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        size_t cap = want < 16 ? 16 : want + want / 4;
+        hipError_t e = hipHostMalloc((void **)&p, cap * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = cap;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
 }  // namespace
 
 struct up_ctx {
@@ -94,6 +116,8 @@ struct up_ctx {
     std::vector<uint32_t> h_counts;
     std::vector<uint8_t> h_emulated;
     std::vector<uint32_t> h_head;
+    HostBuf<up_region> hp_regions;
+    HostBuf<uint32_t> hp_counts;
 };
 
 #define HIPCHK(x)                                                                   \
@@ -185,6 +209,7 @@ void up_close(up_ctx *c) {
     c->d_head.release(); c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
+    c->hp_regions.release(); c->hp_counts.release();
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -646,16 +671,14 @@ static int replay_head_hits(up_ctx *c) {
         fprintf(stderr, "unipeak_hip: head-hit replay failed (flags %u)\n", err);
         return err & 4u ? UP_E_ARG : UP_E_NOMEM;
     }
-    std::vector<up_region> emu(nemu), par(c->nreg);
-    std::vector<uint32_t> ecnt((size_t)nemu * S), pcnt((size_t)c->nreg * S);
+    std::vector<up_region> emu(nemu);
+    std::vector<uint32_t> ecnt((size_t)nemu * S);
     if (nemu) {
         HIPCHK(hipMemcpy(emu.data(), c->d_emu_out.p, nemu * sizeof(up_region), hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(ecnt.data(), c->d_emu_counts.p, ecnt.size() * 4, hipMemcpyDeviceToHost));
     }
-    if (c->nreg) {
-        HIPCHK(hipMemcpy(par.data(), c->d_regions.p, c->nreg * sizeof(up_region), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(pcnt.data(), c->d_counts.p, pcnt.size() * 4, hipMemcpyDeviceToHost));
-    }
+    const up_region *par = c->hp_regions.p;  // staged by up_run
+    const uint32_t *pcnt = c->hp_counts.p;
     // merge: unit-major; within a unit the replayed regions, then the
     // parallel ones that start at or after the resync position
     std::vector<std::pair<uint64_t, int64_t>> keys;  // (unit<<32 | order, +par idx / -emu idx-1)
@@ -681,7 +704,7 @@ static int replay_head_hits(up_ctx *c) {
         } else {
             const uint64_t i = (uint64_t)k.second;
             c->h_regions.push_back(par[i]);
-            c->h_counts.insert(c->h_counts.end(), pcnt.begin() + i * S, pcnt.begin() + (i + 1) * S);
+            c->h_counts.insert(c->h_counts.end(), pcnt + i * S, pcnt + (i + 1) * S);
             c->h_emulated.push_back(0);
         }
     }
@@ -769,6 +792,14 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     c->unit_last.resize(c->units.size());
     HIPCHK(hipMemcpyAsync(c->unit_last.data(), c->d_unit_last.p, c->units.size() * 4,
                           hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c->hp_regions.ensure(nreg + 1));
+    HIPCHK(c->hp_counts.ensure((nreg + 1) * c->p.n_samples));
+    if (nreg) {
+        HIPCHK(hipMemcpyAsync(c->hp_regions.p, c->d_regions.p, nreg * sizeof(up_region),
+                              hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->hp_counts.p, c->d_counts.p, nreg * c->p.n_samples * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     if ((r = replay_head_hits(c))) return r;
     float a = 0, b = 0, d = 0;
@@ -785,21 +816,28 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
 }
 
 int up_get_regions(up_ctx *c, up_region *out, uint32_t *counts, size_t cap) {
-    if (!c) return UP_E_ARG;
+    const up_region *r = nullptr;
+    const uint32_t *k = nullptr;
+    uint64_t nreg = 0;
+    int rc = up_regions_view(c, &r, &k, &nreg);
+    if (rc) return rc;
+    const size_t n = nreg < cap ? (size_t)nreg : cap;
+    if (n && out) std::memcpy(out, r, n * sizeof(up_region));
+    if (n && counts) std::memcpy(counts, k, n * c->p.n_samples * sizeof(uint32_t));
+    return UP_OK;
+}
+
+int up_regions_view(up_ctx *c, const up_region **regions, const uint32_t **counts, uint64_t *n) {
+    if (!c || !regions || !n) return UP_E_ARG;
     if (!c->ran) return UP_E_STATE;
-    const size_t n = c->nreg < cap ? (size_t)c->nreg : cap;
+    *n = c->nreg;
     if (c->host_regions) {
-        if (n && out) std::memcpy(out, c->h_regions.data(), n * sizeof(up_region));
-        if (n && counts) std::memcpy(counts, c->h_counts.data(), n * c->p.n_samples * sizeof(uint32_t));
-        return UP_OK;
+        *regions = c->h_regions.data();
+        if (counts) *counts = c->h_counts.data();
+    } else {
+        *regions = c->hp_regions.p;
+        if (counts) *counts = c->hp_counts.p;
     }
-    HIPCHK(hipSetDevice(c->dev));
-    if (n && out)
-        HIPCHK(hipMemcpyAsync(out, c->d_regions.p, n * sizeof(up_region), hipMemcpyDeviceToHost, c->stream));
-    if (n && counts)
-        HIPCHK(hipMemcpyAsync(counts, c->d_counts.p, n * c->p.n_samples * sizeof(uint32_t),
-                              hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
     return UP_OK;
 }
 
