@@ -96,7 +96,9 @@ def main():
         g.synth(u, 0, 0, args.seed, ci, st, nondir=False, peaks=True)
     local_tags = sum(g.tag_total(i, 0, 0) for i in range(len(mine)))
     gen_s = time.time() - t_gen
-    alg_bytes = 4 * 1 * sum(lens[units[k][0]] for k in mine)  # uint32 per bp per strand
+    # K1 algorithmic bytes: one uint8 count per bp per strand per non-control
+    # sample
+    alg_bytes = 1 * 1 * sum(lens[units[k][0]] for k in mine)
 
     phase = {"allreduce": 0.0, "run": 0.0, "gather_merge": 0.0}
 

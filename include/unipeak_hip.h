@@ -22,7 +22,7 @@
  *
  *   up_kernel_weights   <- Kernel::Kernel            misc/kernel.cpp:16-35
  *   up_open/up_set_params <- ProfileBuffer ctor      misc/peakcall.cpp:88-135
- *   up_add_unit + up_unit_scatter (or up_unit_ptr)
+ *   up_add_unit + up_unit_scatter (or up_unit_pack)
  *                        <- the add() calls of one unit misc/peakcall.cpp:161-222
  *   up_run              <- add()'s window scatter + processPosition +
  *                          processRegion + flushContig  misc/peakcall.cpp:33-86,224-231
@@ -108,8 +108,10 @@ int up_set_params(up_ctx *ctx, const up_params *p);
 /* Units.  A unit is one ProfileBuffer (buffer_id 0 = forward buffer, 1 =
  * reverse buffer) over one contig pass; units of one buffer must be added in
  * the order the buffer sees them.  nstrands is 1 (directional) or 2
- * (nondirectional: strand 0 forward, 1 reverse).  Count tracks are zeroed
- * uint32 arrays covering positions 1..contig_len.
+ * (nondirectional: strand 0 forward, 1 reverse).  Tracks start zeroed and
+ * cover positions 1..contig_len; in device memory they are uint8 counts with
+ * an exact overflow table for counts >= 255 (DESIGN.md "Data layout"), so
+ * any uint32 count can be written.
  * Quirk Q1 (misc/peakcall.cpp:177-183): a unit with pooled tags at a position
  * <= bw is replayed by the exact state machine; if all of its adds sit at
  * positions <= bw its leftover state leaks into the buffer's NEXT unit, which
@@ -117,9 +119,10 @@ int up_set_params(up_ctx *ctx, const up_params *p);
 int up_add_unit(up_ctx *ctx, uint32_t contig_len, int32_t nstrands,
                 int32_t buffer_id, uint32_t *unit_id);
 int up_unit_count(up_ctx *ctx, uint32_t *n);
-/* device pointer to the track: position p (1-based) lives at ptr[p-1] */
-int up_unit_ptr(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
-                uint32_t **dev_ptr);
+/* replace a track from DEVICE-resident dense uint32 counts: position p
+ * (1-based) at dev_counts[p-1], contig_len elements (same device) */
+int up_unit_pack(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
+                 const uint32_t *dev_counts);
 /* write n (pos, count) host pairs (positions 1..len, unique) into a track */
 int up_unit_scatter(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
                     size_t n, const uint32_t *pos, const uint32_t *counts);

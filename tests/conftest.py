@@ -34,6 +34,11 @@ def orc_bin():
 
 @pytest.fixture(scope="session")
 def gpu_lib():
+    # torch's bundled HIP runtime must initialise before the system runtime
+    # our library links, or torch sees no GPU (tools/mix_probe.py)
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     from unipeak_amd import capi
     capi.load_library()  # raises loudly if the HIP library is missing
     if capi.device_count() < 1:

@@ -1,0 +1,139 @@
+"""The uint8 track layout and K1's integer screen against
+the oracle: counts >= 128 (screen escape) and >= 255 (overflow table) at
+peaks and in the background, thresholds from "almost everything is a region"
+to "almost nothing is", every bandwidth class of the screen window, scaled
+pooling with large and negative coefficients, and device-resident input
+through up_unit_pack."""
+import numpy as np
+import pytest
+
+from tests.gen import random_unit
+from tests.test_gpu_unit import compare, run_gpu, close
+
+pytestmark = pytest.mark.gpu
+
+
+def with_big_counts(rng, pos, cnt, n, lo, hi):
+    """add n positions holding counts in [lo, hi) (merged into pos/cnt)"""
+    dense = {int(p): c.copy() for p, c in zip(pos, cnt)}
+    S = cnt.shape[1]
+    for p in rng.choice(pos, size=min(n, len(pos)), replace=False):
+        v = np.zeros(S, np.uint32)
+        v[int(rng.integers(0, S))] = int(rng.integers(lo, hi))
+        dense[int(p)] = dense[int(p)] + v
+    p = np.array(sorted(dense), np.uint32)
+    return p, np.array([dense[int(x)] for x in p], np.uint32).reshape(len(p), S)
+
+
+@pytest.mark.parametrize("lo,hi", [(128, 255), (255, 256), (255, 100_000), (1 << 20, 1 << 24)])
+def test_large_counts_exact(gpu_lib, oracle, lo, hi):
+    rng = np.random.default_rng(lo)
+    length, bw, bg = 200_000, 50, 0.003
+    pos, cnt = random_unit(rng, length, bw)
+    pos, cnt = with_big_counts(rng, pos, cnt, 40, lo, hi)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt)
+    regs, gcnt, f, _, last = run_gpu(gpu_lib, bw, bg, length, pos, cnt)
+    compare(ref, ref_sums, regs, gcnt)
+    assert oracle.profile(bw, bg, length, pos, cnt).tobytes() == f.tobytes()
+    assert last == pos[-1]
+
+
+def test_large_counts_multi_sample_controls(gpu_lib, oracle):
+    rng = np.random.default_rng(77)
+    length, bw, bg, S = 120_000, 30, 0.004, 3
+    pos, cnt = random_unit(rng, length, bw, S=S)
+    pos, cnt = with_big_counts(rng, pos, cnt, 60, 200, 5000)
+    control = [0, 1, 0]
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, control=control)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, control=control)
+    compare(ref, ref_sums, regs, gcnt)
+
+
+def test_tag_total_counts_escapes(gpu_lib):
+    pos = np.array([10, 20, 30, 40], np.uint32)
+    cnt = np.array([1, 254, 255, 70_000], np.uint32)
+    with gpu_lib.Lib(0) as g:
+        g.set_params(50, 1, 0.003)
+        u = g.add_unit(1000)
+        g.scatter(u, 0, 0, pos, cnt)
+        assert g.tag_total(u, 0, 0) == int(cnt.sum())
+        # overwrite: the escape at 40 becomes a plain byte, 20 becomes an escape
+        g.scatter(u, 0, 0, np.array([20, 40], np.uint32), np.array([999, 3], np.uint32))
+        assert g.tag_total(u, 0, 0) == 1 + 999 + 255 + 3
+
+
+@pytest.mark.parametrize("thr", [0.05, 1.0, 25.0, 400.0])
+@pytest.mark.parametrize("bw", [1, 15, 16, 17, 33, 64, 127])
+def test_screen_thresholds_and_bandwidths(gpu_lib, oracle, thr, bw):
+    rng = np.random.default_rng(1000 * bw + int(thr * 10))
+    length, bg = 70_000, 0.003
+    pos, cnt = random_unit(rng, length, bw, max_bg=4)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, region_thr=thr, kurt_thr=0.0, hit_thr=1.0)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, region_thr=thr, kurt_thr=0.0,
+                             hit_thr=1.0)
+    compare(ref, ref_sums, regs, gcnt)
+
+
+@pytest.mark.parametrize("coeffs", [[0.37, 1.91, 0.7], [-2.5, 3.0, 0.01], [900.0, 0.5, 7.0],
+                                    [1e6, 1.0, 1.0]])
+def test_screen_with_coefficients(gpu_lib, oracle, coeffs):
+    rng = np.random.default_rng(int(abs(coeffs[0]) * 10) % 1000)
+    length, bw, bg, S = 80_000, 40, 0.004, 3
+    pos, cnt = random_unit(rng, length, bw, S=S)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, coeffs=coeffs, kurt_thr=0.0)
+    regs, gcnt, f, _, _ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, coeffs=coeffs, kurt_thr=0.0)
+    compare(ref, ref_sums, regs, gcnt)
+    assert oracle.profile(bw, bg, length, pos, cnt, coeffs=coeffs).tobytes() == f.tobytes()
+
+
+def test_regions_across_strip_and_block_edges(gpu_lib, oracle):
+    """clusters centred on 1024-block and 16384-strip boundaries (screen halos)"""
+    rng = np.random.default_rng(5)
+    length, bw, bg = 100_000, 50, 0.003
+    dense = {}
+    for c in [1024 * k for k in range(1, 90, 3)] + [16384 * k for k in range(1, 6)]:
+        for o in np.rint(rng.normal(0, 25, 60)).astype(int):
+            p = c + int(o)
+            if 2 * bw + 2 <= p <= length - 2 * bw - 1:
+                dense[p] = dense.get(p, 0) + 1
+    pos = np.array(sorted(dense), np.uint32)
+    cnt = np.array([[dense[int(p)]] for p in pos], np.uint32)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt)
+    compare(ref, ref_sums, regs, gcnt)
+    assert len(regs) > 20
+
+
+def test_pack_from_device_array(gpu_lib, oracle):
+    """device-resident dense uint32 counts (a torch tensor) -> up_unit_pack"""
+    import torch
+    rng = np.random.default_rng(11)
+    length, bw, bg = 150_000, 50, 0.003
+    pos, cnt = random_unit(rng, length, bw)
+    pos, cnt = with_big_counts(rng, pos, cnt, 20, 250, 3000)
+    dense = np.zeros(length, np.uint32)
+    dense[pos - 1] = cnt[:, 0]
+    t = torch.from_numpy(dense.view(np.int32)).to("cuda:0")
+    with gpu_lib.Lib(0) as g:
+        g.set_params(bw, 1, bg)
+        u = g.add_unit(length)
+        torch.cuda.synchronize()
+        g.pack(u, 0, 0, t.data_ptr())
+        n = g.run()
+        regs, gcnt = g.regions(n)
+        assert g.tag_total(u, 0, 0) == int(cnt.sum())
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt)
+    compare(ref, ref_sums, regs, gcnt)
+
+
+def test_nondir_large_counts_corr(gpu_lib, oracle):
+    rng = np.random.default_rng(21)
+    length, bw, bg = 100_000, 50, 0.004
+    pos, cf = random_unit(rng, length, bw)
+    pos, cf = with_big_counts(rng, pos, cf, 30, 255, 2000)
+    cr = np.roll(cf, 5, axis=0)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cf, cr, nondir=True, corr_thr=0.2)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cf, cr, nondir=True, corr_thr=0.2,
+                             want_corr=True)
+    compare(ref, ref_sums, regs, gcnt)
+    assert close(ref["corr"], regs["corr"])

@@ -39,7 +39,7 @@ def main():
                 t = g.timings()
                 ks.append(t[0])
                 walls.append(t[3])
-            byt = 4 * 2 * sum(lens)
+            byt = 1 * 2 * sum(lens)  # uint8 per bp per strand
             k1 = float(np.median(ks))
             out[mode] = {"k1_ms": round(k1, 4), "GBps": round(byt / k1 / 1e6, 1),
                          "wall_ms": round(float(np.median(walls)), 4), "regions": int(n)}

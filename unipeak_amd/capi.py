@@ -64,7 +64,7 @@ _lib = None
 
 EXPORTS = [
     "up_version", "up_strerror", "up_device_count", "up_kernel_weights", "up_open",
-    "up_close", "up_set_params", "up_add_unit", "up_unit_count", "up_unit_ptr",
+    "up_close", "up_set_params", "up_add_unit", "up_unit_count", "up_unit_pack",
     "up_unit_scatter", "up_unit_synth", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
     "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan",
     "up_timings", "up_unit_profile",
@@ -91,7 +91,7 @@ def load_library(path=LIB_PATH):
         "up_set_params": (c.c_int, [vp, c.POINTER(Params)]),
         "up_add_unit": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_int32, u32p]),
         "up_unit_count": (c.c_int, [vp, u32p]),
-        "up_unit_ptr": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.POINTER(vp)]),
+        "up_unit_pack": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, vp]),
         "up_unit_scatter": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.c_size_t, vp, vp]),
         "up_unit_synth": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.c_uint64,
                                     c.c_uint32, c.c_int32, c.c_int32, c.c_int32]),
@@ -134,6 +134,9 @@ def device_count():
     return n.value
 
 
+# Mixing with torch: torch's bundled HIP runtime must initialise the GPU
+# before this library's (system ROCm) runtime does, or torch then reports no
+# GPU -- touch torch.cuda first (tools/mix_probe.py shows both orders).
 class Lib:
     """One up_ctx (one GPU)."""
 
@@ -197,10 +200,10 @@ class Lib:
         _ck(self.L.up_unit_tag_total(self.ctx, unit, strand, sample, ctypes.byref(v)))
         return v.value
 
-    def unit_ptr(self, unit, strand, sample):
-        p = ctypes.c_void_p()
-        _ck(self.L.up_unit_ptr(self.ctx, unit, strand, sample, ctypes.byref(p)))
-        return p.value
+    def pack(self, unit, strand, sample, dev_ptr):
+        """replace a track from a device uint32 array (e.g. a torch tensor's
+        data_ptr()) of contig_len counts"""
+        _ck(self.L.up_unit_pack(self.ctx, unit, strand, sample, ctypes.c_void_p(dev_ptr)))
 
     def set_last_add(self, unit, pos):
         _ck(self.L.up_unit_set_last_add(self.ctx, unit, pos))

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "../../include/unipeak_hip.h"
@@ -25,12 +26,17 @@ struct Unit {
     uint32_t len = 0;
     int32_t nstrands = 1;
     int32_t buffer = 0;
-    uint32_t *dptr = nullptr;
-    uint64_t stride = 0;
+    uint8_t *dptr = nullptr;   // uint8 tracks (kernels.h)
+    uint64_t stride = 0;       // bytes per track
     uint32_t nstrips = 0;
     uint32_t strip0 = 0;
     uint32_t last_override = 0;
     bool has_override = false;
+    // counts >= 255 per track: position -> count (authoritative copy)
+    std::vector<std::map<uint32_t, uint32_t>> ovf;
+    uint64_t *d_ovf = nullptr;     // uploaded entries, sorted by (track, pos)
+    uint32_t *d_ovf_off = nullptr; // [ntracks + 1]
+    bool ovf_dirty = false;
 };
 
 template <typename T>
@@ -89,6 +95,11 @@ struct up_ctx {
     DevBuf<double> d_kern, d_coef;
     DevBuf<int32_t> d_nc;
     DevBuf<uint8_t> d_ctl;
+    DevBuf<uint32_t> d_wscreen;
+    uint32_t wskip = 0;
+    DevBuf<uint32_t> d_stage;          // dense uint32 staging for synth / pack
+    DevBuf<unsigned long long> d_pack_ovf;
+    DevBuf<uint32_t> d_pack_n;
     std::vector<Unit> units;
     bool units_dirty = true;
     DevBuf<UnitDesc> d_units;
@@ -188,8 +199,11 @@ int up_open(int hip_device, up_ctx **out) {
 }
 
 static void free_units(up_ctx *c) {
-    for (auto &u : c->units)
+    for (auto &u : c->units) {
         if (u.dptr) (void)hipFree(u.dptr);
+        if (u.d_ovf) (void)hipFree(u.d_ovf);
+        if (u.d_ovf_off) (void)hipFree(u.d_ovf_off);
+    }
     c->units.clear();
     c->units_dirty = true;
     c->ran = false;
@@ -210,6 +224,7 @@ void up_close(up_ctx *c) {
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
     c->hp_regions.release(); c->hp_counts.release();
+    c->d_wscreen.release(); c->d_stage.release(); c->d_pack_ovf.release(); c->d_pack_n.release();
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -257,13 +272,35 @@ int up_set_params(up_ctx *c, const up_params *p) {
         if (!c->coef.empty())
             HIPCHK(hipMemcpy(c->d_coef.p, c->coef.data(), c->coef.size() * sizeof(double), hipMemcpyHostToDevice));
     }
+    // K1 screen: integer weight per non-control sample bounding its share of
+    // |countSum| (1, or ceil(|coef| + 1) with coefficients, quirk Q5), and the
+    // largest weighted window tag sum W with W * kmax * (1 + 1e-6) < thr
+    {
+        std::vector<uint32_t> w(c->nc.size() + 1, 1u);
+        bool huge = false;
+        for (size_t k = 0; k < c->coef.size(); ++k) {
+            const double q = std::ceil(std::fabs(c->coef[k]) + 1.0);
+            if (!(q <= 4096.0)) huge = true;
+            w[k] = huge ? 1u : (uint32_t)q;
+        }
+        HIPCHK(c->d_wscreen.ensure(w.size()));
+        HIPCHK(hipMemcpy(c->d_wscreen.p, w.data(), w.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        double kmax = 0.0;
+        for (double v : c->kern) kmax = v > kmax ? v : kmax;
+        const double wf = p->region_thr / (kmax * (1.0 + 1e-6));
+        uint32_t ws = 0;
+        if (huge || !(wf > 0.0)) ws = 0;                    // screen off: any tag -> exact
+        else if (wf >= (double)(kBig - 1)) ws = kBig - 1;
+        else ws = (uint32_t)std::ceil(wf) - 1u;
+        c->wskip = ws;
+    }
     c->have_params = true;
     if (old_bw != p->bw) c->units_dirty = true;
     return UP_OK;
 }
 
-// track geometry: positions 1..len plus the scan domain up to len+bw (Q16),
-// rounded to whole strips, with kPad zero elements on both sides
+// track geometry (bytes): positions 1..len plus the scan domain up to
+// len+bw (Q16), rounded to whole strips, with kPad zero bytes on both sides
 static uint64_t unit_stride(uint32_t len) {
     const uint64_t dom = (uint64_t)len + kMaxBw + 1;
     const uint64_t strips = (dom + kStrip - 1) / kStrip;
@@ -279,7 +316,8 @@ int up_add_unit(up_ctx *c, uint32_t len, int32_t nstrands, int32_t buffer_id, ui
     u.nstrands = nstrands;
     u.buffer = buffer_id;
     u.stride = unit_stride(len);
-    const size_t bytes = u.stride * (size_t)c->p.n_samples * nstrands * sizeof(uint32_t);
+    const size_t bytes = u.stride * (size_t)c->p.n_samples * nstrands;
+    u.ovf.resize((size_t)c->p.n_samples * nstrands);
     hipError_t e = hipMalloc(&u.dptr, bytes);
     if (e != hipSuccess) return UP_E_NOMEM;
     HIPCHK(hipMemsetAsync(u.dptr, 0, bytes, c->stream));
@@ -304,7 +342,7 @@ int up_reset_units(up_ctx *c) {
     return UP_OK;
 }
 
-static uint32_t *track_ptr(up_ctx *c, uint32_t unit, int strand, uint16_t sample) {
+static uint8_t *track_ptr(up_ctx *c, uint32_t unit, int strand, uint16_t sample) {
     const Unit &u = c->units[unit];
     return u.dptr + ((uint64_t)strand * c->p.n_samples + sample) * u.stride;
 }
@@ -317,11 +355,45 @@ static int check_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample
     return UP_OK;
 }
 
-int up_unit_ptr(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uint32_t **ptr) {
+// dense device uint32 counts -> the track (uint8 + overflow table)
+static int pack_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, const uint32_t *src) {
+    Unit &u = c->units[unit];
+    const uint64_t len = u.len;
+    if (len == 0) return UP_OK;
+    HIPCHK(c->d_pack_n.ensure(1));
+    uint32_t cap = (uint32_t)std::max<size_t>(c->d_pack_ovf.n, 4096);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        HIPCHK(c->d_pack_ovf.ensure(cap));
+        HIPCHK(hipMemsetAsync(c->d_pack_n.p, 0, 4, c->stream));
+        const uint64_t groups = (len + 3) / 4;
+        hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, c->stream,
+                           track_ptr(c, unit, strand, sample), src, len, c->d_pack_ovf.p, c->d_pack_n.p, cap);
+        HIPCHK(hipGetLastError());
+        uint32_t n = 0;
+        HIPCHK(hipMemcpyAsync(&n, c->d_pack_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (n > cap) { cap = n + n / 4; continue; }
+        auto &m = u.ovf[(size_t)strand * c->p.n_samples + sample];
+        m.clear();
+        if (n) {
+            std::vector<unsigned long long> e(n);
+            HIPCHK(hipMemcpy(e.data(), c->d_pack_ovf.p, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+            for (auto v : e) m[(uint32_t)(v >> 32)] = (uint32_t)v;
+        }
+        u.ovf_dirty = true;
+        c->units_dirty = true;
+        return UP_OK;
+    }
+    return UP_E_INTERNAL;
+}
+
+int up_unit_pack(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, const uint32_t *dev_counts) {
     int r = check_track(c, unit, strand, sample);
     if (r) return r;
-    if (!ptr) return UP_E_ARG;
-    *ptr = track_ptr(c, unit, strand, sample) + kPad;
+    if (!dev_counts) return UP_E_ARG;
+    HIPCHK(hipSetDevice(c->dev));
+    if ((r = pack_track(c, unit, strand, sample, dev_counts))) return r;
+    c->ran = false;
     return UP_OK;
 }
 
@@ -335,6 +407,15 @@ int up_unit_scatter(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, s
     for (size_t i = 0; i < n; ++i)
         if (pos[i] == 0 || pos[i] > len) return UP_E_ARG;
     HIPCHK(hipSetDevice(c->dev));
+    {   // escapes: the host map holds every count >= 255 of the track
+        Unit &u = c->units[unit];
+        auto &m = u.ovf[(size_t)strand * c->p.n_samples + sample];
+        for (size_t i = 0; i < n; ++i) {
+            if (counts[i] >= kEsc) { m[pos[i]] = counts[i]; u.ovf_dirty = true; }
+            else if (!m.empty() && m.erase(pos[i])) u.ovf_dirty = true;
+        }
+        if (u.ovf_dirty) c->units_dirty = true;
+    }
     uint32_t *d = nullptr;
     HIPCHK(hipMalloc(&d, 2 * n * sizeof(uint32_t)));
     HIPCHK(hipMemcpyAsync(d, pos, n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
@@ -379,7 +460,9 @@ int up_unit_synth(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uin
             cdf += pr;
         }
     }
-    uint32_t *trk = track_ptr(c, unit, strand, sample);
+    HIPCHK(c->d_stage.ensure((size_t)len + 4));
+    uint32_t *trk = c->d_stage.p;  // dense uint32 staging, packed below
+    HIPCHK(hipMemsetAsync(trk, 0, (size_t)len * sizeof(uint32_t), c->stream));
     const uint64_t npos = (uint64_t)(hi - lo + 1);
     hipLaunchKernelGGL(synth_bg_kernel, dim3((unsigned)((npos + 255) / 256)), dim3(256), 0,
                        c->stream, trk, tkey, lo, hi, thr);
@@ -416,7 +499,7 @@ int up_unit_synth(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uin
             HIPCHK(hipFree(d));
         }
     }
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if ((r = pack_track(c, unit, strand, sample, trk))) return r;
     c->ran = false;
     return UP_OK;
 }
@@ -437,6 +520,7 @@ int up_unit_tag_total(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample,
     HIPCHK(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     (void)hipFree(d);
+    for (const auto &kv : u.ovf[(size_t)strand * c->p.n_samples + sample]) h += kv.second;
     *total = h;
     return UP_OK;
 }
@@ -448,10 +532,25 @@ int up_unit_set_last_add(up_ctx *c, uint32_t unit, uint32_t last) {
     return UP_OK;
 }
 
+static int sync_units(up_ctx *c);
+
 int up_unit_last_add(up_ctx *c, uint32_t unit, uint32_t *last) {
     if (!c || !last || unit >= c->units.size()) return UP_E_ARG;
     if (c->units[unit].has_override) { *last = c->units[unit].last_override; return UP_OK; }
-    if (!c->ran) return UP_E_STATE;
+    if (!c->have_params) return UP_E_STATE;
+    HIPCHK(hipSetDevice(c->dev));
+    int r = sync_units(c);
+    if (r) return r;
+    const uint32_t nu = (uint32_t)c->units.size();
+    HIPCHK(c->d_unit_last.ensure(nu));
+    HIPCHK(hipMemsetAsync(c->d_unit_last.p, 0, nu * sizeof(uint32_t), c->stream));
+    hipLaunchKernelGGL(unit_last_kernel, dim3(std::max(1u, std::min(2048u, (c->nstrips + 3) / 4))), dim3(256), 0,
+                       c->stream, c->d_units.p, nu, c->nstrips, (int)c->p.n_samples, (int)c->nc.size(),
+                       c->d_nc.p, c->d_unit_last.p);
+    HIPCHK(hipGetLastError());
+    c->unit_last.resize(nu);
+    HIPCHK(hipMemcpyAsync(c->unit_last.data(), c->d_unit_last.p, nu * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     *last = c->unit_last[unit];
     return UP_OK;
 }
@@ -466,7 +565,28 @@ static int sync_units(up_ctx *c) {
         u.nstrips = (uint32_t)((dom + kStrip - 1) / kStrip);
         u.strip0 = strip;
         strip += u.nstrips;
-        d[i] = UnitDesc{(uint64_t)(uintptr_t)u.dptr, u.stride, u.len, u.strip0, u.nstrips, u.nstrands};
+        if (u.ovf_dirty) {
+            if (u.d_ovf) (void)hipFree(u.d_ovf);
+            if (u.d_ovf_off) (void)hipFree(u.d_ovf_off);
+            u.d_ovf = nullptr;
+            u.d_ovf_off = nullptr;
+            std::vector<uint64_t> e;
+            std::vector<uint32_t> off(u.ovf.size() + 1, 0);
+            for (size_t t = 0; t < u.ovf.size(); ++t) {
+                off[t] = (uint32_t)e.size();
+                for (const auto &kv : u.ovf[t]) e.push_back(((uint64_t)kv.first << 32) | kv.second);
+            }
+            off[u.ovf.size()] = (uint32_t)e.size();
+            if (!e.empty()) {
+                HIPCHK(hipMalloc(&u.d_ovf, e.size() * sizeof(uint64_t)));
+                HIPCHK(hipMalloc(&u.d_ovf_off, off.size() * sizeof(uint32_t)));
+                HIPCHK(hipMemcpy(u.d_ovf, e.data(), e.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(u.d_ovf_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            }
+            u.ovf_dirty = false;
+        }
+        d[i] = UnitDesc{(uint64_t)(uintptr_t)u.dptr, u.stride, u.len, u.strip0, u.nstrips, u.nstrands,
+                        (uint64_t)(uintptr_t)u.d_ovf, (uint64_t)(uintptr_t)u.d_ovf_off};
     }
     c->nstrips = strip;
     HIPCHK(c->d_units.ensure(d.size()));
@@ -491,6 +611,8 @@ static ScanParams scan_params(up_ctx *c) {
     P.nc = c->d_nc.p;
     P.coef = c->d_coef.p;
     P.kern = c->d_kern.p;
+    P.wscreen = c->d_wscreen.p;
+    P.wskip = c->wskip;
     P.bw = c->p.bw;
     P.thr = c->p.region_thr;
     P.strip_info = c->d_info.p;
@@ -507,8 +629,7 @@ static void launch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e) 
     uint32_t blocks = (waves + 3) / 4;
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) return;
-    const size_t lds = (2 * (size_t)P.bw + 1) * sizeof(double);
-    hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF>), dim3(blocks), dim3(256), lds, c->stream, P, b, e);
+    hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF>), dim3(blocks), dim3(256), kScanLds, c->stream, P, b, e);
 }
 
 template <bool PROF>
@@ -734,7 +855,6 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     HIPCHK(c->d_off.ensure(ns));
     HIPCHK(c->d_ovf_count.ensure(1));
     HIPCHK(c->d_nreg.ensure(1));
-    HIPCHK(c->d_unit_last.ensure(c->units.size()));
     size_t tmp = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, c->d_cnt.p, c->d_off.p, (int)ns, c->stream));
     HIPCHK(c->d_tmp.ensure(tmp + 16));
@@ -785,13 +905,6 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
     if ((r = launch_head_detect(c))) return r;
-    hipLaunchKernelGGL(unit_last_kernel, dim3((unsigned)c->units.size()), dim3(256), 0, c->stream,
-                       c->d_units.p, (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p,
-                       c->d_unit_last.p);
-    HIPCHK(hipGetLastError());
-    c->unit_last.resize(c->units.size());
-    HIPCHK(hipMemcpyAsync(c->unit_last.data(), c->d_unit_last.p, c->units.size() * 4,
-                          hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c->hp_regions.ensure(nreg + 1));
     HIPCHK(c->hp_counts.ensure((nreg + 1) * c->p.n_samples));
     if (nreg) {

@@ -70,9 +70,8 @@ struct EmuState {
     bool resynced;
 };
 
-__device__ static const uint32_t *trk(const EmuParams &P, uint32_t u, int strand, int s) {
-    const UnitDesc &U = P.units[u];
-    return (const uint32_t *)U.base + ((uint64_t)strand * P.S + s) * U.stride + kPad;
+__device__ static bool any_at(const EmuParams &P, uint32_t u, int strand, int s, uint64_t p) {
+    return track_u8(P.units[u], P.S, strand, s)[kPad + p - 1] != 0;
 }
 
 // processRegion (peakcall.cpp:33-53) + Region statistics, appended to out
@@ -302,8 +301,8 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
             uint32_t any0 = 0, any1 = 0;
             if (p <= U.len) {
                 for (int s = 0; s < S; ++s) {
-                    any0 |= trk(P, u, 0, s)[p - 1];
-                    if (nstr == 2) any1 |= trk(P, u, 1, s)[p - 1];
+                    any0 |= any_at(P, u, 0, s, p) ? 1u : 0u;
+                    if (nstr == 2) any1 |= any_at(P, u, 1, s, p) ? 1u : 0u;
                 }
             }
             const uint64_t m0 = __ballot(any0 != 0), m1 = __ballot(any1 != 0);
@@ -316,7 +315,7 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
                     for (int st = 0; st < 2 && !E.resynced; ++st) {
                         if (!(((st ? m1 : m0) >> b) & 1)) continue;
                         uint32_t counts[256];
-                        for (int s = 0; s < S; ++s) counts[s] = trk(P, u, nstr == 2 ? st : 0, s)[pos - 1];
+                        for (int s = 0; s < S; ++s) counts[s] = count_at(U, S, nstr == 2 ? st : 0, s, pos);
                         E.close_pos = pos;
                         const bool first_aligned = !E.aligned && pos > (uint32_t)P.bw;
                         emu_add(P, E, counts, pos, nstr == 2 ? st == 0 : P.unit_buffer[u] == 0);
@@ -362,14 +361,13 @@ __global__ void head_detect_kernel(const UnitDesc *units, int S, int nnc, const 
     uint32_t hit = 0;
     if (p <= bw && (uint32_t)p <= U.len) {
         for (int st = 0; st < U.nstrands; ++st) {
-            const uint32_t *t = (const uint32_t *)U.base + (uint64_t)st * S * U.stride + kPad + p - 1;
             double cs = 0.0;
             for (int k = 0; k < nnc; ++k) {
-                const uint32_t c = t[(uint64_t)nc[k] * U.stride];
+                const uint32_t c = count_at(U, S, st, nc[k], p);
                 cs = POOL == 2 ? cs + (double)c * coef[k] : cs + (double)c;
             }
             if (POOL == 2)
-                for (int k = 0; k < nnc; ++k) cs = cs + (double)t[(uint64_t)nc[k] * U.stride];
+                for (int k = 0; k < nnc; ++k) cs = cs + (double)count_at(U, S, st, nc[k], p);
             if (cs != 0.0) hit = 1;
         }
     }

@@ -2,11 +2,13 @@
 // kernels (kernels.hip) and the C-ABI implementation (api.hip).
 //
 // HBM layout (DESIGN.md "Data layout"): every (unit, strand, sample) track is
-// a dense uint32 array; position p (1-based) of a track lives at element
-// kPad + p - 1, with kPad zero elements in front and at least kPad behind
+// a dense uint8 array of tag counts; position p (1-based) of a track lives at
+// byte kPad + p - 1, with kPad zero bytes in front and at least kPad behind
 // the unit's scan domain [1, len + bw], so every halo load is in bounds and
-// reads zeros outside the contig.  Tracks of one unit are contiguous:
-// track(s, k) = base + (s * S + k) * stride.
+// reads zeros outside the contig.  A count >= 255 is stored as the escape
+// byte 255 and its value in the unit's overflow table (entries
+// (pos << 32 | count), sorted by track then position).  Tracks of one unit
+// are contiguous: track(s, k) = base + (s * S + k) * stride bytes.
 #pragma once
 #include <stdint.h>
 
@@ -15,20 +17,26 @@ namespace upk {
 constexpr int kWave = 64;           // CDNA wavefront
 constexpr int kStripWords = 256;    // one strip (wave task) = 256 words of 64 positions
 constexpr int kStrip = kStripWords * kWave;  // 16384 positions per wave task
-constexpr int kStepWords = 16;      // words per register step inside a strip
-constexpr int kPad = 2112;          // 33 words: covers bw <= 2047 halos
+constexpr int kStepWords = 16;      // words per block (= one 1024-position dwordx4 wave load)
+constexpr int kBlocks = kStripWords / kStepWords;  // 16 blocks per strip
+constexpr int kChunk = 16;          // positions per lane in the screening load (dwordx4)
+constexpr int kPad = 256;           // zero bytes before position 1 and after the domain
 constexpr int kMaxBw = 127;         // register-resident halo: NH <= 2 words
 constexpr int kCap = 32;            // inline run records per strip (starts, ends each)
 constexpr int kOvfHalf = kStrip / 2 + 1;  // max starts (= max ends) of one strip
 constexpr int kOvfStride = 2 * kOvfHalf;  // starts + ends of one spilled strip
+constexpr uint32_t kEsc = 255;      // escape byte: count lives in the overflow table
+constexpr uint32_t kBig = 1u << 22; // screen value of a chunk holding a byte >= 128
 
 struct UnitDesc {
     uint64_t base;      // device address of track (0, 0)
-    uint64_t stride;    // elements per track
+    uint64_t stride;    // bytes per track (multiple of 256)
     uint32_t len;       // contig length
     uint32_t strip0;    // first global strip index
     uint32_t nstrips;   // strips covering [1, len + bw]
     int32_t nstrands;   // 1 or 2
+    uint64_t ovf;       // overflow entries (uint64 pos << 32 | count) or 0
+    uint64_t ovf_off;   // uint32[ntracks + 1] offsets into ovf, or 0
 };
 
 // packed per-strip summary written by the scan kernel (uint64):
@@ -49,6 +57,8 @@ struct ScanParams {
     const int32_t *nc;  // indices of non-control samples, in sample order
     const double *coef; // per non-control sample (pool mode 2) or null
     const double *kern; // 2*bw+1 weights
+    const uint32_t *wscreen;  // per non-control sample: integer weight >= |pooled share|
+    uint32_t wskip;     // a window whose weighted tag sum is <= wskip cannot reach thr
     int32_t bw;
     double thr;
     uint64_t *strip_info;

@@ -49,9 +49,12 @@ __device__ __forceinline__ uint64_t win_mask(int d, int bw) {
     return up & ~((1ull << lo) - 1);
 }
 
-// global-address-space view of a track (plain pointers from the unit table
+// global-address-space views of a track (plain pointers from the unit table
 // would otherwise compile to flat loads)
 typedef const __attribute__((address_space(1))) uint32_t gu32;
+typedef const __attribute__((address_space(1))) uint8_t gu8;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 
 // window word storage: raw counts when the pooled count is the single
 // non-control sample's count, otherwise the FP64 pooled count
@@ -63,26 +66,59 @@ __device__ __forceinline__ double rl_cs(double v, int l) { return rl_d(v, l); }
 __device__ __forceinline__ bool nz(uint32_t v) { return v != 0u; }
 __device__ __forceinline__ bool nz(double v) { return v != 0.0; }
 
+// ---- track access (layout in kernels.h) ----
+__device__ __forceinline__ gu8 *track_u8(const UnitDesc &U, int S, int strand, int sample) {
+    return (gu8 *)U.base + ((uint64_t)strand * S + sample) * U.stride;
+}
+
+// count >= 255: binary search of the track's overflow entries
+__device__ __noinline__ uint32_t ovf_lookup(const UnitDesc &U, uint32_t track, uint32_t pos) {
+    if (!U.ovf) return kEsc;
+    const uint32_t *off = (const uint32_t *)U.ovf_off;
+    const uint64_t *e = (const uint64_t *)U.ovf;
+    uint32_t lo = off[track], hi = off[track + 1];
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint32_t p = (uint32_t)(e[mid] >> 32);
+        if (p < pos) lo = mid + 1; else hi = mid;
+    }
+    return (lo < off[track + 1] && (uint32_t)(e[lo] >> 32) == pos) ? (uint32_t)e[lo] : kEsc;
+}
+
+// exact count of (strand, sample) at position p (1-based)
+__device__ __forceinline__ uint32_t count_at(const UnitDesc &U, int S, int strand, int sample,
+                                             int64_t p) {
+    const uint32_t b = track_u8(U, S, strand, sample)[kPad + p - 1];
+    return b == kEsc ? ovf_lookup(U, (uint32_t)(strand * S + sample), (uint32_t)p) : b;
+}
+
 // ---- pooled count (ProfileBuffer::add countSum, peakcall.cpp:186-200) ----
 // POOL 0: one non-control sample, no coefficients; 1: several, unscaled;
 // 2: scaled by coefficients plus the unscaled second loop (quirk Q5).
-// e0 = element index of lane 0 of the first word.
+// x0 = position of lane 0 of the first word.
 template <int N, int POOL>
-__device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], gu32 *strand_base, uint64_t stride,
-                                           int64_t e0, int lane, int nnc, const int32_t *nc,
+__device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], const UnitDesc &U, int S, int strand,
+                                           int64_t x0, int lane, int nnc, const int32_t *nc,
                                            const double *coef) {
-    if constexpr (POOL == 0) {
-        gu32 *t = strand_base + (uint64_t)nc[0] * stride + e0 + lane;
+    uint32_t c[N];
+    auto fetch = [&](int k) {
+        gu8 *t = track_u8(U, S, strand, nc[k]) + kPad + x0 - 1 + lane;
 #pragma unroll
-        for (int w = 0; w < N; ++w) cs[w] = __builtin_nontemporal_load(t + 64 * w);
+        for (int w = 0; w < N; ++w) c[w] = t[64 * w];
+#pragma unroll
+        for (int w = 0; w < N; ++w)
+            if (c[w] == kEsc)
+                c[w] = ovf_lookup(U, (uint32_t)(strand * S + nc[k]), (uint32_t)(x0 + 64 * w + lane));
+    };
+    if constexpr (POOL == 0) {
+        fetch(0);
+#pragma unroll
+        for (int w = 0; w < N; ++w) cs[w] = c[w];
     } else {
 #pragma unroll
         for (int w = 0; w < N; ++w) cs[w] = 0.0;
         for (int k = 0; k < nnc; ++k) {
-            gu32 *t = strand_base + (uint64_t)nc[k] * stride + e0 + lane;
-            uint32_t c[N];
-#pragma unroll
-            for (int w = 0; w < N; ++w) c[w] = __builtin_nontemporal_load(t + 64 * w);
+            fetch(k);
             if constexpr (POOL == 1) {
 #pragma unroll
                 for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w];
@@ -94,9 +130,9 @@ __device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], gu32 *strand_bas
         }
         if constexpr (POOL == 2) {
             for (int k = 0; k < nnc; ++k) {
-                gu32 *t = strand_base + (uint64_t)nc[k] * stride + e0 + lane;
+                fetch(k);
 #pragma unroll
-                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)t[64 * w];
+                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w];
             }
         }
     }
@@ -213,16 +249,49 @@ __device__ __forceinline__ void scatter_hit(A (&acc)[SW], int b, double c, int l
 }
 
 // ------------------------------------------------------------------------
-// K1: one wave streams one 16384-position strip of a unit through a
-// register window of 16 + 2*NH words (64 positions each), one step of 16
-// words at a time, with the next step's counts prefetched (POOL 0) while
-// the current step is scored.  Halo words are carried between steps, so
-// every count is read from HBM once (plus 2*NH words per strip).
-// Scalar work per step is the walk over hit bits plus one flag test: each
-// hit is scattered (in ascending position order, so every position's sum
-// keeps the reference's order) into FP64 accumulators of the words it
-// reaches; run boundaries are only derived for steps holding a flag.
+// K1: one wave owns one 16384-position strip of a unit (16 blocks of 1024).
+//
+// Screen (integer, HBM-streaming): the strip's uint8 counts of every pooled
+// track are read once with 16-byte lane loads (one 1 KiB wave load per
+// block), reduced to per-16-position chunk sums (v_sad_u8), and every chunk's
+// window of +-R = ceil(bw/16) chunks is summed.  kmax * (weighted window
+// sum) bounds every score in the chunk, so a block whose chunks all stay
+// <= wskip holds no flagged position and is skipped -- no FP64 work at all.
+// Exact blocks (peaks, and any chunk with a byte >= 128 / escape) run the
+// KDE: the hits of the block's 16 + 2*NH words (64 positions each, re-read
+// from L2 as lane = position) are walked in ascending order with wave
+// ballots and scattered into FP64 accumulators, so every position's sum
+// keeps the reference's order; flags give run boundaries.
 // ------------------------------------------------------------------------
+constexpr int kScrWords = 8 + kBlocks * kWave + 8;  // chunk sums of one strip + halos
+constexpr size_t kScanLds = (2 * kMaxBw + 2) * sizeof(double) + 4 * kScrWords * sizeof(uint32_t);
+
+// chunk i (0..15) of this lane: window a[8+i-R .. 8+i+R] > wskip
+template <int R>
+__device__ __forceinline__ uint32_t screen_bits(const uint32_t (&a)[32], uint32_t wskip) {
+    uint32_t W = 0;
+#pragma unroll
+    for (int j = 8 - R; j <= 8 + R; ++j) W += a[j];
+    uint32_t m = W > wskip ? 1u : 0u;
+#pragma unroll
+    for (int i = 1; i < 16; ++i) {
+        W += a[8 + i + R] - a[8 + i - 1 - R];
+        m |= (W > wskip ? 1u : 0u) << i;
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint32_t sad4(u32x4 v, uint32_t acc) {
+    acc = __builtin_amdgcn_sad_u8(v.x, 0u, acc);
+    acc = __builtin_amdgcn_sad_u8(v.y, 0u, acc);
+    acc = __builtin_amdgcn_sad_u8(v.z, 0u, acc);
+    return __builtin_amdgcn_sad_u8(v.w, 0u, acc);
+}
+
+__device__ __forceinline__ bool has_big(u32x4 v) {
+    return ((v.x | v.y | v.z | v.w) & 0x80808080u) != 0u;
+}
+
 template <int NH, int POOL, bool NONDIR, bool PROF>
 __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_begin,
                                                    uint32_t strip_end) {
@@ -230,14 +299,16 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
     const int bw = P.bw;
     for (int i = threadIdx.x; i <= 2 * bw; i += blockDim.x) ktab[i] = P.kern[i];
     __syncthreads();
+    uint32_t *scr = (uint32_t *)(ktab + 2 * kMaxBw + 2) + (threadIdx.x >> 6) * kScrWords;
 
     constexpr int SW = kStepWords;
     constexpr int NWIN = SW + 2 * NH;
-    constexpr int NSTEP = kStripWords / SW;
     using T = WinT<POOL>;
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    const int R = (bw + kChunk - 1) / kChunk;
+    const int S = P.S;
     // halo words only matter where they reach an output word
     uint64_t edge_lo[NH], edge_hi[NH];
 #pragma unroll
@@ -254,35 +325,98 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
         const UnitDesc U = P.units[cur];
         const uint32_t local = strip - U.strip0;
         const int64_t p0 = 1 + (int64_t)local * kStrip;  // first position of the strip
-        const int64_t e0 = kPad + p0 - 1;                 // element of strip word 0, lane 0
-        gu32 *fb = (gu32 *)U.base;
-        gu32 *rb = fb + (uint64_t)P.S * U.stride;
 
-        T wf[NWIN], wr[NONDIR ? NWIN : 1];
-        uint64_t hf[NWIN], hr[NONDIR ? NWIN : 1];
-        load_words<NWIN, POOL>(wf, fb, U.stride, e0 - 64 * NH, lane, P.nnc, P.nc, P.coef);
-        if constexpr (NONDIR)
-            load_words<NWIN, POOL>(wr, rb, U.stride, e0 - 64 * NH, lane, P.nnc, P.nc, P.coef);
+        // ---- screen: which blocks can hold a flagged position ----
+        uint32_t exact_blocks = 0xFFFFu;
+        if constexpr (!PROF) {
+            uint32_t cs[kBlocks];
+            uint32_t big = 0, hs = 0;
+            bool hbig = false;
 #pragma unroll
-        for (int w = 0; w < NWIN; ++w) {
-            hf[w] = __ballot(nz(wf[w]));
-            if constexpr (NONDIR) hr[w] = __ballot(nz(wr[w]));
+            for (int k = 0; k < kBlocks; ++k) cs[k] = 0;
+            for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
+                for (int k = 0; k < P.nnc; ++k) {
+                    gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, P.nc[k]) + kPad + p0 - 1);
+                    u32x4 v[kBlocks];
+#pragma unroll
+                    for (int bk = 0; bk < kBlocks; ++bk) v[bk] = __builtin_nontemporal_load(t + 64 * bk + lane);
+                    u32x4 hv = {0u, 0u, 0u, 0u};
+                    if (lane < 16) hv = t[lane < 8 ? lane - 8 : kBlocks * kWave + lane - 8];
+                    const uint32_t w = POOL == 2 ? P.wscreen[k] : 1u;
+#pragma unroll
+                    for (int bk = 0; bk < kBlocks; ++bk) {
+                        const uint32_t x = sad4(v[bk], 0u);
+                        cs[bk] += POOL == 2 ? x * w : x;
+                        big |= has_big(v[bk]) ? (1u << bk) : 0u;
+                    }
+                    const uint32_t hx = sad4(hv, 0u);
+                    hs += POOL == 2 ? hx * w : hx;
+                    hbig = hbig || has_big(hv);
+                }
+            }
+#pragma unroll
+            for (int bk = 0; bk < kBlocks; ++bk) scr[8 + kWave * bk + lane] = ((big >> bk) & 1u) ? kBig : cs[bk];
+            if (lane < 8) scr[lane] = hbig ? kBig : hs;
+            else if (lane < 16) scr[8 + kBlocks * kWave + lane - 8] = hbig ? kBig : hs;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t a[32];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint4 q = *(const uint4 *)(scr + 16 * lane + 4 * j);
+                a[4 * j] = q.x; a[4 * j + 1] = q.y; a[4 * j + 2] = q.z; a[4 * j + 3] = q.w;
+            }
+            uint32_t m = 0;
+            switch (R) {
+            case 1: m = screen_bits<1>(a, P.wskip); break;
+            case 2: m = screen_bits<2>(a, P.wskip); break;
+            case 3: m = screen_bits<3>(a, P.wskip); break;
+            case 4: m = screen_bits<4>(a, P.wskip); break;
+            case 5: m = screen_bits<5>(a, P.wskip); break;
+            case 6: m = screen_bits<6>(a, P.wskip); break;
+            case 7: m = screen_bits<7>(a, P.wskip); break;
+            default: m = screen_bits<8>(a, P.wskip); break;
+            }
+            const uint64_t lanes = __ballot(m != 0u);  // lane l covers chunks 16l..16l+15
+            exact_blocks = 0;
+#pragma unroll
+            for (int bk = 0; bk < kBlocks; ++bk)
+                exact_blocks |= ((lanes >> (4 * bk)) & 0xFull) ? (1u << bk) : 0u;
+            // the next strip reuses scr only after every lane has read it
+            __builtin_amdgcn_wave_barrier();
         }
 
         uint32_t *inl = P.rec + (uint64_t)strip * (2 * kCap);
-        RecList R{inl, inl + kCap, 0, 0, (uint32_t)kCap, false, false};
+        RecList R_{inl, inl + kCap, 0, 0, (uint32_t)kCap, false, false};
         uint64_t prevF = 0, F0 = 0;
 
-        for (int j = 0; j < NSTEP; ++j) {
-            const bool more = j + 1 < NSTEP;
-            const int64_t enext = e0 + 64 * ((j + 1) * SW + NH);  // first new word of step j+1
-            T nf[POOL == 0 ? SW : 1], nr[(POOL == 0 && NONDIR) ? SW : 1];
-            if constexpr (POOL == 0) {
-                if (more) {
-                    load_words<SW, 0>(nf, fb, U.stride, enext, lane, P.nnc, P.nc, P.coef);
-                    if constexpr (NONDIR)
-                        load_words<SW, 0>(nr, rb, U.stride, enext, lane, P.nnc, P.nc, P.coef);
+        for (int j = 0; j < kBlocks; ++j) {
+            if (!((exact_blocks >> j) & 1u)) {
+                // no flag in this block: a run open at its left edge ends there
+                if constexpr (!PROF) {
+                    if (prevF) {
+                        uint64_t en = prevF & ~(prevF >> 1);
+                        const int64_t wpos = p0 + 64 * (j * SW - 1);
+                        while (en) {
+                            const int b = __builtin_ctzll(en);
+                            en &= en - 1;
+                            rec_push(R_, false, (uint32_t)(wpos + b), P, inl, lane);
+                        }
+                        prevF = 0;
+                    }
                 }
+                continue;
+            }
+            const int64_t x0 = p0 + 64 * (j * SW - NH);  // position of window word 0, lane 0
+            T wf[NWIN], wr[NONDIR ? NWIN : 1];
+            uint64_t hf[NWIN], hr[NONDIR ? NWIN : 1];
+            load_words<NWIN, POOL>(wf, U, S, 0, x0, lane, P.nnc, P.nc, P.coef);
+            if constexpr (NONDIR) load_words<NWIN, POOL>(wr, U, S, 1, x0, lane, P.nnc, P.nc, P.coef);
+#pragma unroll
+            for (int w = 0; w < NWIN; ++w) {
+                hf[w] = __ballot(nz(wf[w]));
+                if constexpr (NONDIR) hr[w] = __ballot(nz(wr[w]));
             }
             // ---- KDE: scatter every hit of the window, ascending ----
             double af[SW], ar[NONDIR ? SW : 1];
@@ -330,7 +464,7 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
                     }
                 }
             } else {
-                // ---- flags and run boundaries (only steps touching a run) ----
+                // ---- flags and run boundaries (only blocks touching a run) ----
                 const uint64_t anyflag = __ballot(mx >= P.thr);
                 if (anyflag | prevF) {
 #pragma unroll
@@ -347,46 +481,16 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
                             while (en) {
                                 const int b = __builtin_ctzll(en);
                                 en &= en - 1;
-                                rec_push(R, false, (uint32_t)(wpos - 64 + b), P, inl, lane);
+                                rec_push(R_, false, (uint32_t)(wpos - 64 + b), P, inl, lane);
                             }
                         }
                         while (st) {
                             const int b = __builtin_ctzll(st);
                             st &= st - 1;
-                            rec_push(R, true, (uint32_t)(wpos + b), P, inl, lane);
+                            rec_push(R_, true, (uint32_t)(wpos + b), P, inl, lane);
                         }
                         prevF = F;
                     }
-                }
-            }
-            if (more) {
-#pragma unroll
-                for (int w = 0; w < 2 * NH; ++w) {
-                    wf[w] = wf[SW + w];
-                    hf[w] = hf[SW + w];
-                    if constexpr (NONDIR) { wr[w] = wr[SW + w]; hr[w] = hr[SW + w]; }
-                }
-                if constexpr (POOL == 0) {
-#pragma unroll
-                    for (int w = 0; w < SW; ++w) {
-                        wf[2 * NH + w] = nf[w];
-                        if constexpr (NONDIR) wr[2 * NH + w] = nr[w];
-                    }
-                } else {
-                    T t[SW];
-                    load_words<SW, POOL>(t, fb, U.stride, enext, lane, P.nnc, P.nc, P.coef);
-#pragma unroll
-                    for (int w = 0; w < SW; ++w) wf[2 * NH + w] = t[w];
-                    if constexpr (NONDIR) {
-                        load_words<SW, POOL>(t, rb, U.stride, enext, lane, P.nnc, P.nc, P.coef);
-#pragma unroll
-                        for (int w = 0; w < SW; ++w) wr[2 * NH + w] = t[w];
-                    }
-                }
-#pragma unroll
-                for (int w = 2 * NH; w < NWIN; ++w) {
-                    hf[w] = __ballot(nz(wf[w]));
-                    if constexpr (NONDIR) hr[w] = __ballot(nz(wr[w]));
                 }
             }
         }
@@ -397,13 +501,13 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
             while (en) {
                 const int b = __builtin_ctzll(en);
                 en &= en - 1;
-                rec_push(R, false, (uint32_t)(wpos + b), P, inl, lane);
+                rec_push(R_, false, (uint32_t)(wpos + b), P, inl, lane);
             }
         }
-        const uint64_t info = (uint64_t)R.ns | ((uint64_t)R.ne << 16) | ((F0 & 1ull) << 32) |
+        const uint64_t info = (uint64_t)R_.ns | ((uint64_t)R_.ne << 16) | ((F0 & 1ull) << 32) |
                               ((prevF >> 63) << 33) | ((uint64_t)(local == 0) << 34) |
                               ((uint64_t)(local + 1 == U.nstrips) << 35) |
-                              ((uint64_t)R.spilled << 36);
+                              ((uint64_t)R_.spilled << 36);
         if (lane == 0) P.strip_info[strip] = info;
     }
 }
@@ -455,27 +559,46 @@ __global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
     if (xe) ends[oe++] = (uint32_t)(p0 + kStrip - 1);
 }
 
-// per-unit last add (the last position whose pooled count is nonzero):
-// one workgroup per unit scans its tracks backwards from the contig end
-__global__ void unit_last_kernel(const UnitDesc *units, int S, int nnc, const int32_t *nc,
-                                 uint32_t *__restrict__ out) {
-    const UnitDesc U = units[blockIdx.x];
-    __shared__ uint32_t found;
-    if (threadIdx.x == 0) found = 0;
-    __syncthreads();
-    for (int64_t hi = U.len; hi >= 1; hi -= blockDim.x) {
-        const int64_t p = hi - threadIdx.x;
-        uint32_t any = 0;
-        if (p >= 1)
-            for (int st = 0; st < U.nstrands; ++st)
-                for (int k = 0; k < nnc; ++k)
-                    any |= ((const uint32_t *)U.base)[((uint64_t)st * S + nc[k]) * U.stride + kPad + p - 1];
-        if (any) atomicMax(&found, (uint32_t)p);
-        __syncthreads();
-        if (found) break;
-        __syncthreads();
+// per-unit last add (the last position whose pooled count is nonzero): one
+// wave per strip finds its highest nonzero byte over the pooled tracks and
+// folds it into the unit's slot with atomicMax (out zeroed by the caller)
+__device__ __forceinline__ uint32_t top_byte(uint32_t x) {  // index of highest nonzero byte
+    return (uint32_t)(31 - __builtin_clz(x)) >> 3;
+}
+
+__global__ void __launch_bounds__(256) unit_last_kernel(const UnitDesc *units, uint32_t nunits,
+                                                        uint32_t nstrips, int S, int nnc,
+                                                        const int32_t *nc, uint32_t *out) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t strip = wave; strip < nstrips; strip += nwaves) {
+        const uint32_t u = find_unit(units, nunits, strip);
+        const UnitDesc U = units[u];
+        const int64_t p0 = 1 + (int64_t)(strip - U.strip0) * kStrip;
+        uint32_t best = 0;
+        for (int st = 0; st < U.nstrands; ++st)
+            for (int k = 0; k < nnc; ++k) {
+                gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, nc[k]) + kPad + p0 - 1);
+#pragma unroll 4
+                for (int bk = 0; bk < kBlocks; ++bk) {
+                    const u32x4 v = __builtin_nontemporal_load(t + 64 * bk + lane);
+                    const int64_t q = p0 + kWave * kChunk * bk + kChunk * lane;
+                    uint32_t hi = 0;
+                    if (v.x) hi = (uint32_t)q + top_byte(v.x);
+                    if (v.y) hi = (uint32_t)q + 4 + top_byte(v.y);
+                    if (v.z) hi = (uint32_t)q + 8 + top_byte(v.z);
+                    if (v.w) hi = (uint32_t)q + 12 + top_byte(v.w);
+                    best = hi > best ? hi : best;
+                }
+            }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t ob = (uint32_t)__shfl_xor((int)best, o);
+            best = ob > best ? ob : best;
+        }
+        if (lane == 0 && best) atomicMax(&out[u], best);
     }
-    if (threadIdx.x == 0) out[blockIdx.x] = found;
 }
 
 // ------------------------------------------------------------------------
@@ -490,10 +613,9 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // pooled counts of the 2NH+1 words around block start x0 for one strand
 template <int NH, int POOL>
 __device__ __forceinline__ void region_words(WinT<POOL> (&cs)[2 * NH + 1], uint64_t (&hm)[2 * NH + 1],
-                                             const uint32_t *strand_base, uint64_t stride,
-                                             int64_t x0, int lane, const StatParams &P) {
-    const int64_t idx0 = kPad + x0 - 1 - 64 * NH;
-    load_words<2 * NH + 1, POOL>(cs, (gu32 *)strand_base, stride, idx0, lane, P.nnc, P.nc, P.coef);
+                                             const UnitDesc &U, int strand, int64_t x0, int lane,
+                                             const StatParams &P) {
+    load_words<2 * NH + 1, POOL>(cs, U, P.S, strand, x0 - 64 * NH, lane, P.nnc, P.nc, P.coef);
 #pragma unroll
     for (int w = 0; w < 2 * NH + 1; ++w) hm[w] = __ballot(nz(cs[w]));
 }
@@ -517,8 +639,6 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
     for (uint64_t ri = wave; ri < nreg; ri += nwaves) {
         const uint32_t left = P.starts[ri], right = P.ends[ri], u = P.reg_unit[ri];
         const UnitDesc U = P.units[u];
-        const uint32_t *base = (const uint32_t *)U.base;
-        const uint64_t sstride = (uint64_t)S * U.stride;
         uint32_t esum[4] = {0, 0, 0, 0};  // exptSums[s] lives in lane s%64, slot s/64
 
         uint32_t cnt_acc = 0, sum_acc = 0;
@@ -532,14 +652,14 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             const int nvalid = (int)(((int64_t)right - x0 + 1) < 64 ? ((int64_t)right - x0 + 1) : 64);
             WinT<POOL> cf[NWT];
             uint64_t hf[NWT];
-            region_words<NH, POOL>(cf, hf, base, U.stride, x0, lane, P);
+            region_words<NH, POOL>(cf, hf, U, 0, x0, lane, P);
             double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
             double r = 0.0;
             uint64_t hr_c = 0;
             WinT<POOL> cr[NONDIR ? NWT : 1];
             uint64_t hr[NONDIR ? NWT : 1];
             if constexpr (NONDIR) {
-                region_words<NH, POOL>(cr, hr, base + sstride, U.stride, x0, lane, P);
+                region_words<NH, POOL>(cr, hr, U, 1, x0, lane, P);
                 r = kde_word<NWT, NH, NH>(cr, hr, wm, lane, bw, ktab);
                 hr_c = hr[NH];
             }
@@ -553,13 +673,12 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             }
             // stored hit vectors (peakcall.cpp:210-219; quirk Q7)
             const bool sf_hit = (hf[NH] >> lane) & 1, sr_hit = (hr_c >> lane) & 1;
-            const int64_t idx = kPad + x - 1;
             uint32_t pc = 0;
             for (int s = 0; s < S; ++s) {
                 uint32_t c = 0;
                 if (valid) {
-                    if (sf_hit) c += base[(uint64_t)s * U.stride + idx];
-                    if (NONDIR && sr_hit) c += base[sstride + (uint64_t)s * U.stride + idx];
+                    if (sf_hit) c += count_at(U, S, 0, s, x);
+                    if (NONDIR && sr_hit) c += count_at(U, S, 1, s, x);
                 }
                 pc += c;
                 const uint32_t t = wave_sum_u32(c);
@@ -593,27 +712,26 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
         for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
             const int64_t x = x0 + lane;
             const bool valid = x <= (int64_t)right;
-            const int64_t idx = kPad + x - 1;
             double c0 = 0.0, c1 = 0.0;
             // pooled count at x itself, per strand, to know what was stored
             if (valid) {
                 if (POOL == 0) {
-                    c0 = (double)base[(uint64_t)P.nc[0] * U.stride + idx];
-                    if (NONDIR) c1 = (double)base[sstride + (uint64_t)P.nc[0] * U.stride + idx];
+                    c0 = (double)count_at(U, S, 0, P.nc[0], x);
+                    if (NONDIR) c1 = (double)count_at(U, S, 1, P.nc[0], x);
                 } else {
                     for (int k = 0; k < P.nnc; ++k) {
                         const double q = POOL == 2 ? P.coef[k] : 1.0;
-                        const uint32_t a = base[(uint64_t)P.nc[k] * U.stride + idx];
+                        const uint32_t a = count_at(U, S, 0, P.nc[k], x);
                         c0 = POOL == 2 ? c0 + (double)a * q : c0 + (double)a;
                         if (NONDIR) {
-                            const uint32_t b = base[sstride + (uint64_t)P.nc[k] * U.stride + idx];
+                            const uint32_t b = count_at(U, S, 1, P.nc[k], x);
                             c1 = POOL == 2 ? c1 + (double)b * q : c1 + (double)b;
                         }
                     }
                     if (POOL == 2) {
                         for (int k = 0; k < P.nnc; ++k) {
-                            c0 = c0 + (double)base[(uint64_t)P.nc[k] * U.stride + idx];
-                            if (NONDIR) c1 = c1 + (double)base[sstride + (uint64_t)P.nc[k] * U.stride + idx];
+                            c0 = c0 + (double)count_at(U, S, 0, P.nc[k], x);
+                            if (NONDIR) c1 = c1 + (double)count_at(U, S, 1, P.nc[k], x);
                         }
                     }
                 }
@@ -621,8 +739,8 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             const bool h0 = valid && c0 != 0.0, h1 = valid && NONDIR && c1 != 0.0;
             uint32_t pc = 0;
             for (int s = 0; s < S; ++s) {
-                if (h0) pc += base[(uint64_t)s * U.stride + idx];
-                if (h1) pc += base[sstride + (uint64_t)s * U.stride + idx];
+                if (h0) pc += count_at(U, S, 0, s, x);
+                if (h1) pc += count_at(U, S, 1, s, x);
             }
             uint64_t m = __ballot(h0 || h1);
             while (m) {
@@ -647,8 +765,8 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
                 const int nvalid = (int)(((int64_t)right - x0 + 1) < 64 ? ((int64_t)right - x0 + 1) : 64);
                 WinT<POOL> cf[NWT], cr[NWT];
                 uint64_t hf[NWT], hr[NWT];
-                region_words<NH, POOL>(cf, hf, base, U.stride, x0, lane, P);
-                region_words<NH, POOL>(cr, hr, base + sstride, U.stride, x0, lane, P);
+                region_words<NH, POOL>(cf, hf, U, 0, x0, lane, P);
+                region_words<NH, POOL>(cr, hr, U, 1, x0, lane, P);
                 const double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
                 const double r = kde_word<NWT, NH, NH>(cr, hr, wm, lane, bw, ktab);
                 const double d1 = f - m1, d2 = r - m2;
@@ -716,15 +834,13 @@ __global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t 
         const uint64_t ri = idx[j];
         const uint32_t left = P.starts[ri], right = P.ends[ri], u = P.reg_unit[ri];
         const UnitDesc U = P.units[u];
-        const uint32_t *base = (const uint32_t *)U.base;
-        const uint64_t sstride = (uint64_t)P.S * U.stride;
         const uint32_t len = right - left + 1;
         double *fs = slab + slab_off[j], *rs = fs + len;
         for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
             WinT<POOL> cf[NWT], cr[NWT];
             uint64_t hf[NWT], hr[NWT];
-            region_words<NH, POOL>(cf, hf, base, U.stride, x0, lane, P);
-            region_words<NH, POOL>(cr, hr, base + sstride, U.stride, x0, lane, P);
+            region_words<NH, POOL>(cf, hf, U, 0, x0, lane, P);
+            region_words<NH, POOL>(cr, hr, U, 1, x0, lane, P);
             const double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
             const double r = kde_word<NWT, NH, NH>(cr, hr, wm, lane, bw, ktab);
             const int64_t x = x0 + lane;
@@ -756,10 +872,38 @@ __global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t 
 // ------------------------------------------------------------------------
 // aux kernels
 // ------------------------------------------------------------------------
-__global__ void scatter_kernel(uint32_t *track, const uint32_t *__restrict__ pos,
+// host pairs -> one uint8 track (counts >= 255 become the escape byte; the
+// host keeps their values in the unit's overflow table)
+__global__ void scatter_kernel(uint8_t *track, const uint32_t *__restrict__ pos,
                                const uint32_t *__restrict__ cnt, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) track[kPad + pos[i] - 1] = cnt[i];
+    if (i < n) track[kPad + pos[i] - 1] = (uint8_t)(cnt[i] >= kEsc ? kEsc : cnt[i]);
+}
+
+// dense device uint32 counts (position p at src[p-1]) -> uint8 track;
+// counts >= 255 are appended to an overflow list (pos << 32 | count)
+__global__ void pack_kernel(uint8_t *track, const uint32_t *__restrict__ src, uint64_t len,
+                            unsigned long long *ovf, uint32_t *novf, uint32_t cap) {
+    const uint64_t i4 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i4 >= len) return;
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t i = i4 + k;
+        uint32_t c = i < len ? src[i] : 0u;
+        if (c >= kEsc) {
+            const uint32_t slot = atomicAdd(novf, 1u);
+            if (slot < cap) ovf[slot] = ((unsigned long long)(i + 1) << 32) | c;
+            c = kEsc;
+        }
+        out |= c << (8 * k);
+    }
+    // kPad and p-1 = i4 are multiples of 4: one aligned dword store
+    if (i4 + 4 <= len) {
+        *(uint32_t *)(track + kPad + i4) = out;
+    } else {
+        for (int k = 0; i4 + k < len; ++k) track[kPad + i4 + k] = (uint8_t)(out >> (8 * k));
+    }
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -773,7 +917,9 @@ struct SynthThr {
     uint64_t t[6];
 };
 
-__global__ void synth_bg_kernel(uint32_t *track, uint64_t tkey, int64_t lo, int64_t hi,
+// synthetic counts are generated into a dense uint32 staging track
+// (position p at stage[p-1]) and packed by pack_kernel
+__global__ void synth_bg_kernel(uint32_t *stage, uint64_t tkey, int64_t lo, int64_t hi,
                                 SynthThr thr) {
     const int64_t x = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x > hi) return;
@@ -781,15 +927,28 @@ __global__ void synth_bg_kernel(uint32_t *track, uint64_t tkey, int64_t lo, int6
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) c += u >= thr.t[k];
-    track[kPad + x - 1] = c;
+    stage[x - 1] = c;
 }
 
-__global__ void track_sum_kernel(const uint32_t *__restrict__ t, uint64_t n,
-                                 unsigned long long *out) {
+// sum of a uint8 track's bytes, escapes excluded (their counts are added on
+// the host from the overflow table)
+__global__ void track_sum_kernel(const uint8_t *__restrict__ t, uint64_t n, unsigned long long *out) {
     uint64_t acc = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        acc += t[i];
+    const u32x4 *v = (const u32x4 *)t;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 16;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const u32x4 x = v[i];
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t y = w[k];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t c = (y >> (8 * b)) & 0xFFu;
+                acc += c == kEsc ? 0u : c;
+            }
+        }
+    }
     __shared__ unsigned long long red[256];
     red[threadIdx.x] = acc;
     __syncthreads();
@@ -800,9 +959,9 @@ __global__ void track_sum_kernel(const uint32_t *__restrict__ t, uint64_t n,
     if (threadIdx.x == 0) atomicAdd(out, red[0]);
 }
 
-__global__ void synth_peak_kernel(uint32_t *track, const uint32_t *__restrict__ pos, uint64_t n) {
+__global__ void synth_peak_kernel(uint32_t *stage, const uint32_t *__restrict__ pos, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(&track[kPad + pos[i] - 1], 1u);
+    if (i < n) atomicAdd(&stage[pos[i] - 1], 1u);
 }
 
 }  // namespace upk
