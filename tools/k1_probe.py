@@ -25,14 +25,14 @@ def main():
     lens = [int(l.split()[1]) for l in open(os.path.join(ROOT, "unipeak_amd", "data", "hg19.txt"))
             if l.strip()][:args.contigs]
     out = {}
-    for mode in ("synthetic", "zeros"):
+    for mode in ("synthetic", "nopeaks", "zeros"):
         with capi.Lib(0) as g:
             g.set_params(args.bw, 1, 0.00365)
             for st in (0, 1):
                 for ci, L in enumerate(lens):
                     u = g.add_unit(L, buffer_id=st)
-                    if mode == "synthetic":
-                        g.synth(u, 0, 0, 1000, ci, st, nondir=False, peaks=True)
+                    if mode != "zeros":
+                        g.synth(u, 0, 0, 1000, ci, st, nondir=False, peaks=mode == "synthetic")
             ks, walls = [], []
             for _ in range(args.reps):
                 n = g.run()

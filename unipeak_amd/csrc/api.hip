@@ -100,6 +100,7 @@ struct up_ctx {
     DevBuf<uint32_t> d_stage;          // dense uint32 staging for synth / pack
     DevBuf<unsigned long long> d_pack_ovf;
     DevBuf<uint32_t> d_pack_n;
+    DevBuf<unsigned long long> d_dbg;
     std::vector<Unit> units;
     bool units_dirty = true;
     DevBuf<UnitDesc> d_units;
@@ -224,7 +225,7 @@ void up_close(up_ctx *c) {
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
     c->hp_regions.release(); c->hp_counts.release();
-    c->d_wscreen.release(); c->d_stage.release(); c->d_pack_ovf.release(); c->d_pack_n.release();
+    c->d_wscreen.release(); c->d_stage.release(); c->d_dbg.release(); c->d_pack_ovf.release(); c->d_pack_n.release();
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -863,6 +864,12 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
         HIPCHK(c->d_ovf_rec.ensure((size_t)c->ovf_cap * kOvfStride));
         HIPCHK(hipMemsetAsync(c->d_ovf_count.p, 0, sizeof(uint32_t), c->stream));
         ScanParams SP = scan_params(c);
+        static const bool dbg = getenv("UNIPEAK_DEBUG_COUNTS") != nullptr;
+        if (dbg) {
+            HIPCHK(c->d_dbg.ensure(4));
+            HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 4 * sizeof(unsigned long long), c->stream));
+            SP.dbg = c->d_dbg.p;
+        }
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
         dispatch_scan<false>(c, SP, 0, ns);
         HIPCHK(hipGetLastError());
@@ -881,6 +888,11 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
         if (ovf > c->ovf_cap) {  // more spilled strips than slots: grow and redo
             c->ovf_cap = ovf + ovf / 2 + 64;
             continue;
+        }
+        if (dbg) {
+            unsigned long long h[4];
+            HIPCHK(hipMemcpy(h, c->d_dbg.p, sizeof h, hipMemcpyDeviceToHost));
+            fprintf(stderr, "unipeak_hip: K1 strips %u exact blocks %llu live words %llu\n", ns, h[0], h[1]);
         }
         const uint64_t tot = tail[0] + tail[1];
         const uint64_t nst = tot & 0xFFFFFFFFull, nen = tot >> 32;

@@ -66,6 +66,7 @@ struct ScanParams {
     uint32_t *ovf_count;
     uint32_t *ovf_rec;      // [ovf_cap][kOvfStride]
     uint32_t ovf_cap;
+    unsigned long long *dbg;  // optional counters: exact blocks, live words, hits walked
     double *prof_f, *prof_r;  // optional dense profile of one unit
     uint32_t prof_unit, prof_len;
 };

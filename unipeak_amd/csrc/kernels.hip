@@ -138,6 +138,24 @@ __device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], const UnitDesc &
     }
 }
 
+constexpr int kHB = 4;  // hits per batch in the KDE walks
+
+// next batch of up to kHB set bits of m (ascending) with their broadcast counts
+template <typename T>
+__device__ __forceinline__ void next_hits(uint64_t &m, T v, int (&b)[kHB], double (&c)[kHB]) {
+#pragma unroll
+    for (int h = 0; h < kHB; ++h) {
+        if (m) {
+            b[h] = __builtin_ctzll(m);
+            m &= m - 1;
+            c[h] = rl_cs(v, b[h]);
+        } else {
+            b[h] = -1024;
+            c[h] = 0.0;
+        }
+    }
+}
+
 // KDE value of lane's position in output word K: ascending walk over the
 // hits of words K-NH..K+NH (window-masked).  K must be a compile-time index.
 template <int NWT, int NH, int K, typename T>
@@ -148,12 +166,22 @@ __device__ __forceinline__ double kde_word(const T (&cs)[NWT], const uint64_t (&
 #pragma unroll
     for (int d = -NH; d <= NH; ++d) {
         uint64_t m = hm[K + d] & wm[d + NH];
-        while (m) {
-            const int b = __builtin_ctzll(m);
-            m &= m - 1;
-            const double c = rl_cs(cs[K + d], b);
-            const int idx = lane + (bw - 64 * d - b);
-            if ((unsigned)idx <= (unsigned)(2 * bw)) f = f + ktab[idx] * c;
+        while (m) {  // batches of kHB hits: weight reads first, adds in order
+            int b[kHB];
+            double c[kHB], kv[kHB];
+            bool in[kHB];
+            next_hits(m, cs[K + d], b, c);
+#pragma unroll
+            for (int h = 0; h < kHB; ++h) {
+                const int idx = lane + (bw - 64 * d - b[h]);
+                in[h] = (unsigned)idx <= (unsigned)(2 * bw);
+                kv[h] = ktab[in[h] ? idx : 0];
+            }
+#pragma unroll
+            for (int h = 0; h < kHB; ++h) {
+                const double v = f + kv[h] * c[h];
+                f = in[h] ? v : f;
+            }
         }
     }
     return f;
@@ -229,21 +257,33 @@ __device__ __forceinline__ void rec_push(RecList &R, bool start, uint32_t pos, c
     ++n;
 }
 
-// scatter one hit (window word W, bit b, pooled count c) into the register
-// accumulators of the output words it can reach: branch-free, predicated
-// per lane, so the only scalar work per hit is the bit walk itself
+// scatter up to kHB hits (window word W, bits b[], pooled counts c[], in
+// ascending order; b = -1024 marks an unused slot) into the register
+// accumulators of the live output words they reach.  The kernel-weight reads
+// of the whole batch are issued before the first add, so the LDS latency is
+// paid once per batch rather than once per hit; the adds stay in hit order
+// (mul, then add: the reference's accumulation, peakcall.cpp:203-209).
 template <int NH, int SW, int W, typename A>
-__device__ __forceinline__ void scatter_hit(A (&acc)[SW], int b, double c, int lane, int bw,
-                                            const double *ktab) {
+__device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], const double (&c)[kHB],
+                                             int lane, int bw, const double *ktab, uint32_t live) {
     WordLoop<W - NH, W + NH + 1>::run([&](auto tc) {
         constexpr int t = decltype(tc)::value;
         if constexpr (t >= NH && t < NH + SW) {
+            if (!((live >> (t - NH)) & 1u)) return;  // uniform: word holds no flag
             // output word t-NH, lane position 64(t-NH)+lane; hit at 64(W-NH)+b
-            const int idx = lane + bw - b + 64 * (t - W);
-            const bool in = (unsigned)idx <= (unsigned)(2 * bw);
-            const int ci = in ? idx : 0;
-            const double v = acc[t - NH] + ktab[ci] * c;
-            acc[t - NH] = in ? v : acc[t - NH];
+            double kv[kHB];
+            bool in[kHB];
+#pragma unroll
+            for (int h = 0; h < kHB; ++h) {
+                const int idx = lane + bw - b[h] + 64 * (t - W);
+                in[h] = (unsigned)idx <= (unsigned)(2 * bw);
+                kv[h] = ktab[in[h] ? idx : 0];
+            }
+#pragma unroll
+            for (int h = 0; h < kHB; ++h) {
+                const double v = acc[t - NH] + kv[h] * c[h];
+                acc[t - NH] = in[h] ? v : acc[t - NH];
+            }
         }
     });
 }
@@ -328,6 +368,9 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
 
         // ---- screen: which blocks can hold a flagged position ----
         uint32_t exact_blocks = 0xFFFFu;
+        // live words: word q of lane l's 4 words (chunks 16l+4q..16l+4q+3);
+        // word w of block b is bit (4b + w/4) of live[w % 4]
+        uint64_t live[4] = {~0ull, ~0ull, ~0ull, ~0ull};
         if constexpr (!PROF) {
             uint32_t cs[kBlocks];
             uint32_t big = 0, hs = 0;
@@ -379,6 +422,8 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
             default: m = screen_bits<8>(a, P.wskip); break;
             }
             const uint64_t lanes = __ballot(m != 0u);  // lane l covers chunks 16l..16l+15
+#pragma unroll
+            for (int q = 0; q < 4; ++q) live[q] = __ballot(((m >> (4 * q)) & 0xFu) != 0u);
             exact_blocks = 0;
 #pragma unroll
             for (int bk = 0; bk < kBlocks; ++bk)
@@ -408,6 +453,15 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
                 }
                 continue;
             }
+            // words of this block that can hold a flag (the others keep F = 0
+            // and receive no scatter)
+            uint32_t lw = 0;
+#pragma unroll
+            for (int w = 0; w < SW; ++w) lw |= (uint32_t)((live[w & 3] >> (4 * j + (w >> 2))) & 1ull) << w;
+            if (P.dbg && lane == 0) {
+                atomicAdd(&P.dbg[0], 1ull);
+                atomicAdd(&P.dbg[1], (unsigned long long)__builtin_popcount(lw));
+            }
             const int64_t x0 = p0 + 64 * (j * SW - NH);  // position of window word 0, lane 0
             T wf[NWIN], wr[NONDIR ? NWIN : 1];
             uint64_t hf[NWIN], hr[NONDIR ? NWIN : 1];
@@ -427,22 +481,29 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
             }
             WordLoop<0, NWIN>::run([&](auto wc) {
                 constexpr int W = decltype(wc)::value;
+                // output words a hit of window word W reaches: W-2NH .. W
+                constexpr int OLO = W - 2 * NH < 0 ? 0 : W - 2 * NH;
+                constexpr int OHI = W > SW - 1 ? SW - 1 : W;
+                const uint32_t reach = lw & (((2u << OHI) - 1u) & ~((1u << OLO) - 1u));
+                if (!reach) return;
                 uint64_t m = hf[W];
                 if constexpr (W < NH) m &= edge_lo[W];
                 if constexpr (W >= NH + SW) m &= edge_hi[W - NH - SW];
                 while (m) {
-                    const int b = __builtin_ctzll(m);
-                    m &= m - 1;
-                    scatter_hit<NH, SW, W>(af, b, rl_cs(wf[W], b), lane, bw, ktab);
+                    int hb[kHB];
+                    double hc[kHB];
+                    next_hits(m, wf[W], hb, hc);
+                    scatter_hits<NH, SW, W>(af, hb, hc, lane, bw, ktab, reach);
                 }
                 if constexpr (NONDIR) {
                     uint64_t q = hr[W];
                     if constexpr (W < NH) q &= edge_lo[W];
                     if constexpr (W >= NH + SW) q &= edge_hi[W - NH - SW];
                     while (q) {
-                        const int b = __builtin_ctzll(q);
-                        q &= q - 1;
-                        scatter_hit<NH, SW, W>(ar, b, rl_cs(wr[W], b), lane, bw, ktab);
+                        int hb[kHB];
+                        double hc[kHB];
+                        next_hits(q, wr[W], hb, hc);
+                        scatter_hits<NH, SW, W>(ar, hb, hc, lane, bw, ktab, reach);
                     }
                 }
             });
@@ -452,6 +513,7 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
             for (int k = 0; k < SW; ++k) {
                 if constexpr (NONDIR) sc[k] = af[k] + ar[k];  // forwardScore + reverseScore
                 else sc[k] = af[k];
+                if constexpr (!PROF) sc[k] = ((lw >> k) & 1u) ? sc[k] : -1.0;  // dead word: no flag
                 mx = __builtin_fmax(mx, sc[k]);
             }
             if constexpr (PROF) {
