@@ -112,16 +112,15 @@ def main():
         n = g.run()
         regs, cnt = g.regions_view()
         t2 = time.perf_counter()
+        res = None
         if comm is not None:
             parts = comm.gather_records(regs, cnt)
-            if parts is not None:
+            if parts is not None:  # rank 0: records of every rank in global unit order
                 parts = [(r, mine_all[i], e) for i, (r, e) in enumerate(parts)]
-        else:
-            parts = [(regs, mine, cnt)]
-        res = None
-        if parts is not None:
-            recs, gid, _ = shard.merge(parts, len(units), capi.REGION_DTYPE)
-            res = (len(recs), int(np.count_nonzero(recs["accepted"])))
+                recs, gid, _ = shard.merge(parts, len(units), capi.REGION_DTYPE)
+                res = (len(recs), int(np.count_nonzero(recs["accepted"])))
+        else:  # one rank: units were added in global order, records are unit-major
+            res = (len(regs), int(np.count_nonzero(regs["accepted"])))
         t3 = time.perf_counter()
         phase["allreduce"] += t1 - t0
         phase["run"] += t2 - t1

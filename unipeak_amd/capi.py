@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libunipeak_hip.so")
+# UNIPEAK_LIB overrides the in-tree build (A/B experiments with variant builds)
+LIB_PATH = os.environ.get("UNIPEAK_LIB") or os.path.join(_HERE, "lib", "libunipeak_hip.so")
 
 UP_OK = 0
 

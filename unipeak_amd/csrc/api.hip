@@ -60,24 +60,28 @@ struct DevBuf {
     }
 };
 
-// pinned host staging (results always end on the host)
+// pinned, device-mapped host memory: kernels write results straight into it
+// (coherent, so the writes are visible to the host once the stream syncs)
 template <typename T>
 struct HostBuf {
-    T *p = nullptr;
+    T *p = nullptr;    // host address
+    T *dev = nullptr;  // device address of the same memory
     size_t n = 0;
     hipError_t ensure(size_t want) {
         if (want <= n && p) return hipSuccess;
         if (p) (void)hipHostFree(p);
-        p = nullptr;
+        p = dev = nullptr;
         n = 0;
         size_t cap = want < 16 ? 16 : want + want / 4;
-        hipError_t e = hipHostMalloc((void **)&p, cap * sizeof(T), hipHostMallocDefault);
+        hipError_t e = hipHostMalloc((void **)&p, cap * sizeof(T), hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) return e;
+        e = hipHostGetDevicePointer((void **)&dev, p, 0);
         if (e == hipSuccess) n = cap;
         return e;
     }
     void release() {
         if (p) (void)hipHostFree(p);
-        p = nullptr;
+        p = dev = nullptr;
         n = 0;
     }
 };
@@ -110,8 +114,8 @@ struct up_ctx {
     DevBuf<uint32_t> d_rec, d_lastnz, d_ovf_count, d_ovf_rec, d_unit_last;
     DevBuf<uint64_t> d_cnt, d_off, d_nreg;
     DevBuf<unsigned char> d_tmp;
-    DevBuf<uint32_t> d_starts, d_ends, d_runit, d_counts;
-    DevBuf<up_region> d_regions;
+    DevBuf<uint32_t> d_starts, d_ends, d_runit, d_peak_pos, d_rec_pkp, d_ovf_pkp;
+    DevBuf<double> d_peak_val, d_rec_pkv, d_ovf_pkv;
     uint32_t ovf_cap = 256;
     uint64_t nreg = 0;
     bool ran = false;
@@ -130,6 +134,9 @@ struct up_ctx {
     std::vector<uint32_t> h_head;
     HostBuf<up_region> hp_regions;
     HostBuf<uint32_t> hp_counts;
+    HostBuf<unsigned long long> hp_status;
+    uint64_t reg_cap = 1u << 16;  // record capacity of one pass (grown on demand)
+    uint64_t last_nreg = 0;
 };
 
 #define HIPCHK(x)                                                                   \
@@ -219,12 +226,13 @@ void up_close(up_ctx *c) {
     c->d_units.release(); c->d_info.release(); c->d_rec.release(); c->d_lastnz.release();
     c->d_ovf_count.release(); c->d_ovf_rec.release(); c->d_unit_last.release();
     c->d_cnt.release(); c->d_off.release(); c->d_nreg.release(); c->d_tmp.release();
-    c->d_starts.release(); c->d_ends.release(); c->d_runit.release(); c->d_counts.release();
-    c->d_regions.release();
+    c->d_starts.release(); c->d_ends.release(); c->d_runit.release();
+    c->d_peak_pos.release(); c->d_rec_pkp.release(); c->d_ovf_pkp.release();
+    c->d_peak_val.release(); c->d_rec_pkv.release(); c->d_ovf_pkv.release();
     c->d_head.release(); c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
-    c->hp_regions.release(); c->hp_counts.release();
+    c->hp_regions.release(); c->hp_counts.release(); c->hp_status.release();
     c->d_wscreen.release(); c->d_stage.release(); c->d_dbg.release(); c->d_pack_ovf.release(); c->d_pack_n.release();
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
@@ -618,6 +626,10 @@ static ScanParams scan_params(up_ctx *c) {
     P.thr = c->p.region_thr;
     P.strip_info = c->d_info.p;
     P.rec = c->d_rec.p;
+    P.rec_pkp = c->d_rec_pkp.p;
+    P.rec_pkv = c->d_rec_pkv.p;
+    P.ovf_pkp = c->d_ovf_pkp.p;
+    P.ovf_pkv = c->d_ovf_pkv.p;
     P.ovf_count = c->d_ovf_count.p;
     P.ovf_rec = c->d_ovf_rec.p;
     P.ovf_cap = c->ovf_cap;
@@ -666,9 +678,12 @@ static StatParams stat_params(up_ctx *c) {
     P.starts = c->d_starts.p;
     P.ends = c->d_ends.p;
     P.reg_unit = c->d_runit.p;
+    P.peak_pos = nullptr;  // set by up_run (known peaks from K1)
+    P.peak_val = nullptr;
     P.nreg = c->d_nreg.p;
-    P.out = c->d_regions.p;
-    P.out_counts = c->d_counts.p;
+    P.out = nullptr;  // set by up_run (mapped host records)
+    P.out_counts = nullptr;
+    P.cap = 0;
     return P;
 }
 
@@ -679,7 +694,7 @@ static void dispatch_stats(up_ctx *c, const StatParams &P, uint64_t nreg) {
     uint64_t blocks = (nreg + 3) / 4;
     if (blocks > 4096) blocks = 4096;
     if (blocks == 0) return;
-    const size_t lds = (2 * (size_t)P.bw + 1) * sizeof(double);
+    const size_t lds = kStatLds;
 #define UPK_ST(NH, PL, ND)                                                                   \
     if (nh == NH && pool == PL && nd == ND) {                                                \
         hipLaunchKernelGGL((stats_kernel<NH, PL, ND>), dim3((unsigned)blocks), dim3(256), lds, \
@@ -850,21 +865,42 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     }
     if ((r = sync_units(c))) return r;
     const uint32_t ns = c->nstrips;
+    const int S = c->p.n_samples;
     HIPCHK(c->d_info.ensure(ns));
     HIPCHK(c->d_rec.ensure((size_t)ns * 2 * kCap));
+    HIPCHK(c->d_rec_pkp.ensure((size_t)ns * kCap));
+    HIPCHK(c->d_rec_pkv.ensure((size_t)ns * kCap));
     HIPCHK(c->d_cnt.ensure(ns));
     HIPCHK(c->d_off.ensure(ns));
     HIPCHK(c->d_ovf_count.ensure(1));
     HIPCHK(c->d_nreg.ensure(1));
+    HIPCHK(c->hp_status.ensure(4));
     size_t tmp = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, c->d_cnt.p, c->d_off.p, (int)ns, c->stream));
     HIPCHK(c->d_tmp.ensure(tmp + 16));
+    static const bool dbg = getenv("UNIPEAK_DEBUG_COUNTS") != nullptr;
 
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    // One stream-ordered pass K1 -> K2 -> K3 with no host round trip: the
+    // region count stays on the device, the record areas are pre-sized
+    // (reg_cap, ovf_cap) and K3 writes the records straight into mapped
+    // pinned host memory.  An undersized area is detected after the single
+    // sync; it is grown and the pass rerun (first runs only).
+    uint64_t nreg = 0;
+    for (int attempt = 0;; ++attempt) {
+        if (attempt == 3) return UP_E_INTERNAL;
+        const uint64_t cap = c->reg_cap;
         HIPCHK(c->d_ovf_rec.ensure((size_t)c->ovf_cap * kOvfStride));
+        HIPCHK(c->d_ovf_pkp.ensure((size_t)c->ovf_cap * kOvfHalf));
+        HIPCHK(c->d_ovf_pkv.ensure((size_t)c->ovf_cap * kOvfHalf));
+        HIPCHK(c->d_peak_pos.ensure(cap + 1));
+        HIPCHK(c->d_peak_val.ensure(cap + 1));
+        HIPCHK(c->d_starts.ensure(cap + 1));
+        HIPCHK(c->d_ends.ensure(cap + 1));
+        HIPCHK(c->d_runit.ensure(cap + 1));
+        HIPCHK(c->hp_regions.ensure(cap + 1));
+        HIPCHK(c->hp_counts.ensure((cap + 1) * S));
         HIPCHK(hipMemsetAsync(c->d_ovf_count.p, 0, sizeof(uint32_t), c->stream));
         ScanParams SP = scan_params(c);
-        static const bool dbg = getenv("UNIPEAK_DEBUG_COUNTS") != nullptr;
         if (dbg) {
             HIPCHK(c->d_dbg.ensure(4));
             HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 4 * sizeof(unsigned long long), c->stream));
@@ -879,53 +915,42 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
         HIPCHK(hipGetLastError());
         size_t tb = c->d_tmp.n;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->d_tmp.p, tb, c->d_cnt.p, c->d_off.p, (int)ns, c->stream));
-        uint64_t tail[2];
-        uint32_t ovf = 0;
-        HIPCHK(hipMemcpyAsync(&tail[0], c->d_cnt.p + ns - 1, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(&tail[1], c->d_off.p + ns - 1, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(&ovf, c->d_ovf_count.p, 4, hipMemcpyDeviceToHost, c->stream));
+        hipLaunchKernelGGL(total_kernel, dim3(1), dim3(1), 0, c->stream, c->d_cnt.p, c->d_off.p, ns,
+                           c->d_ovf_count.p, c->d_nreg.p, c->hp_status.dev);
+        hipLaunchKernelGGL(compact_kernel, dim3((ns + 255) / 256), dim3(256), 0, c->stream, c->d_units.p,
+                           (uint32_t)c->units.size(), c->d_info.p, c->d_cnt.p, c->d_off.p, c->d_rec.p,
+                           c->d_ovf_rec.p, c->ovf_cap, c->d_rec_pkp.p, c->d_rec_pkv.p, c->d_ovf_pkp.p,
+                           c->d_ovf_pkv.p, c->d_starts.p, c->d_ends.p, c->d_runit.p, c->d_peak_pos.p,
+                           c->d_peak_val.p, ns, (uint64_t)cap);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev[2], c->stream));
+        StatParams P = stat_params(c);
+        P.cap = cap;
+        P.peak_pos = c->d_peak_pos.p;
+        P.peak_val = c->d_peak_val.p;
+        P.out = c->hp_regions.dev;
+        P.out_counts = c->hp_counts.dev;
+        dispatch_stats(c, P, std::max<uint64_t>(c->last_nreg, 1024));
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev[3], c->stream));
+        if ((r = launch_head_detect(c))) return r;
         HIPCHK(hipStreamSynchronize(c->stream));
-        if (ovf > c->ovf_cap) {  // more spilled strips than slots: grow and redo
-            c->ovf_cap = ovf + ovf / 2 + 64;
-            continue;
-        }
+        const unsigned long long *st = c->hp_status.p;
+        if (st[2]) return UP_E_INTERNAL;  // starts and ends disagree
+        nreg = st[0];
+        const uint64_t ovf = st[1];
+        bool again = false;
+        if (ovf > c->ovf_cap) { c->ovf_cap = (uint32_t)(ovf + ovf / 2 + 64); again = true; }
+        if (nreg > cap) { c->reg_cap = nreg + nreg / 4 + 1024; again = true; }
         if (dbg) {
             unsigned long long h[4];
             HIPCHK(hipMemcpy(h, c->d_dbg.p, sizeof h, hipMemcpyDeviceToHost));
             fprintf(stderr, "unipeak_hip: K1 strips %u exact blocks %llu live words %llu\n", ns, h[0], h[1]);
         }
-        const uint64_t tot = tail[0] + tail[1];
-        const uint64_t nst = tot & 0xFFFFFFFFull, nen = tot >> 32;
-        if (nst != nen) return UP_E_INTERNAL;
-        c->nreg = nst;
-        break;
+        if (!again) break;
     }
-    const uint64_t nreg = c->nreg;
-    HIPCHK(c->d_starts.ensure(nreg + 1));
-    HIPCHK(c->d_ends.ensure(nreg + 1));
-    HIPCHK(c->d_runit.ensure(nreg + 1));
-    HIPCHK(c->d_regions.ensure(nreg + 1));
-    HIPCHK(c->d_counts.ensure((nreg + 1) * c->p.n_samples));
-    hipLaunchKernelGGL(compact_kernel, dim3((ns + 255) / 256), dim3(256), 0, c->stream, c->d_units.p,
-                       (uint32_t)c->units.size(), c->d_info.p, c->d_cnt.p, c->d_off.p, c->d_rec.p,
-                       c->d_ovf_rec.p, c->ovf_cap, c->d_starts.p, c->d_ends.p, c->d_runit.p, ns);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(c->d_nreg.p, &c->nreg, 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipEventRecord(c->ev[2], c->stream));
-    StatParams P = stat_params(c);
-    dispatch_stats(c, P, nreg);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[3], c->stream));
-    if ((r = launch_head_detect(c))) return r;
-    HIPCHK(c->hp_regions.ensure(nreg + 1));
-    HIPCHK(c->hp_counts.ensure((nreg + 1) * c->p.n_samples));
-    if (nreg) {
-        HIPCHK(hipMemcpyAsync(c->hp_regions.p, c->d_regions.p, nreg * sizeof(up_region),
-                              hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(c->hp_counts.p, c->d_counts.p, nreg * c->p.n_samples * sizeof(uint32_t),
-                              hipMemcpyDeviceToHost, c->stream));
-    }
-    HIPCHK(hipStreamSynchronize(c->stream));
+    c->nreg = nreg;
+    c->last_nreg = nreg;
     if ((r = replay_head_hits(c))) return r;
     float a = 0, b = 0, d = 0;
     (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);

@@ -63,8 +63,12 @@ struct ScanParams {
     double thr;
     uint64_t *strip_info;
     uint32_t *rec;          // [nstrips][2*kCap]: starts then ends
+    uint32_t *rec_pkp;      // [nstrips][kCap]: peak position of each end's run (0: unknown)
+    double *rec_pkv;        // [nstrips][kCap]: peak score of each end's run
     uint32_t *ovf_count;
     uint32_t *ovf_rec;      // [ovf_cap][kOvfStride]
+    uint32_t *ovf_pkp;      // [ovf_cap][kOvfHalf]
+    double *ovf_pkv;        // [ovf_cap][kOvfHalf]
     uint32_t ovf_cap;
     unsigned long long *dbg;  // optional counters: exact blocks, live words, hits walked
     double *prof_f, *prof_r;  // optional dense profile of one unit
@@ -83,8 +87,11 @@ struct StatParams {
     int32_t want_corr;
     double region_thr, kurt_thr, corr_thr, hit_thr;
     const uint32_t *starts, *ends, *reg_unit;
+    const uint32_t *peak_pos;  // from K1 (0: unknown -> K3 computes it)
+    const double *peak_val;
     const uint64_t *nreg;
-    void *out;            // up_region records
+    uint64_t cap;         // records the output areas hold
+    void *out;            // up_region records (mapped host memory in up_run)
     uint32_t *out_counts; // [n][S]
 };
 

@@ -139,6 +139,8 @@ __device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], const UnitDesc &
 }
 
 constexpr int kHB = 4;  // hits per batch in the KDE walks
+constexpr int kStatCache = 16;  // K3: 64-position blocks of pass-1 totals kept in LDS
+constexpr size_t kStatLds = (2 * kMaxBw + 2) * sizeof(double) + 4 * kStatCache * 64 * sizeof(uint32_t);
 
 // next batch of up to kHB set bits of m (ascending) with their broadcast counts
 template <typename T>
@@ -223,6 +225,8 @@ __device__ __forceinline__ uint32_t find_unit(const UnitDesc *units, uint32_t nu
 // to an overflow slot (kOvfHalf each) by lane 0 when either list fills
 struct RecList {
     uint32_t *st, *en;
+    uint32_t *pkp;   // peak position per end (0: the run's start lies outside the strip)
+    double *pkv;     // peak score per end
     uint32_t ns, ne, cap;
     bool spilled, lost;
 };
@@ -239,22 +243,55 @@ __device__ __forceinline__ void rec_spill(RecList &R, const ScanParams &P, uint3
         return;
     }
     uint32_t *dst = P.ovf_rec + (uint64_t)slot * kOvfStride;
+    uint32_t *dpp = P.ovf_pkp + (uint64_t)slot * kOvfHalf;
+    double *dpv = P.ovf_pkv + (uint64_t)slot * kOvfHalf;
     if (lane == 0) {  // same lane wrote the inline records: program order suffices
         for (uint32_t i = 0; i < R.ns; ++i) dst[i] = R.st[i];
-        for (uint32_t i = 0; i < R.ne; ++i) dst[kOvfHalf + i] = R.en[i];
+        for (uint32_t i = 0; i < R.ne; ++i) {
+            dst[kOvfHalf + i] = R.en[i];
+            dpp[i] = R.pkp[i];
+            dpv[i] = R.pkv[i];
+        }
         inline_base[0] = slot;
     }
     R.st = dst;
     R.en = dst + kOvfHalf;
+    R.pkp = dpp;
+    R.pkv = dpv;
     R.cap = kOvfHalf;
 }
 
-__device__ __forceinline__ void rec_push(RecList &R, bool start, uint32_t pos, const ScanParams &P,
-                                         uint32_t *inline_base, int lane) {
-    uint32_t &n = start ? R.ns : R.ne;
-    if (n == R.cap && !R.spilled) rec_spill(R, P, inline_base, lane);
-    if (!R.lost && lane == 0) (start ? R.st : R.en)[n] = pos;
-    ++n;
+__device__ __forceinline__ void rec_start(RecList &R, uint32_t pos, const ScanParams &P,
+                                          uint32_t *inline_base, int lane) {
+    if (R.ns == R.cap && !R.spilled) rec_spill(R, P, inline_base, lane);
+    if (!R.lost && lane == 0) R.st[R.ns] = pos;
+    ++R.ns;
+}
+
+__device__ __forceinline__ void rec_end(RecList &R, uint32_t pos, uint32_t pk_pos, double pk_val,
+                                        const ScanParams &P, uint32_t *inline_base, int lane) {
+    if (R.ne == R.cap && !R.spilled) rec_spill(R, P, inline_base, lane);
+    if (!R.lost && lane == 0) {
+        R.en[R.ne] = pos;
+        R.pkp[R.ne] = pk_pos;
+        R.pkv[R.ne] = pk_val;
+    }
+    ++R.ne;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = __builtin_fmax(v, __shfl_xor(v, o));
+    return v;
 }
 
 // scatter up to kHB hits (window word W, bits b[], pooled counts c[], in
@@ -304,7 +341,8 @@ __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], 
 // keeps the reference's order; flags give run boundaries.
 // ------------------------------------------------------------------------
 constexpr int kScrWords = 8 + kBlocks * kWave + 8;  // chunk sums of one strip + halos
-constexpr size_t kScanLds = (2 * kMaxBw + 2) * sizeof(double) + 4 * kScrWords * sizeof(uint32_t);
+constexpr size_t kScanLds = (2 * kMaxBw + 2) * sizeof(double) + 4 * kScrWords * sizeof(uint32_t) +
+                            4 * kStepWords * kWave * sizeof(double);
 
 // chunk i (0..15) of this lane: window a[8+i-R .. 8+i+R] > wskip
 template <int R>
@@ -340,6 +378,8 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
     for (int i = threadIdx.x; i <= 2 * bw; i += blockDim.x) ktab[i] = P.kern[i];
     __syncthreads();
     uint32_t *scr = (uint32_t *)(ktab + 2 * kMaxBw + 2) + (threadIdx.x >> 6) * kScrWords;
+    double *scs = (double *)((uint32_t *)(ktab + 2 * kMaxBw + 2) + 4 * kScrWords) +
+                  (threadIdx.x >> 6) * (kStepWords * kWave);  // this wave's block scores
 
     constexpr int SW = kStepWords;
     constexpr int NWIN = SW + 2 * NH;
@@ -433,23 +473,31 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
         }
 
         uint32_t *inl = P.rec + (uint64_t)strip * (2 * kCap);
-        RecList R_{inl, inl + kCap, 0, 0, (uint32_t)kCap, false, false};
+        RecList R_{inl, inl + kCap, P.rec_pkp + (uint64_t)strip * kCap, P.rec_pkv + (uint64_t)strip * kCap,
+                   0, 0, (uint32_t)kCap, false, false};
         uint64_t prevF = 0, F0 = 0;
+        double lb = -__builtin_inf();  // open run: this lane's best f+r so far
+        uint32_t lp = 0;               // and its (first) position
+        bool pk_ok = false;            // the run started inside this strip
+        auto close_run = [&](uint32_t end_pos) {
+#ifdef UPK_EXP_NOPEAK_REDUCE
+            const double m = lb;
+            const uint32_t pp = lp;
+#else
+            const double m = wave_max_d(lb);
+            const uint32_t pp = wave_min_u32(lb == m ? lp : 0xFFFFFFFFu);
+#endif
+            rec_end(R_, end_pos, pk_ok ? pp : 0u, m, P, inl, lane);
+            lb = -__builtin_inf();
+        };
 
         for (int j = 0; j < kBlocks; ++j) {
             if (!((exact_blocks >> j) & 1u)) {
                 // no flag in this block: a run open at its left edge ends there
                 if constexpr (!PROF) {
-                    if (prevF) {
-                        uint64_t en = prevF & ~(prevF >> 1);
-                        const int64_t wpos = p0 + 64 * (j * SW - 1);
-                        while (en) {
-                            const int b = __builtin_ctzll(en);
-                            en &= en - 1;
-                            rec_push(R_, false, (uint32_t)(wpos + b), P, inl, lane);
-                        }
-                        prevF = 0;
-                    }
+                    if (prevF >> 63)  // the run open at the previous word's last lane ends there
+                        close_run((uint32_t)(p0 + 64 * (j * SW) - 1));
+                    prevF = 0;
                 }
                 continue;
             }
@@ -529,43 +577,71 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
                 // ---- flags and run boundaries (only blocks touching a run) ----
                 const uint64_t anyflag = __ballot(mx >= P.thr);
                 if (anyflag | prevF) {
+                    // scores through LDS so the word loop below stays a loop
+                    // (unrolled, its run bookkeeping overflows the I-cache)
 #pragma unroll
+                    for (int k = 0; k < SW; ++k) scs[64 * k + lane] = sc[k];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
                     for (int k = 0; k < SW; ++k) {
-                        const uint64_t F = __ballot(sc[k] >= P.thr);
+                        const double sck = scs[64 * k + lane];
+                        const uint64_t F = __ballot(sck >= P.thr);
                         const int64_t wpos = p0 + 64 * (j * SW + k);
+                        const bool cont = (prevF >> 63) != 0;  // run open at the previous position
+                        if (cont && !(F & 1ull)) close_run((uint32_t)(wpos - 1));
                         uint64_t st;
                         if (j == 0 && k == 0) {
                             F0 = F;
                             st = F & ~((F << 1) | 1ull);  // no interior start at p0
                         } else {
-                            st = F & ~((F << 1) | (prevF >> 63));
-                            uint64_t en = prevF & ~((prevF >> 1) | ((F & 1ull) << 63));
-                            while (en) {
-                                const int b = __builtin_ctzll(en);
-                                en &= en - 1;
-                                rec_push(R_, false, (uint32_t)(wpos - 64 + b), P, inl, lane);
-                            }
+                            st = F & ~((F << 1) | (cont ? 1ull : 0ull));
                         }
                         while (st) {
                             const int b = __builtin_ctzll(st);
                             st &= st - 1;
-                            rec_push(R_, true, (uint32_t)(wpos + b), P, inl, lane);
+                            rec_start(R_, (uint32_t)(wpos + b), P, inl, lane);
+                        }
+                        // per run segment of this word: running first maximum of
+                        // f+r per lane (Region::addPos, data.cpp:98-101); one
+                        // wave reduction when the run closes
+                        uint64_t rem = F;
+#ifdef UPK_EXP_NOSEG
+                        rem = 0;
+                        {
+                            uint64_t en = F & ~((F >> 1) | (1ull << 63));
+                            while (en) {
+                                const int b = __builtin_ctzll(en);
+                                en &= en - 1;
+                                rec_end(R_, (uint32_t)(wpos + b), 0u, 0.0, P, inl, lane);
+                            }
+                        }
+#endif
+                        while (rem) {
+                            const int a = __builtin_ctzll(rem);
+                            const uint64_t up = ~(rem >> a);
+                            const int len = up ? __builtin_ctzll(up) : 64 - a;
+                            const uint64_t seg = (len >= 64 ? ~0ull : ((1ull << len) - 1ull)) << a;
+                            rem &= ~seg;
+                            if (!(a == 0 && cont)) {  // a new run
+                                lb = -__builtin_inf();
+                                pk_ok = !(j == 0 && k == 0 && a == 0);  // may continue the previous strip
+                            }
+                            if (((seg >> lane) & 1ull) && sck > lb) {
+                                lb = sck;
+                                lp = (uint32_t)(wpos + lane);
+                            }
+                            if (a + len < 64) close_run((uint32_t)(wpos + a + len - 1));
                         }
                         prevF = F;
                     }
+                    __builtin_amdgcn_wave_barrier();  // scs reused by the next block
                 }
             }
         }
         if constexpr (PROF) continue;
-        {   // ends of the last word (no interior end at the strip's last position)
-            uint64_t en = prevF & ~((prevF >> 1) | (1ull << 63));
-            const int64_t wpos = p0 + kStrip - 64;
-            while (en) {
-                const int b = __builtin_ctzll(en);
-                en &= en - 1;
-                rec_push(R_, false, (uint32_t)(wpos + b), P, inl, lane);
-            }
-        }
+        // a run open at the strip's last position has no interior end (K2)
         const uint64_t info = (uint64_t)R_.ns | ((uint64_t)R_.ne << 16) | ((F0 & 1ull) << 32) |
                               ((prevF >> 63) << 33) | ((uint64_t)(local == 0) << 34) |
                               ((uint64_t)(local + 1 == U.nstrips) << 35) |
@@ -594,8 +670,11 @@ __global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
                                const uint64_t *__restrict__ info, const uint64_t *__restrict__ cnt,
                                const uint64_t *__restrict__ off, const uint32_t *__restrict__ rec,
                                const uint32_t *__restrict__ ovf_rec, uint32_t ovf_cap,
+                               const uint32_t *__restrict__ rec_pkp, const double *__restrict__ rec_pkv,
+                               const uint32_t *__restrict__ ovf_pkp, const double *__restrict__ ovf_pkv,
                                uint32_t *__restrict__ starts, uint32_t *__restrict__ ends,
-                               uint32_t *__restrict__ reg_unit, uint32_t n) {
+                               uint32_t *__restrict__ reg_unit, uint32_t *__restrict__ peak_pos,
+                               double *__restrict__ peak_val, uint32_t n, uint64_t cap) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t c = cnt[i];
@@ -615,10 +694,22 @@ __global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
         src = ovf_rec + (uint64_t)slot * kOvfStride;
         eoff = kOvfHalf;
     }
+    const uint32_t *spk = rec_pkp + (uint64_t)i * kCap;
+    const double *spv = rec_pkv + (uint64_t)i * kCap;
+    if (si_bit(v, 36)) {
+        const uint32_t slot = rec[(uint64_t)i * (2 * kCap)];
+        spk = ovf_pkp + (uint64_t)slot * kOvfHalf;
+        spv = ovf_pkv + (uint64_t)slot * kOvfHalf;
+    }
+    if (os + ns > cap || oe + ne > cap) return;  // host grows the areas and reruns
     if (xs) { starts[os] = (uint32_t)p0; reg_unit[os] = u; ++os; }
     for (uint32_t k = 0; k < si_starts(v); ++k) { starts[os] = src[k]; reg_unit[os] = u; ++os; }
-    for (uint32_t k = 0; k < si_ends(v); ++k) ends[oe++] = src[eoff + k];
-    if (xe) ends[oe++] = (uint32_t)(p0 + kStrip - 1);
+    for (uint32_t k = 0; k < si_ends(v); ++k) {
+        peak_pos[oe] = spk[k];
+        peak_val[oe] = spv[k];
+        ends[oe++] = src[eoff + k];
+    }
+    if (xe) { peak_pos[oe] = 0; peak_val[oe] = 0.0; ends[oe++] = (uint32_t)(p0 + kStrip - 1); }
 }
 
 // per-unit last add (the last position whose pooled count is nonzero): one
@@ -692,36 +783,113 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-    const uint64_t nreg = *P.nreg;
+    const uint64_t nreg = *P.nreg < P.cap ? *P.nreg : P.cap;
     uint64_t wm[2 * NH + 1];
 #pragma unroll
     for (int d = -NH; d <= NH; ++d) wm[d + NH] = win_mask(d, bw);
     const int S = P.S;  // <= 256 (checked by the host)
 
+    // per-wave cache of the pass-1 hit totals pc (pass 2 reads them back)
+    uint32_t *pcache = (uint32_t *)(ktab + 2 * kMaxBw + 2) + (threadIdx.x >> 6) * (kStatCache * 64);
+
     for (uint64_t ri = wave; ri < nreg; ri += nwaves) {
         const uint32_t left = P.starts[ri], right = P.ends[ri], u = P.reg_unit[ri];
         const UnitDesc U = P.units[u];
         uint32_t esum[4] = {0, 0, 0, 0};  // exptSums[s] lives in lane s%64, slot s/64
+        uint32_t esum1 = 0;               // S == 1: lane-local partial of exptSums[0]
 
         uint32_t cnt_acc = 0, sum_acc = 0;
         double best = 0.0;
         int64_t best_x = -1;
         double sf = 0.0, sr = 0.0;  // sequential sums of f and r (corr means)
         // ---- pass 1: scores, peak, exptSums, kurtosis first moments ----
-        for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
+        // POOL 0: raw bytes of the next 64-position window are fetched while
+        // the current one is scored (escapes resolved at use)
+        uint32_t nf[NWT], nr[NONDIR ? NWT : 1];
+        auto fetch_raw = [&](uint32_t (&dst)[NWT], int strand, int64_t x0) {
+            gu8 *t = track_u8(U, S, strand, P.nc[0]) + kPad + (x0 - 64 * NH) - 1 + lane;
+#pragma unroll
+            for (int w = 0; w < NWT; ++w) dst[w] = t[64 * w];
+        };
+        // K1 saw the whole run: its peak is known and, unless the strand
+        // correlation is wanted, no score is needed here -- only the counts
+        const bool known = P.peak_pos != nullptr && P.peak_pos[ri] != 0 && !(NONDIR && P.want_corr);
+        int blk = 0;
+        if (known) {
+            best = P.peak_val[ri];
+            best_x = P.peak_pos[ri];
+            for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64, ++blk) {
+                const int64_t x = x0 + lane;
+                const bool valid = x <= (int64_t)right;
+                WinT<POOL> c0[1], c1[1];
+                load_words<1, POOL>(c0, U, S, 0, x0, lane, P.nnc, P.nc, P.coef);
+                if constexpr (NONDIR) load_words<1, POOL>(c1, U, S, 1, x0, lane, P.nnc, P.nc, P.coef);
+                const bool h0 = valid && nz(c0[0]);
+                const bool h1 = NONDIR && valid && nz(c1[0]);
+                uint32_t pc = 0;
+                if (POOL == 0 && S == 1) {
+                    if (h0) pc += (uint32_t)c0[0];
+                    if (h1) pc += (uint32_t)c1[0];
+                    esum1 += pc;
+                } else {
+                    for (int s = 0; s < S; ++s) {
+                        uint32_t c = 0;
+                        if (h0) c += count_at(U, S, 0, s, x);
+                        if (h1) c += count_at(U, S, 1, s, x);
+                        pc += c;
+                        const uint32_t t = wave_sum_u32(c);
+                        if (lane == (s & 63)) {
+                            const int slot = s >> 6;
+                            esum[0] += slot == 0 ? t : 0u;
+                            esum[1] += slot == 1 ? t : 0u;
+                            esum[2] += slot == 2 ? t : 0u;
+                            esum[3] += slot == 3 ? t : 0u;
+                        }
+                    }
+                }
+                if (blk < kStatCache) pcache[64 * blk + lane] = pc;
+                cnt_acc += pc;
+                sum_acc += pc * (uint32_t)(uint16_t)(x - left);
+            }
+        }
+        if (!known) {
+        if constexpr (POOL == 0) {
+            fetch_raw(nf, 0, left);
+            if constexpr (NONDIR) fetch_raw(nr, 1, left);
+        }
+        for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64, ++blk) {
             const int64_t x = x0 + lane;
             const bool valid = x <= (int64_t)right;
             const int nvalid = (int)(((int64_t)right - x0 + 1) < 64 ? ((int64_t)right - x0 + 1) : 64);
             WinT<POOL> cf[NWT];
             uint64_t hf[NWT];
-            region_words<NH, POOL>(cf, hf, U, 0, x0, lane, P);
+            WinT<POOL> cr[NONDIR ? NWT : 1];
+            uint64_t hr[NONDIR ? NWT : 1];
+            if constexpr (POOL == 0) {
+                const int64_t xb = x0 - 64 * NH;
+#pragma unroll
+                for (int w = 0; w < NWT; ++w) {
+                    cf[w] = nf[w] == kEsc ? ovf_lookup(U, (uint32_t)P.nc[0], (uint32_t)(xb + 64 * w + lane)) : nf[w];
+                    if constexpr (NONDIR)
+                        cr[w] = nr[w] == kEsc ? ovf_lookup(U, (uint32_t)(S + P.nc[0]), (uint32_t)(xb + 64 * w + lane)) : nr[w];
+                }
+                if (x0 + 64 <= (int64_t)right) {
+                    fetch_raw(nf, 0, x0 + 64);
+                    if constexpr (NONDIR) fetch_raw(nr, 1, x0 + 64);
+                }
+#pragma unroll
+                for (int w = 0; w < NWT; ++w) {
+                    hf[w] = __ballot(cf[w] != 0u);
+                    if constexpr (NONDIR) hr[w] = __ballot(cr[w] != 0u);
+                }
+            } else {
+                region_words<NH, POOL>(cf, hf, U, 0, x0, lane, P);
+                if constexpr (NONDIR) region_words<NH, POOL>(cr, hr, U, 1, x0, lane, P);
+            }
             double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
             double r = 0.0;
             uint64_t hr_c = 0;
-            WinT<POOL> cr[NONDIR ? NWT : 1];
-            uint64_t hr[NONDIR ? NWT : 1];
             if constexpr (NONDIR) {
-                region_words<NH, POOL>(cr, hr, U, 1, x0, lane, P);
                 r = kde_word<NWT, NH, NH>(cr, hr, wm, lane, bw, ktab);
                 hr_c = hr[NH];
             }
@@ -736,22 +904,31 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             // stored hit vectors (peakcall.cpp:210-219; quirk Q7)
             const bool sf_hit = (hf[NH] >> lane) & 1, sr_hit = (hr_c >> lane) & 1;
             uint32_t pc = 0;
-            for (int s = 0; s < S; ++s) {
-                uint32_t c = 0;
+            if (POOL == 0 && S == 1) {  // the only sample is the pooled one
                 if (valid) {
-                    if (sf_hit) c += count_at(U, S, 0, s, x);
-                    if (NONDIR && sr_hit) c += count_at(U, S, 1, s, x);
+                    if (sf_hit) pc += (uint32_t)cf[NH];
+                    if (NONDIR && sr_hit) pc += (uint32_t)cr[NONDIR ? NH : 0];
                 }
-                pc += c;
-                const uint32_t t = wave_sum_u32(c);
-                if (lane == (s & 63)) {
-                    const int slot = s >> 6;
-                    esum[0] += slot == 0 ? t : 0u;
-                    esum[1] += slot == 1 ? t : 0u;
-                    esum[2] += slot == 2 ? t : 0u;
-                    esum[3] += slot == 3 ? t : 0u;
+                esum1 += pc;
+            } else {
+                for (int s = 0; s < S; ++s) {
+                    uint32_t c = 0;
+                    if (valid) {
+                        if (sf_hit) c += count_at(U, S, 0, s, x);
+                        if (NONDIR && sr_hit) c += count_at(U, S, 1, s, x);
+                    }
+                    pc += c;
+                    const uint32_t t = wave_sum_u32(c);
+                    if (lane == (s & 63)) {
+                        const int slot = s >> 6;
+                        esum[0] += slot == 0 ? t : 0u;
+                        esum[1] += slot == 1 ? t : 0u;
+                        esum[2] += slot == 2 ? t : 0u;
+                        esum[3] += slot == 3 ? t : 0u;
+                    }
                 }
             }
+            if (blk < kStatCache) pcache[64 * blk + lane] = pc;
             cnt_acc += pc;
             sum_acc += pc * (uint32_t)(uint16_t)(x - left);
         }
@@ -765,46 +942,56 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
                 best_x = ox;
             }
         }
+        }  // !known
+        if (POOL == 0 && S == 1) {
+            const uint32_t t = wave_sum_u32(esum1);
+            esum[0] = lane == 0 ? t : 0u;
+        }
         const uint32_t count = wave_sum_u32(cnt_acc);
         const uint32_t psum = wave_sum_u32(sum_acc);
 
         // ---- pass 2: kurtosis (data.cpp:164-182; powi semantics) ----
         const double x_bar = (double)psum / (double)count;
         double sum2 = 0.0, sum4 = 0.0;
-        for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
+        int blk2 = 0;
+        for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64, ++blk2) {
             const int64_t x = x0 + lane;
             const bool valid = x <= (int64_t)right;
-            double c0 = 0.0, c1 = 0.0;
-            // pooled count at x itself, per strand, to know what was stored
-            if (valid) {
-                if (POOL == 0) {
-                    c0 = (double)count_at(U, S, 0, P.nc[0], x);
-                    if (NONDIR) c1 = (double)count_at(U, S, 1, P.nc[0], x);
-                } else {
-                    for (int k = 0; k < P.nnc; ++k) {
-                        const double q = POOL == 2 ? P.coef[k] : 1.0;
-                        const uint32_t a = count_at(U, S, 0, P.nc[k], x);
-                        c0 = POOL == 2 ? c0 + (double)a * q : c0 + (double)a;
-                        if (NONDIR) {
-                            const uint32_t b = count_at(U, S, 1, P.nc[k], x);
-                            c1 = POOL == 2 ? c1 + (double)b * q : c1 + (double)b;
-                        }
-                    }
-                    if (POOL == 2) {
+            uint32_t pc = 0;
+            if (blk2 < kStatCache) {
+                pc = pcache[64 * blk2 + lane];
+            } else {
+                double c0 = 0.0, c1 = 0.0;
+                // pooled count at x itself, per strand, to know what was stored
+                if (valid) {
+                    if (POOL == 0) {
+                        c0 = (double)count_at(U, S, 0, P.nc[0], x);
+                        if (NONDIR) c1 = (double)count_at(U, S, 1, P.nc[0], x);
+                    } else {
                         for (int k = 0; k < P.nnc; ++k) {
-                            c0 = c0 + (double)count_at(U, S, 0, P.nc[k], x);
-                            if (NONDIR) c1 = c1 + (double)count_at(U, S, 1, P.nc[k], x);
+                            const double q = POOL == 2 ? P.coef[k] : 1.0;
+                            const uint32_t a = count_at(U, S, 0, P.nc[k], x);
+                            c0 = POOL == 2 ? c0 + (double)a * q : c0 + (double)a;
+                            if (NONDIR) {
+                                const uint32_t b = count_at(U, S, 1, P.nc[k], x);
+                                c1 = POOL == 2 ? c1 + (double)b * q : c1 + (double)b;
+                            }
+                        }
+                        if (POOL == 2) {
+                            for (int k = 0; k < P.nnc; ++k) {
+                                c0 = c0 + (double)count_at(U, S, 0, P.nc[k], x);
+                                if (NONDIR) c1 = c1 + (double)count_at(U, S, 1, P.nc[k], x);
+                            }
                         }
                     }
                 }
+                const bool h0 = valid && c0 != 0.0, h1 = valid && NONDIR && c1 != 0.0;
+                for (int s = 0; s < S; ++s) {
+                    if (h0) pc += count_at(U, S, 0, s, x);
+                    if (h1) pc += count_at(U, S, 1, s, x);
+                }
             }
-            const bool h0 = valid && c0 != 0.0, h1 = valid && NONDIR && c1 != 0.0;
-            uint32_t pc = 0;
-            for (int s = 0; s < S; ++s) {
-                if (h0) pc += count_at(U, S, 0, s, x);
-                if (h1) pc += count_at(U, S, 1, s, x);
-            }
-            uint64_t m = __ballot(h0 || h1);
+            uint64_t m = __ballot(pc != 0u);  // positions holding a stored hit vector
             while (m) {
                 const int l = __builtin_ctzll(m);
                 m &= m - 1;
@@ -845,32 +1032,47 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
         }
 
         // ---- processRegion filters (peakcall.cpp:33-53) ----
-        uint32_t nonctl = 0;
-        for (int s = 0; s < S; ++s) {
-            const int slot = s >> 6;
-            const uint32_t mine = slot == 0 ? esum[0] : slot == 1 ? esum[1] : slot == 2 ? esum[2] : esum[3];
-            const uint32_t v = rl_u(mine, s & 63);
-            if (!P.is_control[s]) nonctl += v;
-            if (lane == 0) P.out_counts[ri * S + s] = v;
+        // exptSums: lane s % 64 holds sample s (slot s / 64); one coalesced row
+        uint32_t nc_part = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int s = 64 * q + lane;
+            if (s < S) {
+                if (!P.is_control[s]) nc_part += esum[q];
+                P.out_counts[ri * S + s] = esum[q];
+            }
         }
+        const uint32_t nonctl = wave_sum_u32(nc_part);  // HitCount sum (wraps like the reference)
         bool acc = (double)nonctl >= P.hit_thr;
         if (acc) acc = P.kurt_thr == 0 || (n > 1 && kurt <= P.kurt_thr);
         if (acc) acc = P.corr_thr <= -1 || corr >= P.corr_thr;
-        if (lane == 0) {
-            up_region *o = (up_region *)P.out + ri;
-            o->unit = u;
-            o->left = left;
-            o->right = right;
-            o->peak = (uint32_t)best_x;
-            o->sum = count;
-            o->nonctl_sum = nonctl;
-            o->accepted = acc;
-            o->close_pos = UP_CLOSE_RULE;
-            o->peak_score = best;
-            o->kurtosis = kurt;
-            o->corr = corr;
+        // the 56-byte record as 7 words from lanes 0..6 (one write burst)
+        if (lane < 7) {
+            uint64_t w;
+            switch (lane) {
+            case 0: w = (uint64_t)u | ((uint64_t)left << 32); break;
+            case 1: w = (uint64_t)right | ((uint64_t)(uint32_t)best_x << 32); break;
+            case 2: w = (uint64_t)count | ((uint64_t)nonctl << 32); break;
+            case 3: w = (uint64_t)(uint32_t)(acc ? 1 : 0) | ((uint64_t)UP_CLOSE_RULE << 32); break;
+            case 4: w = (uint64_t)__double_as_longlong(best); break;
+            case 5: w = (uint64_t)__double_as_longlong(kurt); break;
+            default: w = (uint64_t)__double_as_longlong(corr); break;
+            }
+            ((uint64_t *)P.out)[ri * 7 + lane] = w;
         }
     }
+}
+
+// K2b': region count from the scan, on the device (no host round trip):
+// status[0] = regions, status[1] = spilled strips, status[2] = start/end mismatch
+__global__ void total_kernel(const uint64_t *cnt, const uint64_t *off, uint32_t ns,
+                             const uint32_t *ovf_count, uint64_t *nreg, unsigned long long *status) {
+    const uint64_t t = cnt[ns - 1] + off[ns - 1];
+    const uint64_t nst = t & 0xFFFFFFFFull, nen = t >> 32;
+    *nreg = nst;
+    status[0] = nst;
+    status[1] = *ovf_count;
+    status[2] = nst != nen;
 }
 
 // ------------------------------------------------------------------------
