@@ -135,7 +135,7 @@ def main():
         st = step()
         if rank == 0:
             tt = st[2]
-            print(f"[bench] warmup: K1 {tt[0]:.3f} ms, K2 {tt[1]:.3f} ms, K3 {tt[2]:.3f} ms, "
+            print(f"[bench] warmup: K1 {tt[0]:.3f} ms (exact part {tt[4]:.3f}), K2 {tt[1]:.3f} ms, K3 {tt[2]:.3f} ms, "
                   f"up_run wall {tt[3]:.3f} ms", file=sys.stderr, flush=True)
     for k in phase:
         phase[k] = 0.0

@@ -21,11 +21,12 @@ def main():
     ap.add_argument("--contigs", type=int, default=25)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--bw", type=int, default=50)
+    ap.add_argument("--modes", default="synthetic,nopeaks,zeros")
     args = ap.parse_args()
     lens = [int(l.split()[1]) for l in open(os.path.join(ROOT, "unipeak_amd", "data", "hg19.txt"))
             if l.strip()][:args.contigs]
     out = {}
-    for mode in ("synthetic", "nopeaks", "zeros"):
+    for mode in args.modes.split(","):
         with capi.Lib(0) as g:
             g.set_params(args.bw, 1, 0.00365)
             for st in (0, 1):
@@ -33,15 +34,17 @@ def main():
                     u = g.add_unit(L, buffer_id=st)
                     if mode != "zeros":
                         g.synth(u, 0, 0, 1000, ci, st, nondir=False, peaks=mode == "synthetic")
-            ks, walls = [], []
+            ks, walls, kb = [], [], []
             for _ in range(args.reps):
                 n = g.run()
                 t = g.timings()
                 ks.append(t[0])
+                kb.append(t[4])
                 walls.append(t[3])
             byt = 1 * 2 * sum(lens)  # uint8 per bp per strand
             k1 = float(np.median(ks))
-            out[mode] = {"k1_ms": round(k1, 4), "GBps": round(byt / k1 / 1e6, 1),
+            out[mode] = {"k1_ms": round(k1, 4), "k1b_ms": round(float(np.median(kb)), 4),
+                         "GBps": round(byt / k1 / 1e6, 1),
                          "wall_ms": round(float(np.median(walls)), 4), "regions": int(n)}
     print(json.dumps(out))
 

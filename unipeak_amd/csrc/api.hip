@@ -114,8 +114,8 @@ struct up_ctx {
     DevBuf<uint32_t> d_rec, d_lastnz, d_ovf_count, d_ovf_rec, d_unit_last;
     DevBuf<uint64_t> d_cnt, d_off, d_nreg;
     DevBuf<unsigned char> d_tmp;
-    DevBuf<uint32_t> d_starts, d_ends, d_runit, d_peak_pos, d_rec_pkp, d_ovf_pkp;
-    DevBuf<double> d_peak_val, d_rec_pkv, d_ovf_pkv;
+    DevBuf<uint32_t> d_starts, d_ends, d_runit, d_peak_pos, d_xlist, d_xcount;
+    DevBuf<double> d_peak_val;
     uint32_t ovf_cap = 256;
     uint64_t nreg = 0;
     bool ran = false;
@@ -227,8 +227,7 @@ void up_close(up_ctx *c) {
     c->d_ovf_count.release(); c->d_ovf_rec.release(); c->d_unit_last.release();
     c->d_cnt.release(); c->d_off.release(); c->d_nreg.release(); c->d_tmp.release();
     c->d_starts.release(); c->d_ends.release(); c->d_runit.release();
-    c->d_peak_pos.release(); c->d_rec_pkp.release(); c->d_ovf_pkp.release();
-    c->d_peak_val.release(); c->d_rec_pkv.release(); c->d_ovf_pkv.release();
+    c->d_peak_pos.release(); c->d_peak_val.release(); c->d_xlist.release(); c->d_xcount.release();
     c->d_head.release(); c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
@@ -626,32 +625,36 @@ static ScanParams scan_params(up_ctx *c) {
     P.thr = c->p.region_thr;
     P.strip_info = c->d_info.p;
     P.rec = c->d_rec.p;
-    P.rec_pkp = c->d_rec_pkp.p;
-    P.rec_pkv = c->d_rec_pkv.p;
-    P.ovf_pkp = c->d_ovf_pkp.p;
-    P.ovf_pkv = c->d_ovf_pkv.p;
     P.ovf_count = c->d_ovf_count.p;
     P.ovf_rec = c->d_ovf_rec.p;
     P.ovf_cap = c->ovf_cap;
+    P.xlist = c->d_xlist.p;
+    P.xcount = c->d_xcount.p;
     return P;
 }
 
-template <int NH, int POOL, bool ND, bool PROF>
+template <int NH, int POOL, bool ND, bool PROF, int MODE>
 static void launch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e) {
-    const uint32_t waves = e - b;
-    uint32_t blocks = (waves + 3) / 4;
-    if (blocks > 2048) blocks = 2048;
-    if (blocks == 0) return;
-    hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF>), dim3(blocks), dim3(256), kScanLds, c->stream, P, b, e);
+    uint32_t blocks;
+    if (MODE == kModeExact) {
+        blocks = 2048;  // grid-stride over the device-side work-list count
+    } else {
+        const uint32_t waves = e - b;
+        blocks = (waves + 3) / 4;
+        if (blocks > 2048) blocks = 2048;
+        if (blocks == 0) return;
+    }
+    const size_t lds = MODE == kModeScreen ? kScreenLds : MODE == kModeExact ? kExactLds : kScanLds;
+    hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF, MODE>), dim3(blocks), dim3(256), lds, c->stream, P, b, e);
 }
 
-template <bool PROF>
+template <bool PROF, int MODE>
 static void dispatch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e) {
     const int nh = P.bw <= 63 ? 1 : 2;
     const int pool = pool_mode(c);
     const bool nd = c->p.nondir != 0;
 #define UPK_SCAN(NH, PL, ND) \
-    if (nh == NH && pool == PL && nd == ND) return launch_scan<NH, PL, ND, PROF>(c, P, b, e);
+    if (nh == NH && pool == PL && nd == ND) return launch_scan<NH, PL, ND, PROF, MODE>(c, P, b, e);
     UPK_SCAN(1, 0, false) UPK_SCAN(1, 1, false) UPK_SCAN(1, 2, false)
     UPK_SCAN(1, 0, true) UPK_SCAN(1, 1, true) UPK_SCAN(1, 2, true)
     UPK_SCAN(2, 0, false) UPK_SCAN(2, 1, false) UPK_SCAN(2, 2, false)
@@ -867,9 +870,9 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     const uint32_t ns = c->nstrips;
     const int S = c->p.n_samples;
     HIPCHK(c->d_info.ensure(ns));
-    HIPCHK(c->d_rec.ensure((size_t)ns * 2 * kCap));
-    HIPCHK(c->d_rec_pkp.ensure((size_t)ns * kCap));
-    HIPCHK(c->d_rec_pkv.ensure((size_t)ns * kCap));
+    HIPCHK(c->d_rec.ensure((size_t)ns * kRecStride));
+    HIPCHK(c->d_xlist.ensure((size_t)ns * kXEntry));
+    HIPCHK(c->d_xcount.ensure(1));
     HIPCHK(c->d_cnt.ensure(ns));
     HIPCHK(c->d_off.ensure(ns));
     HIPCHK(c->d_ovf_count.ensure(1));
@@ -878,7 +881,9 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
     size_t tmp = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, c->d_cnt.p, c->d_off.p, (int)ns, c->stream));
     HIPCHK(c->d_tmp.ensure(tmp + 16));
+#ifdef UPK_DEBUG_COUNTS  // build with -DUPK_DEBUG_COUNTS, run with UNIPEAK_DEBUG_COUNTS=1
     static const bool dbg = getenv("UNIPEAK_DEBUG_COUNTS") != nullptr;
+#endif
 
     // One stream-ordered pass K1 -> K2 -> K3 with no host round trip: the
     // region count stays on the device, the record areas are pre-sized
@@ -890,8 +895,6 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
         if (attempt == 3) return UP_E_INTERNAL;
         const uint64_t cap = c->reg_cap;
         HIPCHK(c->d_ovf_rec.ensure((size_t)c->ovf_cap * kOvfStride));
-        HIPCHK(c->d_ovf_pkp.ensure((size_t)c->ovf_cap * kOvfHalf));
-        HIPCHK(c->d_ovf_pkv.ensure((size_t)c->ovf_cap * kOvfHalf));
         HIPCHK(c->d_peak_pos.ensure(cap + 1));
         HIPCHK(c->d_peak_val.ensure(cap + 1));
         HIPCHK(c->d_starts.ensure(cap + 1));
@@ -901,13 +904,19 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
         HIPCHK(c->hp_counts.ensure((cap + 1) * S));
         HIPCHK(hipMemsetAsync(c->d_ovf_count.p, 0, sizeof(uint32_t), c->stream));
         ScanParams SP = scan_params(c);
+#ifdef UPK_DEBUG_COUNTS
         if (dbg) {
-            HIPCHK(c->d_dbg.ensure(4));
-            HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 4 * sizeof(unsigned long long), c->stream));
+            HIPCHK(c->d_dbg.ensure(8));
+            HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 8 * sizeof(unsigned long long), c->stream));
             SP.dbg = c->d_dbg.p;
         }
+#endif
+        HIPCHK(hipMemsetAsync(c->d_xcount.p, 0, sizeof(uint32_t), c->stream));
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
-        dispatch_scan<false>(c, SP, 0, ns);
+        dispatch_scan<false, kModeScreen>(c, SP, 0, ns);   // K1a: stream + screen
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->ev[4], c->stream));
+        dispatch_scan<false, kModeExact>(c, SP, 0, ns);    // K1b: exact blocks
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
         hipLaunchKernelGGL(finalize_kernel, dim3((ns + 255) / 256), dim3(256), 0, c->stream,
@@ -919,8 +928,7 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
                            c->d_ovf_count.p, c->d_nreg.p, c->hp_status.dev);
         hipLaunchKernelGGL(compact_kernel, dim3((ns + 255) / 256), dim3(256), 0, c->stream, c->d_units.p,
                            (uint32_t)c->units.size(), c->d_info.p, c->d_cnt.p, c->d_off.p, c->d_rec.p,
-                           c->d_ovf_rec.p, c->ovf_cap, c->d_rec_pkp.p, c->d_rec_pkv.p, c->d_ovf_pkp.p,
-                           c->d_ovf_pkv.p, c->d_starts.p, c->d_ends.p, c->d_runit.p, c->d_peak_pos.p,
+                           c->d_ovf_rec.p, c->ovf_cap, c->d_starts.p, c->d_ends.p, c->d_runit.p, c->d_peak_pos.p,
                            c->d_peak_val.p, ns, (uint64_t)cap);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
@@ -942,17 +950,22 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
         bool again = false;
         if (ovf > c->ovf_cap) { c->ovf_cap = (uint32_t)(ovf + ovf / 2 + 64); again = true; }
         if (nreg > cap) { c->reg_cap = nreg + nreg / 4 + 1024; again = true; }
+#ifdef UPK_DEBUG_COUNTS
         if (dbg) {
-            unsigned long long h[4];
+            unsigned long long h[8];
             HIPCHK(hipMemcpy(h, c->d_dbg.p, sizeof h, hipMemcpyDeviceToHost));
-            fprintf(stderr, "unipeak_hip: K1 strips %u exact blocks %llu live words %llu\n", ns, h[0], h[1]);
+            fprintf(stderr, "unipeak_hip: K1 strips %u exact blocks %llu live words %llu hits %llu "
+                            "cycles load %llu scatter %llu\n", ns, h[0], h[1], h[2], h[3], h[4]);
         }
+#endif
         if (!again) break;
     }
     c->nreg = nreg;
     c->last_nreg = nreg;
     if ((r = replay_head_hits(c))) return r;
-    float a = 0, b = 0, d = 0;
+    float a = 0, b = 0, d = 0, x = 0;
+    (void)hipEventElapsedTime(&x, c->ev[4], c->ev[1]);
+    c->times[4] = x;  // K1b share of K1
     (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
     (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
     (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
@@ -1037,7 +1050,7 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
     StatParams P = stat_params(c);
     const int nh = P.bw <= 63 ? 1 : 2;
     const int pool = pool_mode(c);
-    const size_t lds = (2 * (size_t)P.bw + 1) * sizeof(double);
+    const size_t lds = kKTab * sizeof(double);
     const unsigned blocks = (unsigned)std::min<size_t>(n, 8192);
 #define UPK_SH(NH, PL)                                                                        \
     if (nh == NH && pool == PL)                                                               \
@@ -1076,7 +1089,7 @@ int up_unit_profile(up_ctx *c, uint32_t unit, double *out_f, double *out_r, uint
     P.prof_len = len;
     P.prof_unit = unit;
     const Unit &u = c->units[unit];
-    dispatch_scan<true>(c, P, u.strip0, u.strip0 + u.nstrips);
+    dispatch_scan<true, kModeFused>(c, P, u.strip0, u.strip0 + u.nstrips);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(out_f, d, (size_t)len * sizeof(double), hipMemcpyDeviceToHost));

@@ -24,8 +24,14 @@ constexpr int kPad = 256;           // zero bytes before position 1 and after th
 constexpr int kMaxBw = 127;         // register-resident halo: NH <= 2 words
 constexpr int kCap = 32;            // inline run records per strip (starts, ends each)
 constexpr int kOvfHalf = kStrip / 2 + 1;  // max starts (= max ends) of one strip
-constexpr int kOvfStride = 2 * kOvfHalf;  // starts + ends of one spilled strip
-constexpr uint32_t kEsc = 255;      // escape byte: count lives in the overflow table
+// record areas (uint32 words): starts [0,H), ends [H,2H), end-peak positions
+// [2H,3H), end-peak scores as doubles at word 4H (8-byte aligned); H = kCap
+// inline per strip, kOvfHalf per spilled strip's overflow slot
+constexpr int kRecStride = 6 * kCap;
+constexpr int kOvfStride = 6 * kOvfHalf;
+constexpr uint32_t kEsc = 255;
+constexpr int kXEntry = 2 + kWave / 2;  // strip, exact-block mask, 64 x 16-bit chunk masks
+constexpr int kModeFused = 0, kModeScreen = 1, kModeExact = 2;  // K1 variants      // escape byte: count lives in the overflow table
 constexpr uint32_t kBig = 1u << 22; // screen value of a chunk holding a byte >= 128
 
 struct UnitDesc {
@@ -62,15 +68,15 @@ struct ScanParams {
     int32_t bw;
     double thr;
     uint64_t *strip_info;
-    uint32_t *rec;          // [nstrips][2*kCap]: starts then ends
-    uint32_t *rec_pkp;      // [nstrips][kCap]: peak position of each end's run (0: unknown)
-    double *rec_pkv;        // [nstrips][kCap]: peak score of each end's run
+    uint32_t *rec;          // [nstrips][kRecStride]: starts, ends, end peaks (0: unknown)
     uint32_t *ovf_count;
     uint32_t *ovf_rec;      // [ovf_cap][kOvfStride]
-    uint32_t *ovf_pkp;      // [ovf_cap][kOvfHalf]
-    double *ovf_pkv;        // [ovf_cap][kOvfHalf]
+    uint32_t *xlist;        // K1a -> K1b work list: [nstrips][kXEntry]
+    uint32_t *xcount;       // entries in xlist
     uint32_t ovf_cap;
-    unsigned long long *dbg;  // optional counters: exact blocks, live words, hits walked
+#ifdef UPK_DEBUG_COUNTS
+    unsigned long long *dbg;  // counters: exact blocks, live words
+#endif
     double *prof_f, *prof_r;  // optional dense profile of one unit
     uint32_t prof_unit, prof_len;
 };

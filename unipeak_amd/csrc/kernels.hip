@@ -139,8 +139,24 @@ __device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], const UnitDesc &
 }
 
 constexpr int kHB = 4;  // hits per batch in the KDE walks
+// Kernel weights live in LDS with kKPad zero doubles on both sides, so every
+// (lane, hit) index of a window walk is a valid read and out-of-window pairs
+// add exactly +0 (accumulators start at +0 and never become -0, so x + 0 == x
+// bit for bit): no compare/select per pair.
+constexpr int kKPad = 64 * 3;
+constexpr int kKTab = 2 * kKPad + 2 * kMaxBw + 2;  // doubles of the padded table
+
+// fill the padded table; returns the pointer to weight 0
+__device__ __forceinline__ double *load_ktab(double *lds, const double *kern, int bw) {
+    for (int i = threadIdx.x; i < kKTab; i += blockDim.x) {
+        const int j = i - kKPad;
+        lds[i] = (j >= 0 && j <= 2 * bw) ? kern[j] : 0.0;
+    }
+    __syncthreads();
+    return lds + kKPad;
+}
 constexpr int kStatCache = 16;  // K3: 64-position blocks of pass-1 totals kept in LDS
-constexpr size_t kStatLds = (2 * kMaxBw + 2) * sizeof(double) + 4 * kStatCache * 64 * sizeof(uint32_t);
+constexpr size_t kStatLds = kKTab * sizeof(double) + 4 * kStatCache * 64 * sizeof(uint32_t);
 
 // next batch of up to kHB set bits of m (ascending) with their broadcast counts
 template <typename T>
@@ -151,11 +167,70 @@ __device__ __forceinline__ void next_hits(uint64_t &m, T v, int (&b)[kHB], doubl
             b[h] = __builtin_ctzll(m);
             m &= m - 1;
             c[h] = rl_cs(v, b[h]);
-        } else {
-            b[h] = -1024;
+        } else {  // unused slot: a +0 contribution from an in-range index
+            b[h] = 0;
             c[h] = 0.0;
         }
     }
+}
+
+// Same as load_words, but the N*64 bytes of each track are fetched with
+// 16-byte lane loads (one 1 KiB wave load per 16 words) and turned into the
+// lane = position layout through this wave's LDS stage (N*64 <= 2048 bytes).
+// x0 - 1 + kPad must be 16-byte aligned.
+template <int N, int POOL>
+__device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const UnitDesc &U, int S, int strand,
+                                                  int64_t x0, int lane, int nnc, const int32_t *nc,
+                                                  const double *coef, uint8_t *stage) {
+    constexpr int NV = (N * 64 + 1023) / 1024;  // wave loads per track
+    uint32_t c[N];
+    auto fetch = [&](int k) {
+        gu32x4 *t = (gu32x4 *)(track_u8(U, S, strand, nc[k]) + kPad + x0 - 1);
+        u32x4 v[NV];
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+            if (64 * q + lane < N * 4) v[q] = t[64 * q + lane];
+        __builtin_amdgcn_wave_barrier();  // earlier readers of the stage are done
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+            if (64 * q + lane < N * 4) *(u32x4 *)(stage + 16 * (64 * q + lane)) = v[q];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int w = 0; w < N; ++w) c[w] = stage[64 * w + lane];
+#pragma unroll
+        for (int w = 0; w < N; ++w)
+            if (c[w] == kEsc)
+                c[w] = ovf_lookup(U, (uint32_t)(strand * S + nc[k]), (uint32_t)(x0 + 64 * w + lane));
+    };
+    if constexpr (POOL == 0) {
+        fetch(0);
+#pragma unroll
+        for (int w = 0; w < N; ++w) cs[w] = c[w];
+    } else {
+#pragma unroll
+        for (int w = 0; w < N; ++w) cs[w] = 0.0;
+        for (int k = 0; k < nnc; ++k) {
+            fetch(k);
+            if constexpr (POOL == 1) {
+#pragma unroll
+                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w];
+            } else {
+                const double q = coef[k];
+#pragma unroll
+                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w] * q;
+            }
+        }
+        if constexpr (POOL == 2) {
+            for (int k = 0; k < nnc; ++k) {
+                fetch(k);
+#pragma unroll
+                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w];
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();  // stage free for the next fetch
 }
 
 // KDE value of lane's position in output word K: ascending walk over the
@@ -171,19 +246,11 @@ __device__ __forceinline__ double kde_word(const T (&cs)[NWT], const uint64_t (&
         while (m) {  // batches of kHB hits: weight reads first, adds in order
             int b[kHB];
             double c[kHB], kv[kHB];
-            bool in[kHB];
             next_hits(m, cs[K + d], b, c);
 #pragma unroll
-            for (int h = 0; h < kHB; ++h) {
-                const int idx = lane + (bw - 64 * d - b[h]);
-                in[h] = (unsigned)idx <= (unsigned)(2 * bw);
-                kv[h] = ktab[in[h] ? idx : 0];
-            }
+            for (int h = 0; h < kHB; ++h) kv[h] = ktab[lane + (bw - 64 * d - b[h])];  // 0 outside
 #pragma unroll
-            for (int h = 0; h < kHB; ++h) {
-                const double v = f + kv[h] * c[h];
-                f = in[h] ? v : f;
-            }
+            for (int h = 0; h < kHB; ++h) f = f + kv[h] * c[h];
         }
     }
     return f;
@@ -223,58 +290,62 @@ __device__ __forceinline__ uint32_t find_unit(const UnitDesc *units, uint32_t nu
 
 // run-boundary record list of one strip: kCap inline starts/ends, spilled
 // to an overflow slot (kOvfHalf each) by lane 0 when either list fills
+// run-boundary record list of one strip: kCap inline starts/ends (+ end
+// peaks), spilled to an overflow slot (kOvfHalf each) by lane 0 when either
+// list fills.  Index-based, so the uniform state is three scalars.
+constexpr uint32_t kInline = 0xFFFFFFFFu;
 struct RecList {
-    uint32_t *st, *en;
-    uint32_t *pkp;   // peak position per end (0: the run's start lies outside the strip)
-    double *pkv;     // peak score per end
-    uint32_t ns, ne, cap;
-    bool spilled, lost;
+    uint32_t ns, ne;
+    uint32_t slot;  // kInline, an overflow slot, or >= ovf_cap when lost
 };
 
-__device__ __forceinline__ void rec_spill(RecList &R, const ScanParams &P, uint32_t *inline_base,
-                                          int lane) {
+__device__ __forceinline__ uint32_t *rec_area(const ScanParams &P, const RecList &R, uint32_t strip,
+                                               uint32_t &half) {
+    if (R.slot == kInline) {
+        half = kCap;
+        return P.rec + (uint64_t)strip * kRecStride;
+    }
+    half = kOvfHalf;
+    return P.ovf_rec + (uint64_t)R.slot * kOvfStride;
+}
+
+__device__ __forceinline__ void rec_spill(RecList &R, const ScanParams &P, uint32_t strip, int lane) {
     uint32_t slot = 0;
     if (lane == 0) slot = atomicAdd(P.ovf_count, 1u);
     slot = rl_u(slot, 0);
-    R.spilled = true;
-    if (slot >= P.ovf_cap) {  // host grows the area and reruns
-        R.lost = true;
-        if (lane == 0) inline_base[0] = slot;
-        return;
-    }
-    uint32_t *dst = P.ovf_rec + (uint64_t)slot * kOvfStride;
-    uint32_t *dpp = P.ovf_pkp + (uint64_t)slot * kOvfHalf;
-    double *dpv = P.ovf_pkv + (uint64_t)slot * kOvfHalf;
-    if (lane == 0) {  // same lane wrote the inline records: program order suffices
-        for (uint32_t i = 0; i < R.ns; ++i) dst[i] = R.st[i];
+    uint32_t *inl = P.rec + (uint64_t)strip * kRecStride;
+    if (slot < P.ovf_cap && lane == 0) {  // same lane wrote the inline records: program order suffices
+        uint32_t *dst = P.ovf_rec + (uint64_t)slot * kOvfStride;
+        for (uint32_t i = 0; i < R.ns; ++i) dst[i] = inl[i];
         for (uint32_t i = 0; i < R.ne; ++i) {
-            dst[kOvfHalf + i] = R.en[i];
-            dpp[i] = R.pkp[i];
-            dpv[i] = R.pkv[i];
+            dst[kOvfHalf + i] = inl[kCap + i];
+            dst[2 * kOvfHalf + i] = inl[2 * kCap + i];
+            ((double *)(dst + 4 * kOvfHalf))[i] = ((const double *)(inl + 4 * kCap))[i];
         }
-        inline_base[0] = slot;
     }
-    R.st = dst;
-    R.en = dst + kOvfHalf;
-    R.pkp = dpp;
-    R.pkv = dpv;
-    R.cap = kOvfHalf;
+    if (lane == 0) inl[0] = slot;  // compact reads the slot here (>= ovf_cap: host reruns)
+    R.slot = slot;
 }
 
-__device__ __forceinline__ void rec_start(RecList &R, uint32_t pos, const ScanParams &P,
-                                          uint32_t *inline_base, int lane) {
-    if (R.ns == R.cap && !R.spilled) rec_spill(R, P, inline_base, lane);
-    if (!R.lost && lane == 0) R.st[R.ns] = pos;
+__device__ __forceinline__ void rec_start(RecList &R, uint32_t pos, const ScanParams &P, uint32_t strip,
+                                          int lane) {
+    if (R.slot == kInline && R.ns == kCap) rec_spill(R, P, strip, lane);
+    if (lane == 0 && (R.slot == kInline || R.slot < P.ovf_cap)) {
+        uint32_t half;
+        rec_area(P, R, strip, half)[R.ns] = pos;
+    }
     ++R.ns;
 }
 
 __device__ __forceinline__ void rec_end(RecList &R, uint32_t pos, uint32_t pk_pos, double pk_val,
-                                        const ScanParams &P, uint32_t *inline_base, int lane) {
-    if (R.ne == R.cap && !R.spilled) rec_spill(R, P, inline_base, lane);
-    if (!R.lost && lane == 0) {
-        R.en[R.ne] = pos;
-        R.pkp[R.ne] = pk_pos;
-        R.pkv[R.ne] = pk_val;
+                                        const ScanParams &P, uint32_t strip, int lane) {
+    if (R.slot == kInline && R.ne == kCap) rec_spill(R, P, strip, lane);
+    if (lane == 0 && (R.slot == kInline || R.slot < P.ovf_cap)) {
+        uint32_t half;
+        uint32_t *a = rec_area(P, R, strip, half);
+        a[half + R.ne] = pos;
+        a[2 * half + R.ne] = pk_pos;
+        ((double *)(a + 4 * half))[R.ne] = pk_val;
     }
     ++R.ne;
 }
@@ -295,7 +366,7 @@ __device__ __forceinline__ double wave_max_d(double v) {
 }
 
 // scatter up to kHB hits (window word W, bits b[], pooled counts c[], in
-// ascending order; b = -1024 marks an unused slot) into the register
+// ascending order; c = 0 marks an unused slot) into the register
 // accumulators of the live output words they reach.  The kernel-weight reads
 // of the whole batch are issued before the first add, so the LDS latency is
 // paid once per batch rather than once per hit; the adds stay in hit order
@@ -309,18 +380,10 @@ __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], 
             if (!((live >> (t - NH)) & 1u)) return;  // uniform: word holds no flag
             // output word t-NH, lane position 64(t-NH)+lane; hit at 64(W-NH)+b
             double kv[kHB];
-            bool in[kHB];
 #pragma unroll
-            for (int h = 0; h < kHB; ++h) {
-                const int idx = lane + bw - b[h] + 64 * (t - W);
-                in[h] = (unsigned)idx <= (unsigned)(2 * bw);
-                kv[h] = ktab[in[h] ? idx : 0];
-            }
+            for (int h = 0; h < kHB; ++h) kv[h] = ktab[lane + bw - b[h] + 64 * (t - W)];  // 0 outside
 #pragma unroll
-            for (int h = 0; h < kHB; ++h) {
-                const double v = acc[t - NH] + kv[h] * c[h];
-                acc[t - NH] = in[h] ? v : acc[t - NH];
-            }
+            for (int h = 0; h < kHB; ++h) acc[t - NH] = acc[t - NH] + kv[h] * c[h];
         }
     });
 }
@@ -341,8 +404,9 @@ __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], 
 // keeps the reference's order; flags give run boundaries.
 // ------------------------------------------------------------------------
 constexpr int kScrWords = 8 + kBlocks * kWave + 8;  // chunk sums of one strip + halos
-constexpr size_t kScanLds = (2 * kMaxBw + 2) * sizeof(double) + 4 * kScrWords * sizeof(uint32_t) +
-                            4 * kStepWords * kWave * sizeof(double);
+constexpr size_t kScreenLds = kKTab * sizeof(double) + 4 * kScrWords * sizeof(uint32_t);
+constexpr size_t kScanLds = kScreenLds + 4 * kStepWords * kWave * sizeof(double);
+constexpr size_t kExactLds = kKTab * sizeof(double) + 4 * kStepWords * kWave * sizeof(double);
 
 // chunk i (0..15) of this lane: window a[8+i-R .. 8+i+R] > wskip
 template <int R>
@@ -370,16 +434,22 @@ __device__ __forceinline__ bool has_big(u32x4 v) {
     return ((v.x | v.y | v.z | v.w) & 0x80808080u) != 0u;
 }
 
-template <int NH, int POOL, bool NONDIR, bool PROF>
+// MODE kModeScreen (K1a): stream + screen every strip; strips without exact
+// blocks get their (empty) summary, the others go to the work list.
+// MODE kModeExact (K1b): run the exact blocks of the listed strips, so the
+// latency-bound KDE never stalls the streaming waves.  kModeFused: both in
+// one pass (the PROF profile variant, every block exact).
+template <int NH, int POOL, bool NONDIR, bool PROF, int MODE>
 __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_begin,
                                                    uint32_t strip_end) {
-    extern __shared__ double ktab[];
+    extern __shared__ double lds_[];
     const int bw = P.bw;
-    for (int i = threadIdx.x; i <= 2 * bw; i += blockDim.x) ktab[i] = P.kern[i];
-    __syncthreads();
-    uint32_t *scr = (uint32_t *)(ktab + 2 * kMaxBw + 2) + (threadIdx.x >> 6) * kScrWords;
-    double *scs = (double *)((uint32_t *)(ktab + 2 * kMaxBw + 2) + 4 * kScrWords) +
-                  (threadIdx.x >> 6) * (kStepWords * kWave);  // this wave's block scores
+    double *ktab = lds_ + kKPad;
+    if constexpr (MODE != kModeScreen) ktab = load_ktab(lds_, P.kern, bw);
+    uint32_t *scr = (uint32_t *)(lds_ + kKTab) + (threadIdx.x >> 6) * kScrWords;
+    // this wave's block scores (K1b has no screen area)
+    double *scs = (MODE == kModeExact ? lds_ + kKTab : (double *)((uint32_t *)(lds_ + kKTab) + 4 * kScrWords)) +
+                  (threadIdx.x >> 6) * (kStepWords * kWave);
 
     constexpr int SW = kStepWords;
     constexpr int NWIN = SW + 2 * NH;
@@ -399,19 +469,39 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
 
     uint32_t cur = 0;
     bool have = false;
-    for (uint32_t strip = strip_begin + wave; strip < strip_end; strip += nwaves) {
-        if (!have) { cur = find_unit(P.units, P.nunits, strip); have = true; }
-        while (strip >= P.units[cur].strip0 + P.units[cur].nstrips) ++cur;
+    uint32_t it_end = MODE == kModeExact ? *P.xcount : strip_end;
+    uint32_t it0 = (MODE == kModeExact ? 0u : strip_begin) + wave, istep = nwaves;
+#ifdef UPK_EXP_CONTIG
+    if constexpr (MODE == kModeExact) {  // contiguous item ranges per wave (locality experiment)
+        const uint32_t per = (it_end + nwaves - 1) / nwaves;
+        it0 = wave * per;
+        it_end = it0 + per < it_end ? it0 + per : it_end;
+        istep = 1;
+    }
+#endif
+    for (uint32_t it = it0; it < it_end; it += istep) {
+        uint32_t strip = it;
+        // this lane's failing-chunk bits (chunks 16l..16l+15 = words 4l..4l+3
+        // of the strip); the live words of an exact block are gathered from
+        // them with four ballots when that block runs
+        uint32_t mchunk = 0xFFFFu;
+        uint32_t exact_blocks = 0xFFFFu;
+        if constexpr (MODE == kModeExact) {
+            const uint32_t *e = P.xlist + (uint64_t)it * kXEntry;
+            strip = e[0];
+            exact_blocks = e[1];
+            mchunk = (e[2 + (lane >> 1)] >> (16 * (lane & 1))) & 0xFFFFu;
+            cur = find_unit(P.units, P.nunits, strip);
+        } else {
+            if (!have) { cur = find_unit(P.units, P.nunits, strip); have = true; }
+            while (strip >= P.units[cur].strip0 + P.units[cur].nstrips) ++cur;
+        }
         const UnitDesc U = P.units[cur];
         const uint32_t local = strip - U.strip0;
         const int64_t p0 = 1 + (int64_t)local * kStrip;  // first position of the strip
 
         // ---- screen: which blocks can hold a flagged position ----
-        uint32_t exact_blocks = 0xFFFFu;
-        // live words: word q of lane l's 4 words (chunks 16l+4q..16l+4q+3);
-        // word w of block b is bit (4b + w/4) of live[w % 4]
-        uint64_t live[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-        if constexpr (!PROF) {
+        if constexpr (!PROF && MODE != kModeExact) {
             uint32_t cs[kBlocks];
             uint32_t big = 0, hs = 0;
             bool hbig = false;
@@ -462,8 +552,7 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
             default: m = screen_bits<8>(a, P.wskip); break;
             }
             const uint64_t lanes = __ballot(m != 0u);  // lane l covers chunks 16l..16l+15
-#pragma unroll
-            for (int q = 0; q < 4; ++q) live[q] = __ballot(((m >> (4 * q)) & 0xFu) != 0u);
+            mchunk = m;
             exact_blocks = 0;
 #pragma unroll
             for (int bk = 0; bk < kBlocks; ++bk)
@@ -471,10 +560,23 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
             // the next strip reuses scr only after every lane has read it
             __builtin_amdgcn_wave_barrier();
         }
+        if constexpr (MODE == kModeScreen) {
+            if (exact_blocks == 0) {  // no run can touch this strip
+                const uint64_t info = ((uint64_t)(local == 0) << 34) | ((uint64_t)(local + 1 == U.nstrips) << 35);
+                if (lane == 0) P.strip_info[strip] = info;
+            } else {
+                uint32_t slot = 0;
+                if (lane == 0) slot = atomicAdd(P.xcount, 1u);
+                slot = rl_u(slot, 0);
+                uint32_t *e = P.xlist + (uint64_t)slot * kXEntry;
+                const uint32_t hi = (uint32_t)__shfl_down((int)mchunk, 1);
+                if ((lane & 1) == 0) e[2 + (lane >> 1)] = mchunk | (hi << 16);
+                if (lane == 0) { e[0] = strip; e[1] = exact_blocks; }
+            }
+            continue;
+        }
 
-        uint32_t *inl = P.rec + (uint64_t)strip * (2 * kCap);
-        RecList R_{inl, inl + kCap, P.rec_pkp + (uint64_t)strip * kCap, P.rec_pkv + (uint64_t)strip * kCap,
-                   0, 0, (uint32_t)kCap, false, false};
+        RecList R_{0, 0, kInline};
         uint64_t prevF = 0, F0 = 0;
         double lb = -__builtin_inf();  // open run: this lane's best f+r so far
         uint32_t lp = 0;               // and its (first) position
@@ -487,7 +589,7 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
             const double m = wave_max_d(lb);
             const uint32_t pp = wave_min_u32(lb == m ? lp : 0xFFFFFFFFu);
 #endif
-            rec_end(R_, end_pos, pk_ok ? pp : 0u, m, P, inl, lane);
+            rec_end(R_, end_pos, pk_ok ? pp : 0u, m, P, strip, lane);
             lb = -__builtin_inf();
         };
 
@@ -505,21 +607,40 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
             // and receive no scatter)
             uint32_t lw = 0;
 #pragma unroll
-            for (int w = 0; w < SW; ++w) lw |= (uint32_t)((live[w & 3] >> (4 * j + (w >> 2))) & 1ull) << w;
-            if (P.dbg && lane == 0) {
+            for (int q = 0; q < 4; ++q) {  // word w = 4i + q of the block <- lane 4j + i, nibble q
+                const uint64_t bq = __ballot(((mchunk >> (4 * q)) & 0xFu) != 0u) >> (4 * j);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) lw |= (uint32_t)((bq >> i) & 1ull) << (4 * i + q);
+            }
+#ifdef UPK_DEBUG_COUNTS
+            if (lane == 0) {
                 atomicAdd(&P.dbg[0], 1ull);
                 atomicAdd(&P.dbg[1], (unsigned long long)__builtin_popcount(lw));
             }
+#endif
             const int64_t x0 = p0 + 64 * (j * SW - NH);  // position of window word 0, lane 0
+#ifdef UPK_DEBUG_COUNTS
+            const uint64_t tq0 = __builtin_readcyclecounter();
+#endif
             T wf[NWIN], wr[NONDIR ? NWIN : 1];
             uint64_t hf[NWIN], hr[NONDIR ? NWIN : 1];
-            load_words<NWIN, POOL>(wf, U, S, 0, x0, lane, P.nnc, P.nc, P.coef);
-            if constexpr (NONDIR) load_words<NWIN, POOL>(wr, U, S, 1, x0, lane, P.nnc, P.nc, P.coef);
+            load_words_staged<NWIN, POOL>(wf, U, S, 0, x0, lane, P.nnc, P.nc, P.coef, (uint8_t *)scs);
+            if constexpr (NONDIR)
+                load_words_staged<NWIN, POOL>(wr, U, S, 1, x0, lane, P.nnc, P.nc, P.coef, (uint8_t *)scs + 2048);
 #pragma unroll
             for (int w = 0; w < NWIN; ++w) {
                 hf[w] = __ballot(nz(wf[w]));
                 if constexpr (NONDIR) hr[w] = __ballot(nz(wr[w]));
             }
+#ifdef UPK_DEBUG_COUNTS
+            const uint64_t tq1 = __builtin_readcyclecounter();
+            if (lane == 0) {
+                uint32_t nh = 0;
+                for (int w = 0; w < NWIN; ++w) nh += __builtin_popcountll(hf[w]);
+                atomicAdd(&P.dbg[2], (unsigned long long)nh);
+                atomicAdd(&P.dbg[3], (unsigned long long)(tq1 - tq0));
+            }
+#endif
             // ---- KDE: scatter every hit of the window, ascending ----
             double af[SW], ar[NONDIR ? SW : 1];
 #pragma unroll
@@ -555,6 +676,10 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
                     }
                 }
             });
+#ifdef UPK_DEBUG_COUNTS
+            const uint64_t tq2 = __builtin_readcyclecounter();
+            if (lane == 0) atomicAdd(&P.dbg[4], (unsigned long long)(tq2 - tq1));
+#endif
             double sc[SW];
             double mx = -__builtin_inf();
 #pragma unroll
@@ -586,9 +711,15 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll 1
                     for (int k = 0; k < SW; ++k) {
+                        const int64_t wpos = p0 + 64 * (j * SW + k);
+                        if (!((lw >> k) & 1u)) {  // dead word: no flag; a run open at its left edge ends
+                            if (prevF >> 63) close_run((uint32_t)(wpos - 1));
+                            if (j == 0 && k == 0) F0 = 0;
+                            prevF = 0;
+                            continue;
+                        }
                         const double sck = scs[64 * k + lane];
                         const uint64_t F = __ballot(sck >= P.thr);
-                        const int64_t wpos = p0 + 64 * (j * SW + k);
                         const bool cont = (prevF >> 63) != 0;  // run open at the previous position
                         if (cont && !(F & 1ull)) close_run((uint32_t)(wpos - 1));
                         uint64_t st;
@@ -601,7 +732,7 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
                         while (st) {
                             const int b = __builtin_ctzll(st);
                             st &= st - 1;
-                            rec_start(R_, (uint32_t)(wpos + b), P, inl, lane);
+                            rec_start(R_, (uint32_t)(wpos + b), P, strip, lane);
                         }
                         // per run segment of this word: running first maximum of
                         // f+r per lane (Region::addPos, data.cpp:98-101); one
@@ -614,7 +745,7 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
                             while (en) {
                                 const int b = __builtin_ctzll(en);
                                 en &= en - 1;
-                                rec_end(R_, (uint32_t)(wpos + b), 0u, 0.0, P, inl, lane);
+                                rec_end(R_, (uint32_t)(wpos + b), 0u, 0.0, P, strip, lane);
                             }
                         }
 #endif
@@ -645,7 +776,7 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
         const uint64_t info = (uint64_t)R_.ns | ((uint64_t)R_.ne << 16) | ((F0 & 1ull) << 32) |
                               ((prevF >> 63) << 33) | ((uint64_t)(local == 0) << 34) |
                               ((uint64_t)(local + 1 == U.nstrips) << 35) |
-                              ((uint64_t)R_.spilled << 36);
+                              ((uint64_t)(R_.slot != kInline) << 36);
         if (lane == 0) P.strip_info[strip] = info;
     }
 }
@@ -670,8 +801,6 @@ __global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
                                const uint64_t *__restrict__ info, const uint64_t *__restrict__ cnt,
                                const uint64_t *__restrict__ off, const uint32_t *__restrict__ rec,
                                const uint32_t *__restrict__ ovf_rec, uint32_t ovf_cap,
-                               const uint32_t *__restrict__ rec_pkp, const double *__restrict__ rec_pkv,
-                               const uint32_t *__restrict__ ovf_pkp, const double *__restrict__ ovf_pkv,
                                uint32_t *__restrict__ starts, uint32_t *__restrict__ ends,
                                uint32_t *__restrict__ reg_unit, uint32_t *__restrict__ peak_pos,
                                double *__restrict__ peak_val, uint32_t n, uint64_t cap) {
@@ -686,28 +815,23 @@ __global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
     uint32_t os = (uint32_t)o, oe = (uint32_t)(o >> 32);
     const uint32_t u = find_unit(units, nunits, i);
     const int64_t p0 = 1 + (int64_t)(i - units[u].strip0) * kStrip;
-    const uint32_t *src = rec + (uint64_t)i * (2 * kCap);
-    uint32_t eoff = kCap;
+    const uint32_t *src = rec + (uint64_t)i * kRecStride;
+    uint32_t half = kCap;
     if (si_bit(v, 36)) {
         const uint32_t slot = src[0];
         if (slot >= ovf_cap) return;  // host grows the area and reruns
         src = ovf_rec + (uint64_t)slot * kOvfStride;
-        eoff = kOvfHalf;
+        half = kOvfHalf;
     }
-    const uint32_t *spk = rec_pkp + (uint64_t)i * kCap;
-    const double *spv = rec_pkv + (uint64_t)i * kCap;
-    if (si_bit(v, 36)) {
-        const uint32_t slot = rec[(uint64_t)i * (2 * kCap)];
-        spk = ovf_pkp + (uint64_t)slot * kOvfHalf;
-        spv = ovf_pkv + (uint64_t)slot * kOvfHalf;
-    }
+    const uint32_t *spk = src + 2 * half;
+    const double *spv = (const double *)(src + 4 * half);
     if (os + ns > cap || oe + ne > cap) return;  // host grows the areas and reruns
     if (xs) { starts[os] = (uint32_t)p0; reg_unit[os] = u; ++os; }
     for (uint32_t k = 0; k < si_starts(v); ++k) { starts[os] = src[k]; reg_unit[os] = u; ++os; }
     for (uint32_t k = 0; k < si_ends(v); ++k) {
         peak_pos[oe] = spk[k];
         peak_val[oe] = spv[k];
-        ends[oe++] = src[eoff + k];
+        ends[oe++] = src[half + k];
     }
     if (xe) { peak_pos[oe] = 0; peak_val[oe] = 0.0; ends[oe++] = (uint32_t)(p0 + kStrip - 1); }
 }
@@ -775,10 +899,9 @@ __device__ __forceinline__ void region_words(WinT<POOL> (&cs)[2 * NH + 1], uint6
 
 template <int NH, int POOL, bool NONDIR>
 __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
-    extern __shared__ double ktab[];
+    extern __shared__ double lds_[];
     const int bw = P.bw;
-    for (int i = threadIdx.x; i <= 2 * bw; i += blockDim.x) ktab[i] = P.kern[i];
-    __syncthreads();
+    const double *ktab = load_ktab(lds_, P.kern, bw);
     constexpr int NWT = 2 * NH + 1;
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -790,7 +913,7 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
     const int S = P.S;  // <= 256 (checked by the host)
 
     // per-wave cache of the pass-1 hit totals pc (pass 2 reads them back)
-    uint32_t *pcache = (uint32_t *)(ktab + 2 * kMaxBw + 2) + (threadIdx.x >> 6) * (kStatCache * 64);
+    uint32_t *pcache = (uint32_t *)(lds_ + kKTab) + (threadIdx.x >> 6) * (kStatCache * 64);
 
     for (uint64_t ri = wave; ri < nreg; ri += nwaves) {
         const uint32_t left = P.starts[ri], right = P.ends[ri], u = P.reg_unit[ri];
@@ -1085,10 +1208,9 @@ template <int NH, int POOL>
 __global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t *idx, uint32_t n,
                                                    int max_shift, const uint64_t *slab_off,
                                                    double *slab, double *out) {
-    extern __shared__ double ktab[];
+    extern __shared__ double lds_[];
     const int bw = P.bw;
-    for (int i = threadIdx.x; i <= 2 * bw; i += blockDim.x) ktab[i] = P.kern[i];
-    __syncthreads();
+    const double *ktab = load_ktab(lds_, P.kern, bw);
     constexpr int NWT = 2 * NH + 1;
     const int lane = threadIdx.x & 63;
     uint64_t wm[2 * NH + 1];
