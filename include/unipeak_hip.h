@@ -148,6 +148,20 @@ int up_get_regions(up_ctx *ctx, up_region *out, uint32_t *counts, size_t cap);
 int up_regions_view(up_ctx *ctx, const up_region **regions, const uint32_t **counts,
                     uint64_t *n);
 
+/* Multi-GPU delivery: make up_run write the records into a caller-owned
+ * buffer laid out as
+ *   [uint64 n][cap x up_region][cap x n_samples x uint32 exptSums]
+ * either DEVICE memory of this context's GPU (hand it to RCCL without a host
+ * round trip) or HOST memory, e.g. a node-shared segment rank 0 reads
+ * directly (the library pins it and K3 writes through the mapping).
+ * up_run fails with UP_E_NOMEM if a pass yields more than cap records.
+ * buf = NULL restores host delivery (up_get_regions / up_regions_view). */
+int up_set_record_target(up_ctx *ctx, void *buf, uint64_t cap);
+/* pin + map a host range once (e.g. every record slot of a node-shared
+ * segment), so switching record targets inside it costs nothing; released
+ * by up_close */
+int up_host_register(up_ctx *ctx, void *ptr, uint64_t bytes);
+
 /* strandCorr(shift) for shift = 0..max_shift of the given regions
  * (indices into up_get_regions order); out is [n][max_shift+1]. */
 int up_shift_scan(up_ctx *ctx, const uint64_t *region_idx, size_t n,
@@ -155,6 +169,9 @@ int up_shift_scan(up_ctx *ctx, const uint64_t *region_idx, size_t n,
 
 /* device-side timings of the last up_run in ms: [0]=K1 scan, [1]=K2
  * segment, [2]=K3 stats, [3]=whole up_run wall, [4]=K1 launches */
+/* achievable HBM rate: device-to-device copy of `bytes` (best of reps),
+ * GB/s counting read + write (the bench's copy-rate reference) */
+int up_hbm_copy_gbps(up_ctx *ctx, uint64_t bytes, int reps, double *gbps);
 int up_timings(up_ctx *ctx, double *ms, int n);
 /* dense per-position score f+r of one unit (testing/-w): out[len] */
 int up_unit_profile(up_ctx *ctx, uint32_t unit, double *out_f, double *out_r,

@@ -142,3 +142,128 @@ def _empty_worker(rank, world, port, out_dir):
                 f.write("ok" if ok else "bad")
     finally:
         dist.destroy_process_group()
+
+
+def _cap_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = shard.Comm(dist, rank, world, "cpu")
+        recs = np.zeros(4 + rank, REGION_DTYPE)
+        recs["left"] = np.arange(len(recs)) + 100 * rank
+        g = comm.gather_records(recs, None, cap=10)  # fixed capacity: one collective
+        ok = True
+        if rank == 0:
+            ok = [len(x[0]) for x in g] == [4, 5] and list(g[1][0]["left"]) == [100, 101, 102, 103, 104]
+        over = np.zeros(12 if rank == 1 else 1, REGION_DTYPE)
+        try:
+            comm.gather_records(over, None, cap=10)
+            raised = False
+        except RuntimeError:
+            raised = True
+        if rank == 0:
+            ok = ok and raised
+            with open(os.path.join(out_dir, "result"), "w") as f:
+                f.write("ok" if ok else "bad")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_gather_fixed_capacity(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_cap_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert (tmp_path / "result").read_text() == "ok"
+
+
+def test_parse_target_layout():
+    """the record-target byte layout of include/unipeak_hip.h"""
+    cap, S = 5, 3
+    recs = np.zeros(2, REGION_DTYPE)
+    recs["left"] = [7, 9]
+    recs["peak_score"] = [1.5, 2.5]
+    cnt = np.array([[1, 2, 3], [4, 5, 6]], np.uint32)
+    raw = np.zeros(8 + cap * REGION_DTYPE.itemsize + cap * S * 4, np.uint8)
+    raw[:8] = np.frombuffer(np.uint64(2).tobytes(), np.uint8)
+    raw[8:8 + 2 * REGION_DTYPE.itemsize] = recs.view(np.uint8)
+    c0 = 8 + cap * REGION_DTYPE.itemsize
+    raw[c0:c0 + cnt.nbytes] = cnt.view(np.uint8).ravel()
+    r, c = shard.parse_target(raw, cap, S, REGION_DTYPE)
+    assert list(r["left"]) == [7, 9] and list(r["peak_score"]) == [1.5, 2.5]
+    assert np.array_equal(c, cnt)
+    raw[:8] = np.frombuffer(np.uint64(cap + 1).tobytes(), np.uint8)
+    with pytest.raises(RuntimeError):
+        shard.parse_target(raw, cap, S, REGION_DTYPE)
+
+
+def _target_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = shard.Comm(dist, rank, world, "cpu")
+        cap, S = 8, 2
+        buf = comm.target_buffer(cap, S, REGION_DTYPE.itemsize)
+        raw = buf.numpy()
+        k = 3 + rank
+        raw[:8] = np.frombuffer(np.uint64(k).tobytes(), np.uint8)
+        recs = np.zeros(k, REGION_DTYPE)
+        recs["left"] = np.arange(k) + 10 * rank
+        raw[8:8 + k * REGION_DTYPE.itemsize] = recs.view(np.uint8)
+        got = comm.gather_target(buf)
+        if rank == 0:
+            ok = True
+            for w in range(world):
+                r, _ = shard.parse_target(got[w], cap, S, REGION_DTYPE)
+                ok = ok and list(r["left"]) == list(np.arange(3 + w) + 10 * w)
+            with open(os.path.join(out_dir, "result"), "w") as f:
+                f.write("ok" if ok else "bad")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_gather_target_world2(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_target_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert (tmp_path / "result").read_text() == "ok"
+
+
+def _node_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nr = None
+    try:
+        comm = shard.Comm(dist, rank, world, "cpu")
+        nr = shard.NodeRecords(comm, cap=6, n_samples=2, rec_bytes=REGION_DTYPE.itemsize,
+                               tag=f"test_{port}")
+        mine = nr.mine
+        k = 2 + rank
+        mine[:8] = np.frombuffer(np.uint64(k).tobytes(), np.uint8)
+        recs = np.zeros(k, REGION_DTYPE)
+        recs["left"] = np.arange(k) + 50 * rank
+        mine[8:8 + k * REGION_DTYPE.itemsize] = recs.view(np.uint8)
+        dist.barrier()
+        if rank == 0:
+            got = nr.read(REGION_DTYPE)
+            ok = [list(r["left"]) for r, _ in got] == [[0, 1], [50, 51, 52]]
+            with open(os.path.join(out_dir, "result"), "w") as f:
+                f.write("ok" if ok else "bad")
+            del got
+        del mine
+        dist.barrier()
+    finally:
+        if nr is not None:
+            nr.close()
+        dist.destroy_process_group()
+
+
+def test_node_records_world2(tmp_path):
+    import torch.multiprocessing as mp
+    port = _free_port()
+    mp.spawn(_node_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    assert (tmp_path / "result").read_text() == "ok"
+    assert not os.path.exists(f"/dev/shm/unipeak_test_{port}")

@@ -68,7 +68,8 @@ EXPORTS = [
     "up_close", "up_set_params", "up_add_unit", "up_unit_count", "up_unit_pack",
     "up_unit_scatter", "up_unit_synth", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
     "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan",
-    "up_timings", "up_unit_profile",
+    "up_timings", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
+    "up_host_register",
 ]
 
 
@@ -107,6 +108,9 @@ def load_library(path=LIB_PATH):
         "up_shift_scan": (c.c_int, [vp, vp, c.c_size_t, c.c_uint16, vp]),
         "up_timings": (c.c_int, [vp, vp, c.c_int]),
         "up_unit_profile": (c.c_int, [vp, c.c_uint32, vp, vp, c.c_uint32]),
+        "up_hbm_copy_gbps": (c.c_int, [vp, c.c_uint64, c.c_int, c.POINTER(c.c_double)]),
+        "up_set_record_target": (c.c_int, [vp, vp, c.c_uint64]),
+        "up_host_register": (c.c_int, [vp, vp, c.c_uint64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -249,6 +253,19 @@ class Lib:
         _ck(self.L.up_shift_scan(self.ctx, idx.ctypes.data, idx.size, max_shift,
                                  out.ctypes.data))
         return out
+
+    def set_record_target(self, dev_ptr, cap):
+        """records of the next runs go to a device buffer (see the header);
+        dev_ptr = 0 restores host delivery"""
+        _ck(self.L.up_set_record_target(self.ctx, ctypes.c_void_p(dev_ptr or None), cap))
+
+    def host_register(self, ptr, nbytes):
+        _ck(self.L.up_host_register(self.ctx, ctypes.c_void_p(ptr), nbytes))
+
+    def hbm_copy_gbps(self, nbytes=1 << 30, reps=5):
+        v = ctypes.c_double()
+        _ck(self.L.up_hbm_copy_gbps(self.ctx, nbytes, reps, ctypes.byref(v)))
+        return v.value
 
     def timings(self):
         t = np.zeros(5, np.float64)

@@ -131,11 +131,15 @@ struct up_ctx {
     std::vector<up_region> h_regions;
     std::vector<uint32_t> h_counts;
     std::vector<uint8_t> h_emulated;
-    std::vector<uint32_t> h_head;
+    HostBuf<uint32_t> hp_head;  // head-hit flags, written by head_detect_kernel
     HostBuf<up_region> hp_regions;
     HostBuf<uint32_t> hp_counts;
     HostBuf<unsigned long long> hp_status;
     uint64_t reg_cap = 1u << 16;  // record capacity of one pass (grown on demand)
+    uint8_t *target = nullptr;    // device address of the caller's record buffer
+    uint64_t target_cap = 0;
+    void *target_host = nullptr;  // host buffer we registered for it
+    std::vector<void *> host_regs; // up_host_register ranges (unregistered at close)
     uint64_t last_nreg = 0;
 };
 
@@ -217,11 +221,15 @@ static void free_units(up_ctx *c) {
     c->ran = false;
 }
 
+static void drop_target(up_ctx *c);
+
 void up_close(up_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->stream);
     free_units(c);
+    drop_target(c);
+    for (void *h : c->host_regs) (void)hipHostUnregister(h);
     c->d_kern.release(); c->d_coef.release(); c->d_nc.release(); c->d_ctl.release();
     c->d_units.release(); c->d_info.release(); c->d_rec.release(); c->d_lastnz.release();
     c->d_ovf_count.release(); c->d_ovf_rec.release(); c->d_unit_last.release();
@@ -231,7 +239,7 @@ void up_close(up_ctx *c) {
     c->d_head.release(); c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
-    c->hp_regions.release(); c->hp_counts.release(); c->hp_status.release();
+    c->hp_regions.release(); c->hp_counts.release(); c->hp_status.release(); c->hp_head.release();
     c->d_wscreen.release(); c->d_stage.release(); c->d_dbg.release(); c->d_pack_ovf.release(); c->d_pack_n.release();
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
@@ -726,26 +734,26 @@ static int check_runnable(up_ctx *c) {
 static int launch_head_detect(up_ctx *c) {
     const uint32_t nu = (uint32_t)c->units.size();
     HIPCHK(c->d_head.ensure(nu));
-    HIPCHK(hipMemsetAsync(c->d_head.p, 0, nu * sizeof(uint32_t), c->stream));
+    HIPCHK(c->hp_head.ensure(nu));
     if (pool_mode(c) == 2)
         hipLaunchKernelGGL(head_detect_kernel<2>, dim3(nu), dim3(128), 0, c->stream, c->d_units.p,
-                           (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw, c->d_head.p);
+                           (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw,
+                           c->d_head.p, c->hp_head.dev);
     else
         hipLaunchKernelGGL(head_detect_kernel<1>, dim3(nu), dim3(128), 0, c->stream, c->d_units.p,
-                           (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw, c->d_head.p);
+                           (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw,
+                           c->d_head.p, c->hp_head.dev);
     HIPCHK(hipGetLastError());
-    c->h_head.resize(nu);
-    HIPCHK(hipMemcpyAsync(c->h_head.data(), c->d_head.p, nu * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     return UP_OK;
 }
 
-// after launch_head_detect's copy has landed
+// after the stream sync that follows launch_head_detect
 static int replay_head_hits(up_ctx *c) {
     c->host_regions = false;
     const uint32_t nu = (uint32_t)c->units.size();
-    const std::vector<uint32_t> &head = c->h_head;
+    const uint32_t *head = c->hp_head.p;
     bool any = false;
-    for (uint32_t h : head) any |= h != 0;
+    for (uint32_t i = 0; i < nu; ++i) any |= head[i] != 0;
     if (!any) return UP_OK;
 
     const int S = c->p.n_samples;
@@ -850,6 +858,16 @@ static int replay_head_hits(up_ctx *c) {
     }
     c->host_regions = true;
     c->nreg = c->h_regions.size();
+    if (c->target) {  // keep the caller's device buffer authoritative
+        if (c->nreg > c->target_cap) return UP_E_NOMEM;
+        const uint64_t hdr = c->nreg;
+        HIPCHK(hipMemcpy(c->target, &hdr, 8, hipMemcpyHostToDevice));
+        if (c->nreg) {
+            HIPCHK(hipMemcpy(c->target + 8, c->h_regions.data(), c->nreg * sizeof(up_region), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->target + 8 + c->target_cap * sizeof(up_region), c->h_counts.data(),
+                             c->h_counts.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
+    }
     return UP_OK;
 }
 
@@ -925,7 +943,8 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
         size_t tb = c->d_tmp.n;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->d_tmp.p, tb, c->d_cnt.p, c->d_off.p, (int)ns, c->stream));
         hipLaunchKernelGGL(total_kernel, dim3(1), dim3(1), 0, c->stream, c->d_cnt.p, c->d_off.p, ns,
-                           c->d_ovf_count.p, c->d_nreg.p, c->hp_status.dev);
+                           c->d_ovf_count.p, c->d_nreg.p, c->hp_status.dev,
+                           (unsigned long long *)c->target);
         hipLaunchKernelGGL(compact_kernel, dim3((ns + 255) / 256), dim3(256), 0, c->stream, c->d_units.p,
                            (uint32_t)c->units.size(), c->d_info.p, c->d_cnt.p, c->d_off.p, c->d_rec.p,
                            c->d_ovf_rec.p, c->ovf_cap, c->d_starts.p, c->d_ends.p, c->d_runit.p, c->d_peak_pos.p,
@@ -938,6 +957,11 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
         P.peak_val = c->d_peak_val.p;
         P.out = c->hp_regions.dev;
         P.out_counts = c->hp_counts.dev;
+        if (c->target) {  // records into the caller's device buffer instead
+            P.cap = std::min<uint64_t>(cap, c->target_cap);
+            P.out = c->target + 8;
+            P.out_counts = (uint32_t *)(c->target + 8 + c->target_cap * sizeof(up_region));
+        }
         dispatch_stats(c, P, std::max<uint64_t>(c->last_nreg, 1024));
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->ev[3], c->stream));
@@ -950,6 +974,7 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
         bool again = false;
         if (ovf > c->ovf_cap) { c->ovf_cap = (uint32_t)(ovf + ovf / 2 + 64); again = true; }
         if (nreg > cap) { c->reg_cap = nreg + nreg / 4 + 1024; again = true; }
+        if (c->target && nreg > c->target_cap) return UP_E_NOMEM;  // caller's buffer too small
 #ifdef UPK_DEBUG_COUNTS
         if (dbg) {
             unsigned long long h[8];
@@ -990,9 +1015,52 @@ int up_get_regions(up_ctx *c, up_region *out, uint32_t *counts, size_t cap) {
     return UP_OK;
 }
 
+static void drop_target(up_ctx *c) {
+    if (c->target_host) (void)hipHostUnregister(c->target_host);
+    c->target_host = nullptr;
+    c->target = nullptr;
+    c->target_cap = 0;
+}
+
+int up_set_record_target(up_ctx *c, void *buf, uint64_t cap) {
+    if (!c || (buf && cap == 0)) return UP_E_ARG;
+    HIPCHK(hipSetDevice(c->dev));
+    drop_target(c);
+    c->ran = false;
+    if (!buf) return UP_OK;
+    hipPointerAttribute_t attr{};
+    const bool known = hipPointerGetAttributes(&attr, buf) == hipSuccess;
+    (void)hipGetLastError();  // an unregistered host pointer reports an error here
+    if (known && attr.type == hipMemoryTypeDevice) {
+        c->target = (uint8_t *)buf;
+    } else {
+        // host memory (e.g. a node-shared segment): pin it and let K3 write
+        // through the device mapping
+        const uint64_t bytes = 8 + cap * (sizeof(up_region) + (uint64_t)c->p.n_samples * sizeof(uint32_t));
+        if (!known || attr.type != hipMemoryTypeHost) {
+            HIPCHK(hipHostRegister(buf, bytes, hipHostRegisterMapped));
+            c->target_host = buf;
+        }
+        void *dptr = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dptr, buf, 0));
+        c->target = (uint8_t *)dptr;
+    }
+    c->target_cap = cap;
+    return UP_OK;
+}
+
+int up_host_register(up_ctx *c, void *ptr, uint64_t bytes) {
+    if (!c || !ptr || bytes == 0) return UP_E_ARG;
+    HIPCHK(hipSetDevice(c->dev));
+    HIPCHK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+    c->host_regs.push_back(ptr);
+    return UP_OK;
+}
+
 int up_regions_view(up_ctx *c, const up_region **regions, const uint32_t **counts, uint64_t *n) {
     if (!c || !regions || !n) return UP_E_ARG;
     if (!c->ran) return UP_E_STATE;
+    if (c->target && !c->host_regions) return UP_E_STATE;  // records went to the device buffer
     *n = c->nreg;
     if (c->host_regions) {
         *regions = c->h_regions.data();
@@ -1097,3 +1165,32 @@ int up_unit_profile(up_ctx *c, uint32_t unit, double *out_f, double *out_r, uint
     (void)hipFree(d);
     return UP_OK;
 }
+
+// Achievable HBM rate on this device: device-to-device copy of `bytes`
+// (read + write), best of `reps`, reported as (2 * bytes) / time.
+int up_hbm_copy_gbps(up_ctx *c, uint64_t bytes, int reps, double *gbps) {
+    if (!c || !gbps || bytes == 0 || reps < 1) return UP_E_ARG;
+    HIPCHK(hipSetDevice(c->dev));
+    void *a = nullptr, *b = nullptr;
+    HIPCHK(hipMalloc(&a, bytes));
+    if (hipMalloc(&b, bytes) != hipSuccess) {
+        (void)hipFree(a);
+        return UP_E_NOMEM;
+    }
+    HIPCHK(hipMemsetAsync(a, 1, bytes, c->stream));
+    float best = 0;
+    for (int i = 0; i <= reps; ++i) {
+        HIPCHK(hipEventRecord(c->ev[5], c->stream));
+        HIPCHK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipEventRecord(c->ev[6], c->stream));
+        HIPCHK(hipEventSynchronize(c->ev[6]));
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, c->ev[5], c->ev[6]);
+        if (i > 0 && (best == 0 || ms < best)) best = ms;  // first copy is a warm-up
+    }
+    (void)hipFree(a);
+    (void)hipFree(b);
+    *gbps = 2.0 * (double)bytes / (best * 1e-3) / 1e9;
+    return UP_OK;
+}
+

@@ -355,7 +355,7 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
 // head-hit detection: any pooled countSum != 0 at positions 1..bw
 template <int POOL>
 __global__ void head_detect_kernel(const UnitDesc *units, int S, int nnc, const int32_t *nc,
-                                   const double *coef, int bw, uint32_t *head) {
+                                   const double *coef, int bw, uint32_t *head, uint32_t *mirror) {
     const UnitDesc U = units[blockIdx.x];
     const int p = 1 + (int)threadIdx.x;
     uint32_t hit = 0;
@@ -371,7 +371,11 @@ __global__ void head_detect_kernel(const UnitDesc *units, int S, int nnc, const 
             if (cs != 0.0) hit = 1;
         }
     }
-    if (__syncthreads_or(hit) && threadIdx.x == 0) head[blockIdx.x] = 1;
+    const uint32_t v = __syncthreads_or(hit) ? 1u : 0u;
+    if (threadIdx.x == 0) {
+        head[blockIdx.x] = v;
+        if (mirror) mirror[blockIdx.x] = v;  // mapped host copy: no read-back copy
+    }
 }
 
 }  // namespace upk

@@ -1189,13 +1189,15 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
 // K2b': region count from the scan, on the device (no host round trip):
 // status[0] = regions, status[1] = spilled strips, status[2] = start/end mismatch
 __global__ void total_kernel(const uint64_t *cnt, const uint64_t *off, uint32_t ns,
-                             const uint32_t *ovf_count, uint64_t *nreg, unsigned long long *status) {
+                             const uint32_t *ovf_count, uint64_t *nreg, unsigned long long *status,
+                             unsigned long long *target_hdr) {
     const uint64_t t = cnt[ns - 1] + off[ns - 1];
     const uint64_t nst = t & 0xFFFFFFFFull, nen = t >> 32;
     *nreg = nst;
     status[0] = nst;
     status[1] = *ovf_count;
     status[2] = nst != nen;
+    if (target_hdr) *target_hdr = nst;  // caller's device record buffer (up_set_record_target)
 }
 
 // ------------------------------------------------------------------------

@@ -58,6 +58,24 @@ def plan(contig_lens, nondir, world, n_samples=1):
     return units, owner, mine
 
 
+def order_blocks(parts):
+    """Zero-copy form of merge(): [(global unit, records view, counts view)]
+    in global unit order, one block per (rank, unit) with records."""
+    blocks = []
+    for recs, gids, cnt in parts:
+        if len(recs) == 0:
+            continue
+        gids = np.asarray(gids, np.int64)
+        loc = recs["unit"].astype(np.int64)
+        bounds = np.searchsorted(loc, np.arange(len(gids) + 1), side="left")
+        for li, g in enumerate(gids):
+            a, b = int(bounds[li]), int(bounds[li + 1])
+            if b > a:
+                blocks.append((int(g), recs[a:b], None if cnt is None else cnt[a:b]))
+    blocks.sort(key=lambda t: t[0])
+    return blocks
+
+
 def merge(parts, n_units, dtype):
     """parts: [(records, local->global unit ids, counts or None)] from every
     rank, each unit-major.  Returns (records, global unit id per record,
@@ -104,9 +122,11 @@ class Comm:
 
     def global_tags(self, local_tags: int) -> int:
         """The single data-path collective of the scan (regions.cpp:205-213)."""
-        t = self.torch.tensor([int(local_tags)], dtype=self.torch.int64, device=self.device)
-        self.dist.all_reduce(t)
-        return int(t.item())
+        if getattr(self, "_tags", None) is None:
+            self._tags = self.torch.zeros(1, dtype=self.torch.int64, device=self.device)
+        self._tags.fill_(int(local_tags))
+        self.dist.all_reduce(self._tags)
+        return int(self._tags.item())
 
     def max_over_ranks(self, x: float) -> float:
         t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=self.device)
@@ -118,31 +138,171 @@ class Comm:
         self.dist.all_reduce(t)
         return float(t.item())
 
-    def gather_records(self, recs: np.ndarray, extra: np.ndarray | None = None):
+    def gather_records(self, recs: np.ndarray, extra: np.ndarray | None = None,
+                       cap: int | None = None):
         """Fixed-size records (+ an optional fixed-width uint32 row per record)
         to rank 0.  Returns a list of (records, extra) per rank on rank 0,
-        None elsewhere."""
+        None elsewhere.  With `cap` (agreed by every rank, e.g. from a
+        warm-up) the gather is the only collective; a rank holding more than
+        `cap` records makes rank 0 raise.  Rows travel as one byte matrix per
+        rank: host (pinned) -> device -> one gather into a contiguous
+        [world, rows, row] device buffer on rank 0 -> one copy back."""
         torch = self.torch
         n = len(recs)
-        nmax = int(self.max_over_ranks(n))
+        nmax = int(self.max_over_ranks(n)) if cap is None else int(cap)
+        nmax = max(nmax, 1)
+        sent = min(n, nmax)
         rb = recs.dtype.itemsize
         eb = 0 if extra is None else extra.shape[1] * 4
-        row = rb + eb
-        buf = np.zeros((max(nmax, 1), row + 8), np.uint8)
-        buf[:n, :rb] = recs.view(np.uint8).reshape(n, rb)
-        if eb:
-            buf[:n, rb:rb + eb] = np.ascontiguousarray(extra, np.uint32).view(np.uint8).reshape(n, eb)
-        buf[0, row:row + 8] = np.frombuffer(np.int64(n).tobytes(), np.uint8)
-        t = torch.from_numpy(buf).to(self.device)
-        glist = [torch.empty_like(t) for _ in range(self.world)] if self.rank == 0 else None
-        self.dist.gather(t, glist, dst=0)
+        row = rb + eb + 8  # record, extra row, and (row 0 only) the rank's count
+        key = (nmax, row)
+        if getattr(self, "_gkey", None) != key:  # buffers reused across steps
+            self._gkey = key
+            on_gpu = self.device != "cpu"
+            self._hsend = torch.zeros((nmax, row), dtype=torch.uint8, pin_memory=on_gpu)
+            self._dsend = self._hsend.to(self.device) if on_gpu else self._hsend
+            if self.rank == 0:
+                self._dall = torch.zeros((self.world, nmax, row), dtype=torch.uint8, device=self.device)
+                self._hall = (torch.zeros((self.world, nmax, row), dtype=torch.uint8, pin_memory=True)
+                              if on_gpu else self._dall)
+        h = self._hsend.numpy()
+        if sent:
+            h[:sent, :rb] = recs[:sent].view(np.uint8).reshape(sent, rb)
+            if eb:
+                h[:sent, rb:rb + eb] = np.ascontiguousarray(extra[:sent], np.uint32).view(np.uint8).reshape(sent, eb)
+        h[0, row - 8:row] = np.frombuffer(np.int64(n).tobytes(), np.uint8)
+        if self._dsend is not self._hsend:
+            self._dsend.copy_(self._hsend, non_blocking=True)
+        glist = list(self._dall.unbind(0)) if self.rank == 0 else None
+        self.dist.gather(self._dsend, glist, dst=0)
         if self.rank != 0:
             return None
+        if self._hall is not self._dall:
+            self._hall.copy_(self._dall)
+        a = self._hall.numpy()
         out = []
-        for g in glist:
-            a = g.cpu().numpy()
-            k = int(np.frombuffer(a[0, row:row + 8].tobytes(), np.int64)[0])
-            r = np.ascontiguousarray(a[:k, :rb]).view(recs.dtype).reshape(k)
-            e = None if not eb else np.ascontiguousarray(a[:k, rb:rb + eb]).view(np.uint32).reshape(k, -1)
+        for w in range(self.world):
+            k = int(np.frombuffer(a[w, 0, row - 8:row].tobytes(), np.int64)[0])
+            if k > nmax:
+                raise RuntimeError(f"a rank holds {k} records, the gather capacity is {nmax}")
+            r = np.ascontiguousarray(a[w, :k, :rb]).view(recs.dtype).reshape(k)
+            e = None if not eb else np.ascontiguousarray(a[w, :k, rb:rb + eb]).view(np.uint32).reshape(k, -1)
             out.append((r, e))
         return out
+
+    # ---- device-resident records (up_set_record_target layout) ----
+    def target_buffer(self, cap: int, n_samples: int, rec_bytes: int):
+        """A device byte buffer in the library's record-target layout:
+        [uint64 n][cap records][cap x S uint32 exptSums]."""
+        nbytes = 8 + cap * rec_bytes + cap * n_samples * 4
+        nbytes = (nbytes + 255) // 256 * 256
+        return self.torch.zeros(nbytes, dtype=self.torch.uint8, device=self.device)
+
+    def gather_target(self, buf):
+        """One RCCL gather of every rank's target buffer to rank 0 and one
+        copy back; returns the host bytes [world, nbytes] on rank 0."""
+        torch = self.torch
+        if self.rank == 0:
+            if getattr(self, "_tall", None) is None or self._tall.shape[1] != buf.numel():
+                self._tall = torch.empty((self.world, buf.numel()), dtype=torch.uint8, device=self.device)
+                self._thost = (torch.empty((self.world, buf.numel()), dtype=torch.uint8, pin_memory=True)
+                               if self.device != "cpu" else self._tall)
+            self.dist.gather(buf, list(self._tall.unbind(0)), dst=0)
+            if self._thost is not self._tall:
+                self._thost.copy_(self._tall)
+            return self._thost.numpy()
+        self.dist.gather(buf, None, dst=0)
+        return None
+
+
+def parse_target(raw, cap, n_samples, dtype):
+    """(records, exptSums) from one rank's target bytes."""
+    n = int(np.frombuffer(raw[:8].tobytes(), np.uint64)[0])
+    if n > cap:
+        raise RuntimeError(f"a rank produced {n} records, the gather capacity is {cap}")
+    rb = dtype.itemsize
+    recs = np.frombuffer(raw[8:8 + n * rb].tobytes(), dtype)
+    c0 = 8 + cap * rb
+    cnt = np.frombuffer(raw[c0:c0 + n * n_samples * 4].tobytes(), np.uint32).reshape(n, n_samples)
+    return recs, cnt
+
+
+class NodeRecords:
+    """Node-shared pinned host segment that every rank's K3 writes its
+    records into (up_set_record_target with a host pointer): on one node the
+    records reach rank 0 without a gather collective or a device-to-host copy
+    on rank 0 -- each GPU writes its own slot over its own PCIe link.  Two
+    slots per rank (step parity) let rank 0 read step i-1 while step i runs;
+    the collective at the start of each step orders the writes.  Slot layout
+    = the record target layout of include/unipeak_hip.h."""
+
+    def __init__(self, comm, cap, n_samples, rec_bytes, tag):
+        from multiprocessing import resource_tracker, shared_memory
+        self.comm, self.cap, self.S, self.rb = comm, cap, n_samples, rec_bytes
+        slot = 8 + cap * (rec_bytes + 4 * n_samples)
+        self.slot = (slot + 4095) // 4096 * 4096
+        self.world = comm.world if comm is not None else 1
+        if comm is None:  # one process: plain page-aligned host memory, no segment
+            self.shm = None
+            self.owner = True
+            self._mem = np.zeros(2 * self.slot + 4096, np.uint8)
+            off = (-self._mem.ctypes.data) % 4096
+            self.raw = self._mem[off:off + 2 * self.slot]
+            self.mine = self.raw
+            return
+        name = f"unipeak_{tag}"
+        self.owner = comm.rank == 0
+        if self.owner:
+            try:  # a stale segment of an earlier crashed run
+                old = shared_memory.SharedMemory(name=name)
+                old.close()
+                old.unlink()
+            except FileNotFoundError:
+                pass
+            self.shm = shared_memory.SharedMemory(name=name, create=True, size=2 * self.slot * comm.world)
+        comm.dist.barrier()
+        if not self.owner:
+            self.shm = shared_memory.SharedMemory(name=name)
+            # attachers must not unlink it at exit (Python's resource tracker would)
+            resource_tracker.unregister(self.shm._name, "shared_memory")
+        self.raw = np.frombuffer(self.shm.buf, np.uint8)
+        self.mine = self.raw[2 * comm.rank * self.slot:2 * (comm.rank + 1) * self.slot]
+
+    def my_range(self):
+        """(address, bytes) of this rank's two slots (register them once)"""
+        return self.mine.ctypes.data, 2 * self.slot
+
+    def my_slot_address(self, parity=0):
+        return self.mine.ctypes.data + (parity & 1) * self.slot
+
+    def read(self, dtype, parity=0):
+        """rank 0, once every rank's step of this parity is done:
+        [(records view, counts view)] per rank"""
+        out = []
+        for w in range(self.world):
+            base = (2 * w + (parity & 1)) * self.slot
+            n = int(self.raw[base:base + 8].view(np.uint64)[0])
+            if n > self.cap:
+                raise RuntimeError(f"rank {w} produced {n} records, the slot holds {self.cap}")
+            recs = self.raw[base + 8:base + 8 + n * self.rb].view(dtype)
+            c0 = base + 8 + self.cap * self.rb
+            cnt = self.raw[c0:c0 + n * self.S * 4].view(np.uint32).reshape(n, self.S)
+            out.append((recs, cnt))
+        return out
+
+    def close(self):
+        self.raw = self.mine = None
+        if self.shm is None:
+            self._mem = None
+            return
+        try:
+            self.shm.close()
+        except BufferError:  # a caller still holds a view; the mapping dies with the process
+            import gc
+            gc.collect()
+            try:
+                self.shm.close()
+            except BufferError:
+                pass
+        if self.owner:
+            self.shm.unlink()
