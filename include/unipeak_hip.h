@@ -176,6 +176,11 @@ int up_timings(up_ctx *ctx, double *ms, int n);
 /* dense per-position score f+r of one unit (testing/-w): out[len] */
 int up_unit_profile(up_ctx *ctx, uint32_t unit, double *out_f, double *out_r,
                     uint32_t len);
+/* the same for positions [first, first + count) (first >= 1; the range may
+ * run past the contig end into the scan domain, quirk Q16); out_r may be
+ * NULL for directional units */
+int up_unit_profile_range(up_ctx *ctx, uint32_t unit, uint64_t first, uint32_t count,
+                          double *out_f, double *out_r);
 
 #ifdef __cplusplus
 }

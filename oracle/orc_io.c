@@ -740,6 +740,55 @@ static FILE *open_out(const char *fname) {
     return fp;
 }
 
+/* density profile writer: FormatOutStream::write(const PosScore&) and
+ * trackHeader(), misc/format.cpp:1091-1132, 1164-1219; constants
+ * misc/defaults.hpp:38-42 (colours, PROFILE_PRIORITY = 2) */
+typedef struct {
+    FILE *fp;
+    const ctab *ct;
+    int directional;
+    const char *name, *assembly;
+    int have_contig, forward;
+    uint32_t contig;
+} prof_writer;
+
+static void prof_track_header(prof_writer *w) {
+    fprintf(w->fp, "track name=\"%s", w->name);
+    if (w->directional) fputs(w->forward ? " +" : " -", w->fp);
+    fputc('"', w->fp);
+    if (w->directional) fprintf(w->fp, " description=\"%s\"", w->forward ? w->name : " ");
+    fputs(" priority=2 visibility=", w->fp);
+    if (w->directional)
+        fputs(w->forward ? "full type=wiggle_0 alwaysZero=on color=0,0,255"
+                         : "full type=wiggle_0 alwaysZero=on color=255,0,0 altColor=255,0,0", w->fp);
+    else
+        fputs("full type=wiggle_0 alwaysZero=on color=191,0,191", w->fp);
+    if (*w->assembly) fprintf(w->fp, " db=%s", w->assembly);
+    fputc('\n', w->fp);
+}
+
+static void prof_write(void *user, int forward, uint32_t contig, uint32_t pos, double score) {
+    prof_writer *w = (prof_writer *)user;
+    if (score == 0) return;
+    if (w->directional) {
+        if (!w->have_contig || w->forward != forward) {
+            w->forward = forward;
+            w->have_contig = 0;
+            prof_track_header(w);
+        }
+    } else if (!w->have_contig) {
+        prof_track_header(w);
+    }
+    if (!w->have_contig || w->contig != contig) {  /* names are unique in the table */
+        w->contig = contig;
+        w->have_contig = 1;
+        fprintf(w->fp, "variableStep chrom=%s\n", w->ct->names[contig]);
+    }
+    fprintf(w->fp, "%u ", pos);
+    if (w->directional && !forward) fputc('-', w->fp);
+    fprintf(w->fp, "%g\n", score);
+}
+
 int orc_regions_main(int argc, char **argv) {
     argspec sp[] = {
         {"q", "quiet", 1, 0, 0, 0},          {"D", "non-directional", 1, 0, 0, 0},
@@ -761,7 +810,8 @@ int orc_regions_main(int argc, char **argv) {
     if (nfiles == 0) fail("error: Required argument missing for arg alignment filenames\n\n");
     const int quiet = sp[0].seen, directional = !sp[1].seen;
     const char *profile = sp[4].seen ? sp[4].value : "";
-    if (*profile) fail("oracle: -w profile output is not restated\n");
+    const char *assembly = sp[2].seen ? sp[2].value : "";
+    const char *track_nm = sp[3].seen ? sp[3].value : "";
     uint32_t mappable = (uint32_t)arg_uint(&sp[5], 0, 0xFFFFFFFFull);
     double hit_thr = arg_double(&sp[6], 10);
     int out_corrs = sp[7].seen;
@@ -899,6 +949,16 @@ int orc_regions_main(int argc, char **argv) {
     sb_os(&hdr, background);
     sb_puts(&hdr, "\n");
 
+    /* regions.cpp:103, 276-284: the profile stream gets the common header */
+    prof_writer pw = {0};
+    if (*profile) {
+        pw.fp = open_out(profile);
+        pw.ct = ct;
+        pw.directional = directional;
+        pw.name = *track_nm ? track_nm : fname_prefix(profile);
+        pw.assembly = assembly;
+        fwrite(hdr.p, 1, hdr.n, pw.fp);
+    }
     FILE *out = open_out(out_name);
     region_writer wr = {out, ct, out_peaks, out_corrs};
     fwrite(hdr.p, 1, hdr.n, out);
@@ -918,10 +978,10 @@ int orc_regions_main(int argc, char **argv) {
     regvec pending = {0};
     orc_buf *fb = orc_buf_new(kern, W, region_thr, kurt_thr, corr_thr, hit_thr, 1,
                               (uint16_t)nfiles, control, coeffs, (uint32_t)ncoeffs,
-                              regvec_push, &pending, NULL, NULL);
+                              regvec_push, &pending, *profile ? prof_write : NULL, &pw);
     orc_buf *rb = orc_buf_new(kern, W, region_thr, kurt_thr, corr_thr, hit_thr, 0,
                               (uint16_t)nfiles, control, coeffs, (uint32_t)ncoeffs,
-                              regvec_push, &pending, NULL, NULL);
+                              regvec_push, &pending, *profile ? prof_write : NULL, &pw);
     uint32_t *fh = (uint32_t *)xcalloc((size_t)nfiles, sizeof(uint32_t));
     uint32_t *rh = (uint32_t *)xcalloc((size_t)nfiles, sizeof(uint32_t));
     uint32_t contig = 0;
@@ -975,6 +1035,7 @@ int orc_regions_main(int argc, char **argv) {
         }
     }
     if (out != stdout) fclose(out); else fflush(out);
+    if (pw.fp) { if (pw.fp != stdout) fclose(pw.fp); else fflush(pw.fp); }
     /* Q3: regions closed by the final flush are never written */
     for (size_t k = 0; k < pending.n; ++k) orc_region_free(pending.v[k]);
 

@@ -96,6 +96,77 @@ def test_regions_cli_matches_oracle(orc_bin, gpu_lib, tmp_path, case):
     assert out.count("\n") > 10
 
 
+PROFILE_CASES = [
+    ("directional", HG_LIKE, 1, ["-f"], {}),
+    ("directional_named_db", HG_LIKE, 2, ["-f", "-n", "trk", "-a", "hg19", "-b", "20"], {}),
+    ("one_contig_interleave", [("chrX", 80_000)], 1, ["-f", "-b", "100"], {}),
+    ("nondir", HG_LIKE, 2, ["-D", "-y"], {"shift_rev": 100}),
+]
+
+
+def test_oracle_profile_writer_matches_kde(orc_bin, oracle, tmp_path):
+    """the oracle's -w writer (FormatOutStream::write(PosScore), format.cpp:
+    1091-1132) emits exactly the nonzero KDE scores of each strand buffer,
+    as %g, reverse negated, one track per strand, one variableStep per contig"""
+    contigs = [("chrA", 30_000), ("chrB", 20_000)]
+    rng = np.random.default_rng(5)
+    ct = tmp_path / "contigs.txt"
+    write_contigs(ct, contigs)
+    fwd, rev = gen_sample(rng, contigs)
+    write_wig(tmp_path / "s0.wig", "s0", fwd, rev)
+    run([orc_bin, "regions", "-q", "-f", "-c", str(ct), "-n", "trk", "-a", "hg19", "-w", "p.wig",
+         "-o", "r.txt", "s0.wig"], tmp_path)
+    lines = (tmp_path / "p.wig").read_text().split("\n")
+    tracks = [l for l in lines if l.startswith("track")]
+    assert tracks == [
+        'track name="trk +" description="trk" priority=2 visibility=full type=wiggle_0 '
+        'alwaysZero=on color=0,0,255 db=hg19',
+        'track name="trk -" description=" " priority=2 visibility=full type=wiggle_0 '
+        'alwaysZero=on color=255,0,0 altColor=255,0,0 db=hg19']
+    bg = float(next(l for l in lines if l.startswith("# background=")).split("=")[1])
+    got, key = {}, None
+    strand = -1
+    for l in lines:
+        if l.startswith("track"):
+            strand += 1
+        elif l.startswith("variableStep"):
+            key = (strand, l.split("chrom=")[1])
+            assert key not in got
+            got[key] = []
+        elif l and not l.startswith("#"):
+            got[key].append(l)
+    for st, d in enumerate((fwd, rev)):
+        for name, L in contigs:
+            pos = np.array([p for p, _ in d[name]], np.uint32)
+            cnt = np.array([[c] for _, c in d[name]], np.uint32)
+            f = (oracle.profile(50, bg, L, pos, cnt) if st == 0 else
+                 oracle.profile(50, bg, L, pos, None, cnt, buffer_forward=False))
+            nz = np.flatnonzero(f)
+            want = ["%d %s%s" % (i + 1, "-" if st else "", "%g" % f[i]) for i in nz]
+            assert got[(st, name)] == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PROFILE_CASES, ids=lambda c: c[0])
+def test_regions_cli_profile_matches_oracle(orc_bin, gpu_lib, tmp_path, case):
+    """-w: the density profile, written in the order the reference retires
+    positions (both buffers interleaved), byte-identical to the oracle's"""
+    name, contigs, ns, args, kw = case
+    ct, files = make_inputs(tmp_path, zlib.crc32(name.encode()) % 10_000 + 7, contigs, ns, **kw)
+    common = ["-q", "-c", ct] + args
+    # same file name in two directories: the default track name is its prefix
+    (tmp_path / "ref").mkdir()
+    (tmp_path / "got").mkdir()
+    run([orc_bin, "regions"] + common + ["-w", "ref/p.wig", "-o", "ref/r.txt"] + files, tmp_path)
+    run([os.path.join(BIN, "regions")] + common + ["-w", "got/p.wig", "-o", "got/r.txt"] + files,
+        tmp_path)
+    assert (tmp_path / "ref/r.txt").read_bytes() == (tmp_path / "got/r.txt").read_bytes()
+    a, b = (tmp_path / "ref/p.wig").read_bytes(), (tmp_path / "got/p.wig").read_bytes()
+    assert a.count(b"\n") > 1000
+    assert a == b, "profile differs at byte %d" % next(
+        (i for i, (x, y) in enumerate(zip(a, b)) if x != y), min(len(a), len(b)))
+
+
 @pytest.mark.gpu
 def test_regions_cli_survey_kat(orc_bin, gpu_lib, tmp_path):
     """Q7 known answer (reference run recorded in SURVEY.md) through bin/regions."""

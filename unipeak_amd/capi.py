@@ -69,7 +69,7 @@ EXPORTS = [
     "up_unit_scatter", "up_unit_synth", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
     "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan",
     "up_timings", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
-    "up_host_register",
+    "up_host_register", "up_unit_profile_range",
 ]
 
 
@@ -111,6 +111,7 @@ def load_library(path=LIB_PATH):
         "up_hbm_copy_gbps": (c.c_int, [vp, c.c_uint64, c.c_int, c.POINTER(c.c_double)]),
         "up_set_record_target": (c.c_int, [vp, vp, c.c_uint64]),
         "up_host_register": (c.c_int, [vp, vp, c.c_uint64]),
+        "up_unit_profile_range": (c.c_int, [vp, c.c_uint32, c.c_uint64, c.c_uint32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -1142,28 +1142,39 @@ int up_timings(up_ctx *c, double *ms, int n) {
     return UP_OK;
 }
 
-int up_unit_profile(up_ctx *c, uint32_t unit, double *out_f, double *out_r, uint32_t len) {
+int up_unit_profile_range(up_ctx *c, uint32_t unit, uint64_t first, uint32_t count, double *out_f,
+                          double *out_r) {
     int r = check_runnable(c);
     if (r) return r;
-    if (unit >= c->units.size() || !out_f || !out_r) return UP_E_ARG;
+    if (unit >= c->units.size() || !out_f || first < 1 || count == 0) return UP_E_ARG;
     HIPCHK(hipSetDevice(c->dev));
     if ((r = sync_units(c))) return r;
+    const Unit &u = c->units[unit];
+    const uint64_t dom = (uint64_t)u.nstrips * kStrip;  // scan domain incl. Q16 tail
+    if (first + count - 1 > dom) return UP_E_ARG;
     double *d = nullptr;
-    HIPCHK(hipMalloc(&d, 2 * (size_t)len * sizeof(double) + 16));
-    HIPCHK(hipMemsetAsync(d, 0, 2 * (size_t)len * sizeof(double), c->stream));
+    HIPCHK(hipMalloc(&d, 2 * (size_t)count * sizeof(double) + 16));
+    HIPCHK(hipMemsetAsync(d, 0, 2 * (size_t)count * sizeof(double), c->stream));
     ScanParams P = scan_params(c);
     P.prof_f = d;
-    P.prof_r = d + len;
-    P.prof_len = len;
+    P.prof_r = d + count;
+    P.prof_first = (int64_t)first;
+    P.prof_len = count;
     P.prof_unit = unit;
-    const Unit &u = c->units[unit];
-    dispatch_scan<true, kModeFused>(c, P, u.strip0, u.strip0 + u.nstrips);
+    const uint32_t s0 = u.strip0 + (uint32_t)((first - 1) / kStrip);
+    const uint32_t s1 = u.strip0 + (uint32_t)((first + count - 2) / kStrip) + 1;
+    dispatch_scan<true, kModeFused>(c, P, s0, s1);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipMemcpy(out_f, d, (size_t)len * sizeof(double), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(out_r, d + len, (size_t)len * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out_f, d, (size_t)count * sizeof(double), hipMemcpyDeviceToHost));
+    if (out_r) HIPCHK(hipMemcpy(out_r, d + count, (size_t)count * sizeof(double), hipMemcpyDeviceToHost));
     (void)hipFree(d);
     return UP_OK;
+}
+
+int up_unit_profile(up_ctx *c, uint32_t unit, double *out_f, double *out_r, uint32_t len) {
+    if (!out_r) return UP_E_ARG;
+    return up_unit_profile_range(c, unit, 1, len, out_f, out_r);
 }
 
 // Achievable HBM rate on this device: device-to-device copy of `bytes`

@@ -77,8 +77,9 @@ struct ScanParams {
 #ifdef UPK_DEBUG_COUNTS
     unsigned long long *dbg;  // counters: exact blocks, live words
 #endif
-    double *prof_f, *prof_r;  // optional dense profile of one unit
-    uint32_t prof_unit, prof_len;
+    double *prof_f, *prof_r;  // optional dense profile of one unit's positions
+    uint32_t prof_unit, prof_len;  // [prof_first, prof_first + prof_len)
+    int64_t prof_first;
 };
 
 struct StatParams {

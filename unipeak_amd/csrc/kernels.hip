@@ -692,10 +692,10 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
             if constexpr (PROF) {
 #pragma unroll
                 for (int k = 0; k < SW; ++k) {
-                    const int64_t p = p0 + 64 * (j * SW + k) + lane;
-                    if (p <= P.prof_len) {
-                        P.prof_f[p - 1] = af[k];
-                        if constexpr (NONDIR) P.prof_r[p - 1] = ar[k];
+                    const int64_t q = p0 + 64 * (j * SW + k) + lane - P.prof_first;
+                    if (q >= 0 && q < (int64_t)P.prof_len) {
+                        P.prof_f[q] = af[k];
+                        if constexpr (NONDIR) P.prof_r[q] = ar[k];
                     }
                 }
             } else {

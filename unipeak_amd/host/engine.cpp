@@ -281,6 +281,94 @@ void shift_scan(const EngineParams &ep, PassResult &out, const std::vector<const
     }
 }
 
+void ProfileSink::header() {  // FormatOutStream::trackHeader, format.cpp:1164-1219
+    std::fprintf(fp, "track name=\"%s", name.c_str());
+    if (directional) std::fputs(forward ? " +" : " -", fp);
+    std::fputc('"', fp);
+    if (directional) std::fprintf(fp, " description=\"%s\"", forward ? name.c_str() : " ");
+    std::fputs(" priority=2 visibility=", fp);  // PROFILE_PRIORITY, defaults.hpp:42
+    if (directional)
+        std::fputs(forward ? "full type=wiggle_0 alwaysZero=on color=0,0,255"
+                           : "full type=wiggle_0 alwaysZero=on color=255,0,0 altColor=255,0,0", fp);
+    else
+        std::fputs("full type=wiggle_0 alwaysZero=on color=191,0,191", fp);
+    if (!assembly.empty()) std::fprintf(fp, " db=%s", assembly.c_str());
+    std::fputc('\n', fp);
+}
+
+void ProfileSink::write(bool fwd, uint32_t c, uint64_t pos, double score) {
+    if (score == 0) return;  // format.cpp:1092
+    if (directional) {
+        if (!have_contig || forward != fwd) {
+            forward = fwd;
+            have_contig = false;
+            header();
+        }
+    } else if (!have_contig) {
+        header();
+    }
+    if (!have_contig || contig != c) {
+        contig = c;
+        have_contig = true;
+        std::fprintf(fp, "variableStep chrom=%s\n", ct->name(c).c_str());
+    }
+    // ostream << double: 6 significant digits (%g); reverse strand negated
+    std::fprintf(fp, (directional && !fwd) ? "%llu -%g\n" : "%llu %g\n", (unsigned long long)pos, score);
+}
+
+void write_profile(const PassResult &pr, uint16_t bw, ProfileSink &sink) {
+    // device context and unit id of every global unit
+    std::vector<std::pair<up_ctx *, uint32_t>> where(pr.units.size(), {nullptr, 0});
+    for (const DeviceJob &j : g_jobs)
+        for (size_t k = 0; k < j.dev_unit.size(); ++k) where[j.dev_unit[k]] = {j.ctx, (uint32_t)k};
+    for (const UnitBuild &u : pr.units)
+        if (u.head_hit)
+            fatal("-w with tags within the first bandwidth positions of a contig (quirk Q1) is not "
+                  "supported on the GPU path yet");
+    // retirement events: add() at p after q retires q-bw .. q-bw+min(W,p-q)-1
+    // (peakcall.cpp:171-184); flushContig() retires q-bw .. q+bw
+    struct Ev { uint64_t t; uint32_t unit; int64_t lo, hi; };
+    std::vector<Ev> ev;
+    const int64_t W = 2 * (int64_t)bw + 1;
+    for (uint32_t k = 0; k < pr.units.size(); ++k) {
+        const UnitBuild &u = pr.units[k];
+        int64_t q = 0;
+        for (size_t i = 0; i < u.add_pos.size(); ++i) {
+            const int64_t p = u.add_pos[i];
+            if (q != 0 && p > q) {
+                const int64_t n = std::min<int64_t>(W, p - q);
+                ev.push_back({u.add_time[i], k, std::max<int64_t>(1, q - bw), q - bw + n - 1});
+            }
+            q = p;
+        }
+        if (q != 0) ev.push_back({u.flush_time, k, std::max<int64_t>(1, q - bw), q + bw});
+    }
+    std::sort(ev.begin(), ev.end(), [](const Ev &a, const Ev &b) { return a.t < b.t; });
+    // per-unit cache of one chunk of the device profile
+    constexpr uint32_t kChunkPos = 1u << 22;
+    struct Cache { int64_t first = -1; std::vector<double> f, r; };
+    std::vector<Cache> cache(pr.units.size());
+    for (const Ev &e : ev) {
+        const UnitBuild &u = pr.units[e.unit];
+        Cache &c = cache[e.unit];
+        for (int64_t x = e.lo; x <= e.hi; ++x) {
+            if (c.first < 0 || x < c.first || x >= c.first + (int64_t)kChunkPos) {
+                c.first = ((x - 1) / kChunkPos) * kChunkPos + 1;
+                const uint64_t dom_end = (uint64_t)u.len + bw;  // highest position a flush retires
+                const uint32_t n = (uint32_t)std::min<uint64_t>(kChunkPos, dom_end - (uint64_t)c.first + 1);
+                c.f.assign(n, 0.0);
+                c.r.assign(n, 0.0);
+                const int rc = up_unit_profile_range(where[e.unit].first, where[e.unit].second,
+                                                     (uint64_t)c.first, n, c.f.data(), c.r.data());
+                if (rc != UP_OK) fatal(std::string("up_unit_profile_range: ") + up_strerror(rc));
+            }
+            const size_t i = (size_t)(x - c.first);
+            if (i >= c.f.size()) continue;  // beyond the scan domain: never scored
+            sink.write(u.buffer == 0, u.contig, (uint64_t)x, c.f[i] + c.r[i]);
+        }
+    }
+}
+
 void release_devices() {
     for (DeviceJob &j : g_jobs)
         if (j.ctx) up_close(j.ctx);

@@ -11,6 +11,7 @@
 #pragma once
 
 #include <cstdint>
+#include <cstdio>
 #include <string>
 #include <vector>
 
@@ -75,6 +76,22 @@ std::vector<Emitted> order_candidates(const PassResult &out, uint16_t bw, bool a
 // strandCorr(shift) table for accepted candidates (strand_shift), on GPU
 void shift_scan(const EngineParams &ep, PassResult &out, const std::vector<const Candidate *> &regs,
                 uint16_t max_shift, std::vector<double> &table);
+
+// -w density profile (regions.cpp:276-284): every processed position with a
+// nonzero score, written when the reference's processPosition writes it --
+// at the add() (or flush) that retires it, interleaved across the two
+// buffers by the replayed event clock (misc/format.cpp:1091-1132)
+struct ProfileSink {
+    std::FILE *fp = nullptr;
+    const ContigTable *ct = nullptr;
+    bool directional = true;
+    std::string name, assembly;
+    bool have_contig = false, forward = true;
+    uint32_t contig = 0;
+    void header();
+    void write(bool fwd, uint32_t contig, uint64_t pos, double score);
+};
+void write_profile(const PassResult &pr, uint16_t bw, ProfileSink &sink);
 
 void release_devices();
 

@@ -49,7 +49,9 @@ int main(int argc, char **argv) {
     const std::string control_str = ap.str("e");
     const bool out_peaks = ap.on("f");
     const std::string out_name = ap.str("o"), ct_name = ap.str("c");
-    if (!profile.empty()) fatal("-w density profile output is not implemented on the GPU path yet");
+    const std::string assembly = ap.str("a");
+    std::string track_name = ap.str("n");
+    if (!profile.empty() && track_name.empty()) track_name = fname_prefix(profile);  // regions.cpp:103
 
     if (directional) {  // regions.cpp:104-109
         if (corr_thr != 0.3) std::cerr << "warning: correlation threshold is not used on strand-specific analysis" << std::endl;
@@ -174,6 +176,18 @@ int main(int argc, char **argv) {
     }
     h << "# total_tags=" << nc_tags << "\n";
     h << "# background=" << background << "\n";
+    ProfileSink prof;
+    if (!profile.empty()) {  // regions.cpp:276-284: header first, profile as positions retire
+        prof.fp = profile == "stdout" ? stdout : std::fopen(profile.c_str(), "wb");
+        if (!prof.fp) { std::cerr << "error: could not write " << profile << std::endl << std::endl; return 1; }
+        std::setvbuf(prof.fp, nullptr, _IOFBF, 1 << 22);
+        prof.ct = &ct;
+        prof.directional = directional;
+        prof.name = track_name;
+        prof.assembly = assembly;
+        const std::string hs = h.str();
+        std::fwrite(hs.data(), 1, hs.size(), prof.fp);
+    }
     std::string table = h.str();
     table += "# region_threshold=" + fmt_lexical(region_thr) + "\n";
     table += "# kurtosis_threshold=" + fmt_lexical(kurt_thr) + "\n";
@@ -202,6 +216,10 @@ int main(int argc, char **argv) {
     ep.coeffs = coeffs;
     ep.ngpus = env_gpus();
     run_units(ep, pr);
+    if (prof.fp) {
+        write_profile(pr, bw, prof);
+        if (prof.fp != stdout) std::fclose(prof.fp); else std::fflush(stdout);
+    }
 
     // emission in the reference's order (Q2-Q4); Q3 drops final-flush regions
     const std::vector<Emitted> em = order_candidates(pr, bw, false);
