@@ -1,6 +1,10 @@
 // unipeak_amd/host/cli.cpp -- see cli.hpp.
 #include "cli.hpp"
 
+#include <cstdio>
+#include <ctime>
+#include <sys/resource.h>
+
 #include <cstdlib>
 #include <iostream>
 
@@ -88,6 +92,38 @@ uint64_t ArgParser::uint(const std::string &s, uint64_t dflt, uint64_t maxv) con
     if (!lex_uint(f.value, maxv, &v))
         fail("Couldn't read argument value from string '" + f.value + "'", "-" + f.s + " (--" + f.l + ")");
     return v;
+}
+
+static double now_s() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void cpu_s(double *user, double *sys);
+
+PhaseTimer::PhaseTimer() : on_(false), t_(now_s()) {
+    cpu_s(&u_, &s_);
+    const char *e = std::getenv("UNIPEAK_TIMING");
+    on_ = e && *e && *e != '0';
+}
+
+static void cpu_s(double *user, double *sys) {
+    rusage ru;
+    getrusage(RUSAGE_SELF, &ru);
+    *user = (double)ru.ru_utime.tv_sec + 1e-6 * (double)ru.ru_utime.tv_usec;
+    *sys = (double)ru.ru_stime.tv_sec + 1e-6 * (double)ru.ru_stime.tv_usec;
+}
+
+void PhaseTimer::mark(const char *phase) {
+    const double t = now_s();
+    double u, s;
+    cpu_s(&u, &s);
+    if (on_)
+        std::fprintf(stderr, "[timing] %s %.3f s (cpu user %.3f sys %.3f)\n", phase, t - t_, u - u_, s - s_);
+    t_ = t;
+    u_ = u;
+    s_ = s;
 }
 
 int env_gpus() {

@@ -41,4 +41,15 @@ class ArgParser {
 // GPU count for the engine: UNIPEAK_GPUS (0 or unset = every visible device)
 int env_gpus();
 
+// UNIPEAK_TIMING=1: phase wall times on stderr ("[timing] <phase> <s>"),
+// so ingest and the GPU phase can be reported apart
+class PhaseTimer {
+  public:
+    PhaseTimer();
+    void mark(const char *phase);  // time since the previous mark
+  private:
+    bool on_;
+    double t_, u_ = 0, s_ = 0;
+};
+
 }  // namespace unipeak

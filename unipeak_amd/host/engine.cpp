@@ -2,6 +2,8 @@
 #include "engine.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <mutex>
@@ -27,72 +29,263 @@ static double count_sum(const uint32_t *c, size_t S, const std::vector<uint8_t> 
     return s;
 }
 
-void build_units(std::vector<SampleStream *> &streams, const ContigTable &ct, bool directional,
-                 uint16_t bw, const std::vector<uint8_t> &control, const std::vector<double> &coeffs,
-                 bool quiet, PassResult &out) {
-    (void)quiet;
-    const size_t S = streams.size();
-    std::vector<uint32_t> fh(S), rh(S);
-    uint64_t clock = 0;
-    int cur[2] = {-1, -1};  // unit index per buffer for the current iteration
-    uint32_t contig = 0, iteration = 0;
-    bool forward = true;
+namespace {
 
+// one driver-loop iteration (a contig pass): the units it creates and the
+// number of add() calls, with add times on a clock local to the iteration
+struct IterOut {
+    std::vector<UnitBuild> units;
+    uint64_t adds = 0;
+    bool stepped = false;  // the position loop ran at least once
+};
+
+struct MergeSpec {
+    size_t S;
+    bool directional;
+    uint16_t bw;
+    const std::vector<uint8_t> *control;
+    const std::vector<double> *coeffs;
+};
+
+// the position loop of one iteration, src/regions.cpp:311-371 (and
+// src/strand_shift.cpp:144-186): every stream whose head lies on this contig
+// is consumed position by position; head(i) is stream i's current record,
+// advance(i) reads its next one
+template <class Head, class Advance>
+void merge_iteration(const MergeSpec &m, uint32_t contig, uint32_t lim, uint32_t iteration,
+                     uint32_t len, Head head, Advance advance, IterOut &o, uint64_t reserve = 0) {
+    const size_t S = m.S;
+    std::vector<uint32_t> fh(S), rh(S);
+    int cur[2] = {-1, -1};
     auto add = [&](int buffer, int strand, const std::vector<uint32_t> &counts, uint32_t pos) {
         if (cur[buffer] < 0) {
             UnitBuild u;
             u.buffer = buffer;
             u.contig = contig;
-            u.len = ct.length(contig);
+            u.len = len;
             u.iteration = iteration;
-            out.units.push_back(std::move(u));
-            cur[buffer] = (int)out.units.size() - 1;
-        }
-        UnitBuild &u = out.units[cur[buffer]];
-        const int track = directional ? 0 : strand;
-        u.pos[track].push_back(pos);
-        u.cnt[track].insert(u.cnt[track].end(), counts.begin(), counts.end());
-        u.add_pos.push_back(pos);
-        u.add_time.push_back(++clock);
-        if (pos <= bw && count_sum(counts.data(), S, control, coeffs) != 0) u.head_hit = true;
-    };
-
-    // src/regions.cpp:311-391 (and src/strand_shift.cpp:144-190)
-    while (contig < ct.size()) {
-        const uint32_t lim = ct.length(contig);
-        uint32_t pos = 1;
-        while (pos <= lim) {
-            bool ff = false, fr = false;
-            uint32_t next = lim + 1;
-            for (size_t i = 0; i < S; ++i) {
-                fh[i] = 0;
-                rh[i] = 0;
-                const Align *a = &streams[i]->last();
-                while (a->count != 0 && a->first == pos && a->contig == contig) {
-                    if (a->forward) { fh[i] += a->count; ff = true; }
-                    else { rh[i] += a->count; fr = true; }
-                    a = &streams[i]->read_align();
-                }
-                if (a->count != 0 && a->contig == contig && a->first < next) next = a->first;
+            if (reserve) {
+                const int tr = m.directional ? 0 : strand;
+                u.pos[tr].reserve(reserve);
+                u.cnt[tr].reserve(reserve * S);
+                u.add_pos.reserve(reserve);
+                u.add_time.reserve(reserve);
             }
-            if (ff) add(0, 0, fh, pos);
-            if (fr) add(directional ? 1 : 0, 1, rh, pos);
-            out.write_times.push_back(clock);  // pending regions are written here
-            pos = next;
+            o.units.push_back(std::move(u));
+            cur[buffer] = (int)o.units.size() - 1;
         }
-        // flushContig(): forward buffer, then reverse buffer
-        for (int b = 0; b < 2; ++b) {
-            ++clock;
-            if (cur[b] >= 0) out.units[cur[b]].flush_time = clock;
-            cur[b] = -1;
+        UnitBuild &u = o.units[cur[buffer]];
+        const int track = m.directional ? 0 : strand;
+        u.pos[track].push_back(pos);
+        for (size_t i = 0; i < S; ++i) u.cnt[track].push_back(counts[i]);
+        u.add_pos.push_back(pos);
+        u.add_time.push_back(++o.adds);
+        if (pos <= m.bw && count_sum(counts.data(), S, *m.control, *m.coeffs) != 0) u.head_hit = true;
+    };
+    uint32_t pos = 1;
+    while (pos <= lim) {
+        o.stepped = true;
+        bool ff = false, fr = false;
+        uint32_t next = lim + 1;
+        for (size_t i = 0; i < S; ++i) {
+            fh[i] = 0;
+            rh[i] = 0;
+            const auto *a = &head(i);
+            while (a->count != 0 && a->first == pos && a->contig == contig) {
+                if (a->forward) { fh[i] += a->count; ff = true; }
+                else { rh[i] += a->count; fr = true; }
+                a = &advance(i);
+            }
+            if (a->count != 0 && a->contig == contig && a->first < next) next = a->first;
         }
-        ++contig;
-        ++iteration;
-        if (directional && contig == ct.size() && forward) {
-            contig = 0;
-            forward = false;
+        if (ff) add(0, 0, fh, pos);
+        if (fr) add(m.directional ? 1 : 0, 1, rh, pos);
+        pos = next;
+    }
+    // flushContig(): forward buffer (local time adds+1), then reverse (adds+2)
+    for (int b = 0; b < 2; ++b)
+        if (cur[b] >= 0) o.units[cur[b]].flush_time = o.adds + 1 + b;
+}
+
+// the driver's iteration sequence: contig of iteration i
+struct Iterations {
+    uint32_t nc;
+    bool directional;
+    uint32_t count() const { return directional ? 2 * nc : nc; }
+    uint32_t contig(uint32_t i) const { return i % nc; }
+};
+
+// concatenate iterations on the global event clock: each add ticks once,
+// each iteration ends with two flush ticks
+void stitch(std::vector<IterOut> &its, PassResult &out) {
+    uint64_t base = 0;
+    for (IterOut &o : its) {
+        for (UnitBuild &u : o.units) {
+            for (uint64_t &t : u.add_time) t += base;
+            if (u.flush_time) u.flush_time += base;
+            out.units.push_back(std::move(u));
+        }
+        if (o.stepped) out.last_write = base + o.adds;
+        base += o.adds + 2;
+    }
+}
+
+// a stream decoded ahead of the merge: every record read_align() returns
+// (the record already read by the caller first), then the count-0 end
+struct Rec {
+    uint32_t contig, first, count;
+    bool forward;
+};
+
+struct Decoded {
+    std::unique_ptr<SampleStream> stream;
+    std::vector<Rec> recs;
+    bool ok = false;
+};
+
+void decode_stream(const SampleStream &orig, Decoded &d) {
+    t_defer_errors = true;
+    try {
+        d.stream = orig.reopen();
+        d.stream->expected_tags();
+        d.recs.reserve(d.stream->size_hint() + 1);
+        const Align *a = &d.stream->read_align();
+        for (;;) {
+            d.recs.push_back(Rec{a->contig, a->first, a->count, a->forward});
+            if (a->count == 0) break;
+            a = &d.stream->read_align();
+        }
+        d.ok = true;
+    } catch (const DeferredError &) {
+        d.ok = false;
+    }
+    t_defer_errors = false;
+}
+
+}  // namespace
+
+void build_units(std::vector<SampleStream *> &streams, const ContigTable &ct, bool directional,
+                 uint16_t bw, const std::vector<uint8_t> &control, const std::vector<double> &coeffs,
+                 bool quiet, PassResult &out) {
+    (void)quiet;
+    const size_t S = streams.size();
+    const MergeSpec m{S, directional, bw, &control, &coeffs};
+    const Iterations itn{ct.size(), directional};
+    const unsigned T = ingest_threads();
+
+    // (1) decode every stream ahead, one thread per stream
+    std::vector<Decoded> dec(S);
+    const char *ser = std::getenv("UNIPEAK_SERIAL_INGEST");
+    bool parallel = !(ser && *ser && *ser != '0');
+    if (parallel) {
+        std::vector<std::thread> pool;
+        std::atomic<size_t> next{0};
+        for (unsigned t = 0; t < std::min<size_t>(T, S); ++t)
+            pool.emplace_back([&] {
+                for (size_t i; (i = next.fetch_add(1)) < S;) decode_stream(*streams[i], dec[i]);
+            });
+        for (auto &th : pool) th.join();
+    }
+    // (2) which iteration consumes each run of same-contig records: the
+    // first one after the previous run's whose contig matches.  A run no
+    // iteration reaches leaves its stream stuck there; that case, and any
+    // input error, goes to the serial replay below.
+    std::vector<std::vector<std::pair<size_t, size_t>>> slice(
+        itn.count(), std::vector<std::pair<size_t, size_t>>(S, {0, 0}));
+    for (size_t i = 0; i < S && parallel; ++i) {
+        const Decoded &d = dec[i];
+        if (!d.ok) { parallel = false; break; }
+        const size_t n = d.recs.size() - 1;
+        int64_t prev = -1;
+        for (size_t b = 0; b < n;) {
+            const uint32_t c = d.recs[b].contig;
+            size_t e = b + 1;
+            while (e < n && d.recs[e].contig == c) ++e;
+            int64_t it = -1;
+            for (uint32_t k = (uint32_t)(prev + 1); k < itn.count(); ++k)
+                if (itn.contig(k) == c) { it = k; break; }
+            if (it < 0) { parallel = false; break; }
+            slice[it][i] = {b, e};
+            prev = it;
+            b = e;
         }
     }
+    std::vector<IterOut> its(itn.count());
+    if (parallel) {
+        // (3) iterations in parallel, each over its slices of the records
+        std::vector<uint32_t> order(itn.count());
+        for (uint32_t k = 0; k < itn.count(); ++k) order[k] = k;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+            return ct.length(itn.contig(a)) > ct.length(itn.contig(b));
+        });
+        std::vector<std::thread> pool;
+        std::atomic<size_t> next{0};
+        for (unsigned t = 0; t < std::min<size_t>(T, order.size()); ++t)
+            pool.emplace_back([&] {
+                std::vector<size_t> at(S);
+                for (size_t j; (j = next.fetch_add(1)) < order.size();) {
+                    const uint32_t k = order[j];
+                    for (size_t i = 0; i < S; ++i) at[i] = slice[k][i].first;
+                    auto head = [&](size_t i) -> const Rec & {
+                        const Decoded &d = dec[i];
+                        return at[i] < slice[k][i].second ? d.recs[at[i]] : d.recs.back();
+                    };
+                    auto advance = [&](size_t i) -> const Rec & {
+                        ++at[i];
+                        return head(i);
+                    };
+                    const uint32_t c = itn.contig(k);
+                    uint64_t bound = 0;  // adds per buffer are at most the records consumed
+                    for (size_t i = 0; i < S; ++i) bound += slice[k][i].second - slice[k][i].first;
+                    merge_iteration(m, c, ct.length(c), k, ct.length(c), head, advance, its[k], bound);
+                }
+            });
+        for (auto &th : pool) th.join();
+        // the callers' streams continue from where the decode left them (EOF)
+        for (size_t i = 0; i < S; ++i) *streams[i] = std::move(*dec[i].stream);
+    } else {
+        // serial replay on the callers' streams, exactly as the reference reads
+        for (uint32_t k = 0; k < itn.count(); ++k) {
+            const uint32_t c = itn.contig(k);
+            merge_iteration(
+                m, c, ct.length(c), k, ct.length(c),
+                [&](size_t i) -> const Align & { return streams[i]->last(); },
+                [&](size_t i) -> const Align & { return streams[i]->read_align(); }, its[k]);
+        }
+    }
+    dec.clear();
+    stitch(its, out);
+    out.parallel_ingest = parallel;
+}
+
+template <class V>
+static uint64_t fnv(const V &v) {
+    uint64_t h = 1469598103934665603ull;
+    const unsigned char *p = (const unsigned char *)v.data();
+    for (size_t i = 0; i < v.size() * sizeof(v[0]); ++i) h = (h ^ p[i]) * 1099511628211ull;
+    return h;
+}
+
+void maybe_dump_units(const PassResult &pr, const std::vector<SampleStream *> &streams) {
+    const char *path = std::getenv("UNIPEAK_DUMP_UNITS");
+    if (!path || !*path) return;
+    FILE *f = std::fopen(path, "w");
+    if (!f) fatal(std::string("could not write ") + path);
+    std::fprintf(f, "ingest %s\n", pr.parallel_ingest ? "parallel" : "serial");
+    std::fprintf(f, "last_write %llu\n", (unsigned long long)pr.last_write);
+    for (const UnitBuild &u : pr.units)
+        std::fprintf(f, "unit b%d c%u it%u len%u flush%llu head%d n%zu/%zu %016llx %016llx %016llx %016llx %016llx %016llx\n",
+                     u.buffer, u.contig, u.iteration, u.len, (unsigned long long)u.flush_time,
+                     (int)u.head_hit, u.pos[0].size(), u.pos[1].size(),
+                     (unsigned long long)fnv(u.pos[0]), (unsigned long long)fnv(u.pos[1]),
+                     (unsigned long long)fnv(u.cnt[0]), (unsigned long long)fnv(u.cnt[1]),
+                     (unsigned long long)fnv(u.add_pos), (unsigned long long)fnv(u.add_time));
+    for (SampleStream *s : streams)
+        std::fprintf(f, "stream %s expected %llu confident %llu oob %llu\n", s->expt_name().c_str(),
+                     (unsigned long long)s->expected_tags(), (unsigned long long)s->confident(),
+                     (unsigned long long)s->out_of_bounds());
+    std::fclose(f);
+    std::exit(0);
 }
 
 namespace {
@@ -183,6 +376,11 @@ void run_units(const EngineParams &ep, PassResult &out) {
             job.dev_unit.push_back(gi);
             for (int st = 0; st < nstr; ++st) {
                 const size_t n = u.pos[st].size();
+                if (S == 1) {  // every add of a single sample carries a nonzero count
+                    if (n && (rc = up_unit_scatter(job.ctx, id, st, 0, n, u.pos[st].data(), u.cnt[st].data())))
+                        return fail(rc, "up_unit_scatter");
+                    continue;
+                }
                 for (size_t s = 0; s < S; ++s) {
                     tp.clear();
                     tc.clear();
@@ -225,7 +423,7 @@ void run_units(const EngineParams &ep, PassResult &out) {
 std::vector<Emitted> order_candidates(const PassResult &out, uint16_t bw, bool accepted_only) {
     std::vector<Emitted> v;
     v.reserve(out.cands.size());
-    const uint64_t last_write = out.write_times.empty() ? 0 : out.write_times.back();
+    const uint64_t last_write = out.last_write;
     for (const Candidate &c : out.cands) {
         const UnitBuild &u = out.units[c.unit_index];
         // closed by the first add at pos >= right + bw + 2, else by the flush;

@@ -43,7 +43,8 @@ struct Candidate {
 
 struct PassResult {
     std::vector<UnitBuild> units;
-    std::vector<uint64_t> write_times;  // event clock after each loop step
+    uint64_t last_write = 0;            // event clock after the last loop step (Q3)
+    bool parallel_ingest = false;       // built by the per-iteration parallel merge
     std::vector<Candidate> cands;       // all candidates, any order
 };
 
@@ -59,6 +60,11 @@ struct EngineParams {
 void build_units(std::vector<SampleStream *> &streams, const ContigTable &ct,
                  bool directional, uint16_t bw, const std::vector<uint8_t> &control,
                  const std::vector<double> &coeffs, bool quiet, PassResult &out);
+
+// UNIPEAK_DUMP_UNITS=<file>: write a digest of the merge result (units, add
+// clocks, stream counters) and exit before the GPU phase -- lets CPU tests
+// check the parallel ingest against the serial replay (UNIPEAK_SERIAL_INGEST=1)
+void maybe_dump_units(const PassResult &pr, const std::vector<SampleStream *> &streams);
 
 // run every unit on the GPU(s); fills out.cands
 void run_units(const EngineParams &ep, PassResult &out);

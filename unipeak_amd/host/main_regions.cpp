@@ -28,6 +28,7 @@ int main(int argc, char **argv) {
                   {"f", "peaks", true, false},          {"o", "out", false, true},
                   {"c", "contig", false, true}});
     ap.parse(argc, argv);
+    PhaseTimer timer;
     const std::vector<std::string> files = ap.files();
     if (files.empty()) {
         std::cerr << "error: Required argument missing for arg alignment filenames" << std::endl << std::endl;
@@ -201,7 +202,10 @@ int main(int argc, char **argv) {
 
     std::cerr << "calling enriched regions..." << std::endl;
     PassResult pr;
+    timer.mark("open");
     build_units(sp, ct, directional, bw, control, coeffs, quiet, pr);
+    maybe_dump_units(pr, sp);
+    timer.mark("ingest");
     EngineParams ep;
     ep.p.bw = bw;
     ep.p.n_samples = (uint16_t)files.size();
@@ -216,9 +220,11 @@ int main(int argc, char **argv) {
     ep.coeffs = coeffs;
     ep.ngpus = env_gpus();
     run_units(ep, pr);
+    timer.mark("gpu");
     if (prof.fp) {
         write_profile(pr, bw, prof);
         if (prof.fp != stdout) std::fclose(prof.fp); else std::fflush(stdout);
+        timer.mark("profile");
     }
 
     // emission in the reference's order (Q2-Q4); Q3 drops final-flush regions
@@ -253,6 +259,7 @@ int main(int argc, char **argv) {
     if (!out) { std::cerr << "error: could not write " << out_name << std::endl << std::endl; return 1; }
     std::fwrite(table.data(), 1, table.size(), out);
     if (out != stdout) std::fclose(out); else std::fflush(stdout);
+    timer.mark("table");
 
     if (!quiet) {  // per-pass progress lines, regions.cpp:312-384, printed after the run
         std::vector<uint64_t> per(pr.units.size(), 0);

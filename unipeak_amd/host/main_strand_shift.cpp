@@ -79,6 +79,7 @@ int main(int argc, char **argv) {
     std::vector<uint8_t> control(S, 0);
     PassResult pr;
     build_units(sp, ct, false, bw, control, {}, true, pr);
+    maybe_dump_units(pr, sp);
     EngineParams ep;
     ep.p.bw = bw;
     ep.p.n_samples = (uint16_t)S;

@@ -1,6 +1,16 @@
 // unipeak_amd/host/wigio.cpp -- see wigio.hpp.
 #include "wigio.hpp"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <thread>
+
 #include <cctype>
 #include <cerrno>
 #include <cmath>
@@ -10,7 +20,10 @@
 
 namespace unipeak {
 
+thread_local bool t_defer_errors = false;
+
 void fatal(const std::string &msg) {
+    if (t_defer_errors) throw DeferredError();
     std::cerr << "error: " << msg << "\n" << std::endl;
     std::exit(1);
 }
@@ -95,19 +108,149 @@ std::string fname_prefix(const std::string &path) {
 }
 
 // ---------------------------------------------------------------------------
+// LexedFile
+// ---------------------------------------------------------------------------
+unsigned ingest_threads() {
+    if (const char *e = std::getenv("UNIPEAK_THREADS")) {
+        const int v = std::atoi(e);
+        if (v > 0) return (unsigned)v;
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return std::max(1u, std::min(16u, hw));
+}
+
+// canonical data line [p, e): digits, one ' ' or '\t', optional '-', digits
+static bool lex_data(const char *p, const char *e, uint32_t *pos, uint32_t *cnt) {
+    uint64_t v = 0;
+    const char *q = p;
+    while (q < e && (unsigned)(*q - '0') < 10u && q - p < 10) v = v * 10 + (uint64_t)(*q++ - '0');
+    if (q == p || q == e || (*q != ' ' && *q != '\t') || v > 0xFFFFFFFFull) return false;
+    *pos = (uint32_t)v;
+    ++q;
+    if (q < e && *q == '-') ++q;
+    const char *d = q;
+    v = 0;
+    while (q < e && (unsigned)(*q - '0') < 10u && q - d < 10) v = v * 10 + (uint64_t)(*q++ - '0');
+    if (q == d || q != e || v > 0xFFFFFFFFull) return false;
+    *cnt = (uint32_t)v;
+    return true;
+}
+
+LexedFile::~LexedFile() {
+    if (base_ && size_) munmap((void *)base_, size_);
+}
+
+void LexedFile::lex(const std::string &fname, int fd, uint64_t size) {
+    (void)fname;
+    size_ = size;
+    if (size_) {
+        void *m = mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) fatal("could not map " + fname);
+        madvise(m, size_, MADV_SEQUENTIAL);
+        base_ = (const char *)m;
+    }
+    // newline-aligned chunk boundaries
+    const unsigned T = ingest_threads();
+    const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(4ull * T, size_ / (1u << 20) + 1));
+    std::vector<uint64_t> cut{0};
+    for (uint64_t k = 1; k < want; ++k) {
+        uint64_t c = size_ * k / want;
+        if (c <= cut.back()) continue;
+        const void *nl = std::memchr(base_ + c, '\n', size_ - c);
+        if (!nl) break;
+        c = (uint64_t)((const char *)nl - base_) + 1;
+        if (c > cut.back() && c < size_) cut.push_back(c);
+    }
+    cut.push_back(size_);
+    const size_t nchunk = cut.size() - 1;
+    chunks_.assign(nchunk, Chunk());
+    auto lex_chunk = [&](size_t k) {
+        Chunk &ch = chunks_[k];
+        const char *p = base_ + cut[k], *end = base_ + cut[k + 1];
+        const bool last = k + 1 == nchunk;
+        const size_t guess = (size_t)(end - p) / 10 + 2;
+        ch.kind.reserve(guess);
+        ch.a.reserve(guess);
+        ch.b.reserve(guess);
+        for (;;) {
+            const char *nl = (const char *)std::memchr(p, '\n', (size_t)(end - p));
+            const char *e = nl ? nl : end;
+            if (!nl && !last) break;  // a non-final chunk ends with its '\n'
+            uint32_t x = 0, y = 0;
+            uint8_t kind;
+            if (e == p) {
+                kind = kEmpty;
+            } else if (lex_data(p, e, &x, &y)) {
+                kind = kData;
+            } else {
+                kind = kText;
+                x = (uint32_t)ch.toff.size();
+                y = (uint32_t)(e - p);
+                ch.toff.push_back((uint64_t)(p - base_));
+            }
+            ch.kind.push_back(kind);
+            ch.a.push_back(x);
+            ch.b.push_back(y);
+            if (!nl) break;
+            p = nl + 1;
+        }
+    };
+    std::vector<std::thread> pool;
+    std::atomic<size_t> next{0};
+    for (unsigned t = 0; t < std::min<size_t>(T, nchunk); ++t)
+        pool.emplace_back([&] {
+            for (size_t k; (k = next.fetch_add(1)) < nchunk;) lex_chunk(k);
+        });
+    for (auto &th : pool) th.join();
+    if (size_ == 0) {  // an empty file reads as one empty line at end-of-file
+        chunks_.assign(1, Chunk());
+        chunks_[0].kind.push_back(kEmpty);
+        chunks_[0].a.push_back(0);
+        chunks_[0].b.push_back(0);
+    }
+    for (Chunk &ch : chunks_) {
+        ch.first_line = lines_;
+        lines_ += ch.kind.size();
+    }
+}
+
+std::shared_ptr<const LexedFile> LexedFile::open(const std::string &fname) {
+    static std::mutex mu;
+    static std::unordered_map<std::string, std::weak_ptr<const LexedFile>> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    if (auto sp = cache[fname].lock()) return sp;
+    const int fd = ::open(fname.c_str(), O_RDONLY);
+    if (fd < 0) return nullptr;
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
+        ::close(fd);
+        return nullptr;
+    }
+    std::shared_ptr<LexedFile> f(new LexedFile());
+    f->lex(fname, fd, (uint64_t)st.st_size);
+    ::close(fd);
+    cache[fname] = f;
+    return f;
+}
+
+// ---------------------------------------------------------------------------
 // LineReader
 // ---------------------------------------------------------------------------
-LineReader::LineReader(const std::string &fname) {
+LineReader::LineReader(const std::string &fname, bool lexed) {
     if (fname == "stdin") {
         fp_ = stdin;
         shown_ = "standard input stream";
     } else {
-        fp_ = std::fopen(fname.c_str(), "rb");
-        if (!fp_) {
-            std::cerr << "error: could not read " << fname << std::endl << std::endl;
-            std::exit(1);
+        const char *nl = std::getenv("UNIPEAK_NO_LEX");  // tests: the plain getline reader
+        if (lexed && !(nl && *nl && *nl != '0')) lexed_ = LexedFile::open(fname);
+        if (!lexed_) {
+            fp_ = std::fopen(fname.c_str(), "rb");
+            if (!fp_) {
+                std::cerr << "error: could not read " << fname << std::endl << std::endl;
+                std::exit(1);
+            }
+            owned_ = true;
         }
-        owned_ = true;
         shown_ = fname;
     }
     open_ = true;
@@ -125,6 +268,11 @@ void LineReader::close() {
 }
 
 const std::string &LineReader::read() {
+    if (lexed_) {
+        uint32_t p, c;
+        if (next(&p, &c)) line_ = std::to_string(p) + " " + std::to_string(c);
+        return line_;
+    }
     ++line_no_;
     const ssize_t n = getline(&buf_, &cap_, fp_);
     if (n < 0) {
@@ -137,6 +285,39 @@ const std::string &LineReader::read() {
     else eof_ = true;  // a last line without '\n' sets eofbit
     line_.assign(buf_, len);
     return line_;
+}
+
+bool LineReader::next(uint32_t *pos, uint32_t *count) {
+    if (!lexed_) {
+        read();
+        return false;
+    }
+    ++line_no_;
+    const auto &cs = lexed_->chunks();
+    while (chunk_ < cs.size() && at_ >= cs[chunk_].kind.size()) {
+        ++chunk_;
+        at_ = 0;
+    }
+    if (chunk_ >= cs.size()) {  // past the end: what getline gives after eof
+        eof_ = true;
+        line_.clear();
+        return false;
+    }
+    const LexedFile::Chunk &ch = cs[chunk_];
+    const size_t i = at_++;
+    if (line_no_ == lexed_->lines()) eof_ = true;
+    switch (ch.kind[i]) {
+    case LexedFile::kData:
+        *pos = ch.a[i];
+        *count = ch.b[i];
+        return true;
+    case LexedFile::kText:
+        line_.assign(lexed_->bytes() + ch.toff[ch.a[i]], ch.b[i]);
+        return false;
+    default:
+        line_.clear();
+        return false;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -198,7 +379,7 @@ ContigTable ContigTable::parse(const std::string &fname) {
 // ---------------------------------------------------------------------------
 WigStream::WigStream(const std::string &fname, const ContigTable *ct, int16_t offset,
                      uint16_t use_length, int strand_filter)
-    : in_(fname), fname_(fname), ct_(ct), offset_(offset), use_length_(use_length),
+    : in_(fname, true), fname_(fname), ct_(ct), offset_(offset), use_length_(use_length),
       filter_(strand_filter) {
     name_ = fname_prefix(fname);
     a_.forward = true;
@@ -206,6 +387,7 @@ WigStream::WigStream(const std::string &fname, const ContigTable *ct, int16_t of
 }
 
 void WigStream::bad(const char *what) const {
+    if (t_defer_errors) throw DeferredError();
     std::cerr << "error: " << what << " in " << in_.display_name() << " line " << in_.line_no()
               << "\n" << std::endl;
     std::exit(1);
@@ -286,12 +468,8 @@ void WigStream::parse(const std::string &l) {
         if (!lex_uint(l.substr(0, d), 0xFFFFFFFFull, &pos)) bad("bad format");
         const size_t cs = d + (d + 1 < l.size() && l[d + 1] == '-' ? 2 : 1);
         if (!lex_uint(cs <= l.size() ? l.substr(cs) : std::string(), 0xFFFFFFFFull, &cnt)) bad("bad format");
-        a_.first = (uint32_t)pos;
-        a_.count = (uint32_t)cnt;
-        const uint32_t ext = use_length_ == 0 ? 0u : (uint32_t)(use_length_ - 1);
-        if (format_ == 6) a_.last = a_.first + (a_.forward ? ext : (uint32_t)(0u - ext));
-        else a_.last = a_.first + ext;
-        total_ += a_.count;
+        take((uint32_t)pos, (uint32_t)cnt);
+        return;
     } else if (starts(l, "variableStep chrom=") && l.size() > 19) {
         a_.contig = ct_->index(l.substr(19));
         return;
@@ -311,6 +489,15 @@ void WigStream::parse(const std::string &l) {
     } else {
         bad("bad format");
     }
+}
+
+void WigStream::take(uint32_t pos, uint32_t cnt) {
+    a_.first = pos;
+    a_.count = cnt;
+    const uint32_t ext = use_length_ == 0 ? 0u : (uint32_t)(use_length_ - 1);
+    if (format_ == 6) a_.last = a_.first + (a_.forward ? ext : (uint32_t)(0u - ext));
+    else a_.last = a_.first + ext;
+    total_ += a_.count;
     // offset and bounds (format.cpp:654-678)
     if (a_.count != 0 && a_.contig != ct_->size()) {
         if (use_length_ != 0) {
@@ -338,14 +525,25 @@ void WigStream::parse(const std::string &l) {
     }
 }
 
+// one line through the lexed fast path or the text parser; a lexed data
+// line is what parse() would make of its text
+void WigStream::next_line() {
+    uint32_t pos, cnt;
+    if (!in_.next(&pos, &cnt)) return parse(in_.line());
+    a_.count = 0;
+    if (format_ == 0) fatal("unsupported input format in " + fname_ + " (wiggle files only)");
+    if (a_.contig == ct_->size()) return;
+    take(pos, cnt);
+}
+
 void WigStream::read_plain() {
     if (in_.good()) {
-        parse(in_.read());
+        next_line();
     } else {
         a_.count = 0;
         a_.contig = ct_->size();
     }
-    while ((a_.count == 0 || a_.contig == ct_->size()) && in_.good()) parse(in_.read());
+    while ((a_.count == 0 || a_.contig == ct_->size()) && in_.good()) next_line();
 }
 
 const Align &WigStream::read_align() {
@@ -393,7 +591,7 @@ uint64_t WigStream::expected_tags() {
 // ---------------------------------------------------------------------------
 SampleStream::SampleStream(const std::string &fname, const ContigTable *ct, int16_t offset,
                            uint16_t use_length, bool nondirectional)
-    : nondir_(nondirectional) {
+    : fname_(fname), ct_(ct), offset_(offset), use_length_(use_length), nondir_(nondirectional) {
     if (!nondir_) {
         plain_.reset(new WigStream(fname, ct, offset, use_length, 0));
     } else {
@@ -405,6 +603,12 @@ SampleStream::SampleStream(const std::string &fname, const ContigTable *ct, int1
         merged_.contig = ct->size();
     }
 }
+
+std::unique_ptr<SampleStream> SampleStream::reopen() const {
+    return std::unique_ptr<SampleStream>(new SampleStream(fname_, ct_, offset_, use_length_, nondir_));
+}
+
+uint64_t SampleStream::size_hint() const { return nondir_ ? fwd_->size_hint() : plain_->size_hint(); }
 
 const WigStream &SampleStream::further() const {
     return fwd_->line_no() >= rev_->line_no() ? *fwd_ : *rev_;
@@ -427,6 +631,7 @@ const Align &SampleStream::read_align() {
     if (merged_.forward) {
         const Align &f = fwd_->read_align();
         if (f.forward && f.contig == merged_.contig && f.first < merged_.first) {
+            if (t_defer_errors) throw DeferredError();
             std::cerr << f.first << "\t" << merged_.first << "\n";
             fatal("alignments out of order");
         }

@@ -21,6 +21,13 @@ namespace unipeak {
 
 [[noreturn]] void fatal(const std::string &msg);  // "error: ..." + exit(1)
 
+// While set on a thread, input errors (fatal(), WigStream::bad()) throw
+// DeferredError instead of printing and exiting: a read-ahead decode uses it
+// to bail out to the serial replay, which then reports the error exactly
+// where the reference would.
+extern thread_local bool t_defer_errors;
+struct DeferredError {};
+
 // ---- misc/data.hpp:75-98 --------------------------------------------------
 class ContigTable {
   public:
@@ -39,16 +46,58 @@ class ContigTable {
     uint32_t genome_ = 0;
 };
 
-// std::getline + istream::good() semantics (filterstream.cpp:66-72)
+// A file split into the lines std::getline would return -- count('\n') + 1
+// of them, the last one (possibly empty) reaching end-of-file -- and lexed
+// by a thread pool over newline-aligned chunks of the memory-mapped file
+// (SURVEY.md 8(f) #1).  Lines of the canonical data form
+// "<digits>< |\t>[-]<digits>" with both values < 2^32 are stored as two
+// integers; every other line (track/variableStep headers, comments, anything
+// unusual) keeps its text for the exact serial parser, so the lexed path
+// changes speed only.  One instance per file name, shared by every handle
+// that reads the file (both strand handles of a nondirectional sample and
+// the counting pass of expected_tags).
+class LexedFile {
+  public:
+    enum Kind : uint8_t { kEmpty = 0, kData = 1, kText = 2 };
+    static std::shared_ptr<const LexedFile> open(const std::string &fname);  // null if unreadable
+    ~LexedFile();
+    uint64_t lines() const { return lines_; }
+    struct Chunk {
+        uint64_t first_line = 0;
+        std::vector<uint8_t> kind;
+        std::vector<uint32_t> a, b;  // data: pos, count; text: index into toff, length
+        std::vector<uint64_t> toff;  // byte offsets of the text lines
+    };
+    const std::vector<Chunk> &chunks() const { return chunks_; }
+    const char *bytes() const { return base_; }
+
+  private:
+    LexedFile() = default;
+    void lex(const std::string &fname, int fd, uint64_t size);
+    const char *base_ = nullptr;
+    uint64_t size_ = 0, lines_ = 0;
+    std::vector<Chunk> chunks_;
+};
+
+// host threads for ingest: UNIPEAK_THREADS, else min(16, hardware threads)
+unsigned ingest_threads();
+
+// std::getline + istream::good() semantics (filterstream.cpp:66-72); a
+// regular file is read through its LexedFile, stdin line by line
 class LineReader {
   public:
-    explicit LineReader(const std::string &fname);
+    explicit LineReader(const std::string &fname, bool lexed = false);
     ~LineReader();
     bool good() const { return open_ && !eof_; }
     const std::string &read();  // the next line without '\n'
+    // lexed readers: the next line; true with *pos, *count set for a data
+    // line, false with the text in line() otherwise
+    bool next(uint32_t *pos, uint32_t *count);
+    const std::string &line() const { return line_; }
     void close();
     uint64_t line_no() const { return line_no_; }
     const std::string &display_name() const { return shown_; }
+    uint64_t size_hint() const { return lexed_ ? lexed_->lines() : 0; }
 
   private:
     FILE *fp_ = nullptr;
@@ -57,6 +106,8 @@ class LineReader {
     std::string line_, shown_;
     char *buf_ = nullptr;
     size_t cap_ = 0;
+    std::shared_ptr<const LexedFile> lexed_;
+    size_t chunk_ = 0, at_ = 0;
 };
 
 // one parsed alignment record (misc/data.hpp:27-43, wiggle subset)
@@ -80,9 +131,12 @@ class WigStream {
     uint64_t confident() const { return confident_; }
     uint64_t out_of_bounds() const { return oob_; }
     uint64_t line_no() const { return in_.line_no(); }
+    uint64_t size_hint() const { return in_.size_hint(); }
 
   private:
     void parse(const std::string &line);
+    void take(uint32_t pos, uint32_t count);  // a data line's values (format.cpp:654-678)
+    void next_line();
     void read_plain();
     [[noreturn]] void bad(const char *what) const;
     LineReader in_;
@@ -103,6 +157,11 @@ class SampleStream {
   public:
     SampleStream(const std::string &fname, const ContigTable *ct, int16_t offset,
                  uint16_t use_length, bool nondirectional);
+    SampleStream(SampleStream &&) = default;
+    SampleStream &operator=(SampleStream &&) = default;
+    // a second, independent stream over the same input (shares its lexed file)
+    std::unique_ptr<SampleStream> reopen() const;
+    uint64_t size_hint() const;  // lines in the input (0 if unknown)
     const Align &read_align();
     const Align &last() const { return nondir_ ? merged_ : plain_->last(); }
     uint64_t expected_tags();
@@ -112,6 +171,10 @@ class SampleStream {
 
   private:
     const WigStream &further() const;  // the handle that has read more lines
+    std::string fname_;
+    const ContigTable *ct_;
+    int16_t offset_;
+    uint16_t use_length_;
     bool nondir_;
     std::unique_ptr<WigStream> plain_, fwd_, rev_;
     Align merged_;
