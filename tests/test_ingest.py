@@ -21,6 +21,7 @@ MODES = {
     "lexed_serial": {"UNIPEAK_SERIAL_INGEST": "1"},
     "lexed_parallel": {"UNIPEAK_THREADS": "4"},
     "lexed_parallel_1": {"UNIPEAK_THREADS": "1"},
+    "lexed_parallel_small_chunks": {"UNIPEAK_THREADS": "3", "UNIPEAK_LEX_CHUNK": "1500"},
 }
 
 

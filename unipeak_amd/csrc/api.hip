@@ -135,6 +135,11 @@ struct up_ctx {
     HostBuf<up_region> hp_regions;
     HostBuf<uint32_t> hp_counts;
     HostBuf<unsigned long long> hp_status;
+    // up_unit_scatter staging: two mapped host buffers the scatter kernel
+    // reads directly, reused once the event of their previous use fired
+    HostBuf<uint32_t> hp_scat[2];
+    hipEvent_t scat_ev[2] = {};
+    int scat_i = 0;
     uint64_t reg_cap = 1u << 16;  // record capacity of one pass (grown on demand)
     uint8_t *target = nullptr;    // device address of the caller's record buffer
     uint64_t target_cap = 0;
@@ -206,6 +211,7 @@ int up_open(int hip_device, up_ctx **out) {
     HIPCHK(hipSetDevice(hip_device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
+    for (auto &e : c->scat_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     *out = c;
     return UP_OK;
 }
@@ -240,6 +246,9 @@ void up_close(up_ctx *c) {
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
     c->hp_regions.release(); c->hp_counts.release(); c->hp_status.release(); c->hp_head.release();
+    for (auto &e : c->scat_ev) (void)hipEventSynchronize(e);
+    c->hp_scat[0].release(); c->hp_scat[1].release();
+    for (auto &e : c->scat_ev) (void)hipEventDestroy(e);
     c->d_wscreen.release(); c->d_stage.release(); c->d_dbg.release(); c->d_pack_ovf.release(); c->d_pack_n.release();
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
@@ -432,15 +441,23 @@ int up_unit_scatter(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, s
         }
         if (u.ovf_dirty) c->units_dirty = true;
     }
-    uint32_t *d = nullptr;
-    HIPCHK(hipMalloc(&d, 2 * n * sizeof(uint32_t)));
-    HIPCHK(hipMemcpyAsync(d, pos, n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(d + n, counts, n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
-                       track_ptr(c, unit, strand, sample), d, d + n, (uint64_t)n);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipFree(d));
+    // the caller's arrays are copied into the staging buffers before we
+    // return, so they may be reused at once; the kernels stay stream-ordered
+    constexpr size_t kChunk = (size_t)4 << 20;
+    uint8_t *track = track_ptr(c, unit, strand, sample);
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t m = std::min(kChunk, n - off);
+        const int k = c->scat_i;
+        c->scat_i ^= 1;
+        HIPCHK(hipEventSynchronize(c->scat_ev[k]));
+        HIPCHK(c->hp_scat[k].ensure(2 * kChunk));
+        std::memcpy(c->hp_scat[k].p, pos + off, m * sizeof(uint32_t));
+        std::memcpy(c->hp_scat[k].p + kChunk, counts + off, m * sizeof(uint32_t));
+        hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream,
+                           track, c->hp_scat[k].dev, c->hp_scat[k].dev + kChunk, (uint64_t)m);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->scat_ev[k], c->stream));
+    }
     c->ran = false;
     return UP_OK;
 }

@@ -124,6 +124,18 @@ void PhaseTimer::mark(const char *phase) {
     t_ = t;
     u_ = u;
     s_ = s;
+    a_last_ = t;
+}
+
+void PhaseTimer::accumulate(int slot) {
+    const double t = now_s();
+    if (a_last_ == 0) a_last_ = t_;
+    acc_[slot] += t - a_last_;
+    a_last_ = t;
+}
+
+void PhaseTimer::report(int slot, const char *phase) const {
+    if (on_) std::fprintf(stderr, "[timing] %s %.3f s\n", phase, acc_[slot]);
 }
 
 int env_gpus() {

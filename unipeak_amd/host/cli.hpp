@@ -47,9 +47,11 @@ class PhaseTimer {
   public:
     PhaseTimer();
     void mark(const char *phase);  // time since the previous mark
+    void accumulate(int slot);     // add the time since the last mark/accumulate to a slot
+    void report(int slot, const char *phase) const;
   private:
     bool on_;
-    double t_, u_ = 0, s_ = 0;
+    double t_, u_ = 0, s_ = 0, a_last_ = 0, acc_[4] = {0, 0, 0, 0};
 };
 
 }  // namespace unipeak

@@ -1,5 +1,6 @@
 // unipeak_amd/host/engine.cpp -- see engine.hpp.
 #include "engine.hpp"
+#include "cli.hpp"
 
 #include <algorithm>
 #include <atomic>
@@ -132,10 +133,7 @@ void stitch(std::vector<IterOut> &its, PassResult &out) {
 
 // a stream decoded ahead of the merge: every record read_align() returns
 // (the record already read by the caller first), then the count-0 end
-struct Rec {
-    uint32_t contig, first, count;
-    bool forward;
-};
+using Rec = Tag;
 
 struct Decoded {
     std::unique_ptr<SampleStream> stream;
@@ -143,18 +141,21 @@ struct Decoded {
     bool ok = false;
 };
 
-void decode_stream(const SampleStream &orig, Decoded &d) {
+void decode_stream(const SampleStream &orig, Decoded &d, unsigned threads) {
     t_defer_errors = true;
     try {
         d.stream = orig.reopen();
         d.stream->expected_tags();
         d.recs.reserve(d.stream->size_hint() + 1);
-        const Align *a = &d.stream->read_align();
-        for (;;) {
+        const Align *a = &d.stream->read_align();  // the caller's first read
+        if (a->count != 0) {
             d.recs.push_back(Rec{a->contig, a->first, a->count, a->forward});
-            if (a->count == 0) break;
-            a = &d.stream->read_align();
+            if (!d.stream->decode_rest(d.recs, threads)) {  // nondirectional: record by record
+                for (a = &d.stream->read_align(); a->count != 0; a = &d.stream->read_align())
+                    d.recs.push_back(Rec{a->contig, a->first, a->count, a->forward});
+            }
         }
+        d.recs.push_back(Rec{0, 0, 0, true});
         d.ok = true;
     } catch (const DeferredError &) {
         d.ok = false;
@@ -180,9 +181,10 @@ void build_units(std::vector<SampleStream *> &streams, const ContigTable &ct, bo
     if (parallel) {
         std::vector<std::thread> pool;
         std::atomic<size_t> next{0};
-        for (unsigned t = 0; t < std::min<size_t>(T, S); ++t)
+        const unsigned outer = (unsigned)std::min<size_t>(T, S), inner = std::max(1u, T / outer);
+        for (unsigned t = 0; t < outer; ++t)
             pool.emplace_back([&] {
-                for (size_t i; (i = next.fetch_add(1)) < S;) decode_stream(*streams[i], dec[i]);
+                for (size_t i; (i = next.fetch_add(1)) < S;) decode_stream(*streams[i], dec[i], inner);
             });
         for (auto &th : pool) th.join();
     }
@@ -285,7 +287,7 @@ void maybe_dump_units(const PassResult &pr, const std::vector<SampleStream *> &s
                      (unsigned long long)s->expected_tags(), (unsigned long long)s->confident(),
                      (unsigned long long)s->out_of_bounds());
     std::fclose(f);
-    std::exit(0);
+    exit_now(0);
 }
 
 namespace {
@@ -308,9 +310,40 @@ void check(int rc, const char *what) {
 
 }  // namespace
 
+// device contexts opened ahead, while the host parses (HIP runtime start-up
+// and context creation overlap ingest); run_units takes them over
+namespace {
+std::thread g_prewarm;
+std::vector<up_ctx *> g_pre;
+int g_pre_ndev = 0;
+}  // namespace
+
+static void join_prewarm() {
+    if (g_prewarm.joinable()) g_prewarm.join();
+}
+
+void prewarm_devices(int ngpus) {
+    g_exit_hook = join_prewarm;  // an input error must not exit mid-initialisation
+    g_prewarm = std::thread([ngpus] {
+        int nd = 0;
+        up_device_count(&nd);
+        if (ngpus > 0 && ngpus < nd) nd = ngpus;
+        std::vector<up_ctx *> pre(std::max(nd, 0), nullptr);
+        for (int d = 0; d < nd; ++d)
+            if (up_open(d, &pre[d]) != UP_OK) pre[d] = nullptr;
+        g_pre = std::move(pre);
+        g_pre_ndev = nd;
+    });
+}
+
 void run_units(const EngineParams &ep, PassResult &out) {
     int ndev = 0;
-    up_device_count(&ndev);
+    if (g_prewarm.joinable()) {
+        g_prewarm.join();
+        ndev = g_pre_ndev;
+    } else {
+        up_device_count(&ndev);
+    }
     if (ndev < 1) fatal("no HIP device available (the GPU path has no CPU fallback)");
     if (ep.ngpus > 0 && ep.ngpus < ndev) ndev = ep.ngpus;
     const size_t S = ep.p.n_samples;
@@ -361,8 +394,15 @@ void run_units(const EngineParams &ep, PassResult &out) {
             job.err = std::string(what) + ": " + up_strerror(rc);
         };
         if (job.units.empty()) return;
-        int rc = up_open(job.dev, &job.ctx);
-        if (rc) return fail(rc, "up_open");
+        PhaseTimer tm;
+        int rc = UP_OK;
+        if (job.dev < (int)g_pre.size() && g_pre[job.dev]) {
+            job.ctx = g_pre[job.dev];
+            g_pre[job.dev] = nullptr;
+        } else if ((rc = up_open(job.dev, &job.ctx))) {
+            return fail(rc, "up_open");
+        }
+        tm.mark("  gpu: up_open");
         up_params p = ep.p;
         p.is_control = ep.control.data();
         p.coeffs = ep.coeffs.empty() ? nullptr : ep.coeffs.data();
@@ -373,6 +413,7 @@ void run_units(const EngineParams &ep, PassResult &out) {
             const UnitBuild &u = out.units[gi];
             uint32_t id = 0;
             if ((rc = up_add_unit(job.ctx, u.len, nstr, u.buffer, &id))) return fail(rc, "up_add_unit");
+            tm.accumulate(0);
             job.dev_unit.push_back(gi);
             for (int st = 0; st < nstr; ++st) {
                 const size_t n = u.pos[st].size();
@@ -397,12 +438,18 @@ void run_units(const EngineParams &ep, PassResult &out) {
                 }
             }
             if (!u.add_pos.empty()) up_unit_set_last_add(job.ctx, id, u.add_pos.back());
+            tm.accumulate(1);
         }
+        tm.report(0, "  gpu: up_add_unit");
+        tm.report(1, "  gpu: scatter");
+        tm.mark("  gpu: units + scatter");
         uint64_t n = 0;
         if ((rc = up_run(job.ctx, &n))) return fail(rc, "up_run");
+        tm.mark("  gpu: up_run");
         std::vector<up_region> regs(n);
         std::vector<uint32_t> cnt(n * S);
         if (n && (rc = up_get_regions(job.ctx, regs.data(), cnt.data(), n))) return fail(rc, "up_get_regions");
+        tm.mark("  gpu: fetch");
         std::lock_guard<std::mutex> lk(mu);
         for (uint64_t i = 0; i < n; ++i) {
             Candidate c;
@@ -568,9 +615,13 @@ void write_profile(const PassResult &pr, uint16_t bw, ProfileSink &sink) {
 }
 
 void release_devices() {
+    join_prewarm();
     for (DeviceJob &j : g_jobs)
         if (j.ctx) up_close(j.ctx);
     g_jobs.clear();
+    for (up_ctx *c : g_pre)
+        if (c) up_close(c);
+    g_pre.clear();
 }
 
 }  // namespace unipeak

@@ -66,6 +66,10 @@ void build_units(std::vector<SampleStream *> &streams, const ContigTable &ct,
 // check the parallel ingest against the serial replay (UNIPEAK_SERIAL_INGEST=1)
 void maybe_dump_units(const PassResult &pr, const std::vector<SampleStream *> &streams);
 
+// start the HIP runtime and open the device contexts on a helper thread
+// (overlaps ingest); optional, run_units opens them itself otherwise
+void prewarm_devices(int ngpus);
+
 // run every unit on the GPU(s); fills out.cands
 void run_units(const EngineParams &ep, PassResult &out);
 

@@ -106,6 +106,7 @@ int main(int argc, char **argv) {
         }
     }
     const ContigTable ct = ContigTable::parse(ct_name);
+    prewarm_devices(env_gpus());
 
     // input streams, regions.cpp:184-202
     std::vector<std::unique_ptr<SampleStream>> st;
@@ -180,7 +181,7 @@ int main(int argc, char **argv) {
     ProfileSink prof;
     if (!profile.empty()) {  // regions.cpp:276-284: header first, profile as positions retire
         prof.fp = profile == "stdout" ? stdout : std::fopen(profile.c_str(), "wb");
-        if (!prof.fp) { std::cerr << "error: could not write " << profile << std::endl << std::endl; return 1; }
+        if (!prof.fp) { std::cerr << "error: could not write " << profile << std::endl << std::endl; exit_now(1); }
         std::setvbuf(prof.fp, nullptr, _IOFBF, 1 << 22);
         prof.ct = &ct;
         prof.directional = directional;
@@ -256,7 +257,7 @@ int main(int argc, char **argv) {
         table += row;
     }
     FILE *out = out_name == "stdout" ? stdout : std::fopen(out_name.c_str(), "wb");
-    if (!out) { std::cerr << "error: could not write " << out_name << std::endl << std::endl; return 1; }
+    if (!out) { std::cerr << "error: could not write " << out_name << std::endl << std::endl; exit_now(1); }
     std::fwrite(table.data(), 1, table.size(), out);
     if (out != stdout) std::fclose(out); else std::fflush(stdout);
     timer.mark("table");

@@ -55,6 +55,7 @@ int main(int argc, char **argv) {
         }
     }
     const ContigTable ct = ContigTable::parse(ct_name);
+    prewarm_devices(env_gpus());
     std::vector<std::unique_ptr<SampleStream>> st;
     std::vector<SampleStream *> sp;
     uint64_t total = 0;
@@ -125,7 +126,7 @@ int main(int argc, char **argv) {
             ++tested;
         }
     }
-    if (tested == 0) { std::cerr << "error: no regions qualified with given settings" << std::endl << std::endl; return 1; }
+    if (tested == 0) { std::cerr << "error: no regions qualified with given settings" << std::endl << std::endl; exit_now(1); }
     if (tested < n_test) std::cerr << "warning: too few regions qualified with given settings" << std::endl;
     char pct[64];
     std::snprintf(pct, sizeof pct, "%.1f", 100 * (double)tags_in / (double)total);
@@ -174,7 +175,7 @@ int main(int argc, char **argv) {
         for (size_t i = 0; i < W; ++i)
             if (freq[i]) o += fmt_lexical((double)i) + "\t" + fmt_lexical((double)freq[i]) + "\n";
         FILE *out = out_name == "stdout" ? stdout : std::fopen(out_name.c_str(), "wb");
-        if (!out) { std::cerr << "error: could not write " << out_name << std::endl << std::endl; return 1; }
+        if (!out) { std::cerr << "error: could not write " << out_name << std::endl << std::endl; exit_now(1); }
         std::fwrite(o.data(), 1, o.size(), out);
         if (out != stdout) std::fclose(out); else std::fflush(stdout);
     }

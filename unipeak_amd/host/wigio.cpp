@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <mutex>
 #include <thread>
 
@@ -21,11 +22,17 @@
 namespace unipeak {
 
 thread_local bool t_defer_errors = false;
+void (*g_exit_hook)() = nullptr;
+
+void exit_now(int code) {
+    if (g_exit_hook) g_exit_hook();
+    std::exit(code);
+}
 
 void fatal(const std::string &msg) {
     if (t_defer_errors) throw DeferredError();
     std::cerr << "error: " << msg << "\n" << std::endl;
-    std::exit(1);
+    exit_now(1);
 }
 
 // ---------------------------------------------------------------------------
@@ -151,7 +158,10 @@ void LexedFile::lex(const std::string &fname, int fd, uint64_t size) {
     }
     // newline-aligned chunk boundaries
     const unsigned T = ingest_threads();
-    const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(4ull * T, size_ / (1u << 20) + 1));
+    uint64_t chunk_bytes = 1u << 20;  // UNIPEAK_LEX_CHUNK: tests force many small chunks
+    if (const char *e = std::getenv("UNIPEAK_LEX_CHUNK")) chunk_bytes = std::max(1, std::atoi(e));
+    uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(4ull * T, size_ / chunk_bytes + 1));
+    if (std::getenv("UNIPEAK_LEX_CHUNK")) want = size_ / chunk_bytes + 1;
     std::vector<uint64_t> cut{0};
     for (uint64_t k = 1; k < want; ++k) {
         uint64_t c = size_ * k / want;
@@ -247,7 +257,7 @@ LineReader::LineReader(const std::string &fname, bool lexed) {
             fp_ = std::fopen(fname.c_str(), "rb");
             if (!fp_) {
                 std::cerr << "error: could not read " << fname << std::endl << std::endl;
-                std::exit(1);
+                exit_now(1);
             }
             owned_ = true;
         }
@@ -285,6 +295,27 @@ const std::string &LineReader::read() {
     else eof_ = true;  // a last line without '\n' sets eofbit
     line_.assign(buf_, len);
     return line_;
+}
+
+bool LineReader::take_run(const LexedFile::Chunk **ch, size_t *b, size_t *e) {
+    if (!lexed_ || !good()) return false;
+    const auto &cs = lexed_->chunks();
+    while (chunk_ < cs.size() && at_ >= cs[chunk_].kind.size()) {
+        ++chunk_;
+        at_ = 0;
+    }
+    if (chunk_ >= cs.size()) return false;
+    const LexedFile::Chunk &c = cs[chunk_];
+    size_t j = at_;
+    while (j < c.kind.size() && c.kind[j] != LexedFile::kText) ++j;
+    if (j == at_) return false;
+    *ch = &c;
+    *b = at_;
+    *e = j;
+    line_no_ += j - at_;
+    at_ = j;
+    if (line_no_ == lexed_->lines()) eof_ = true;
+    return true;
 }
 
 bool LineReader::next(uint32_t *pos, uint32_t *count) {
@@ -362,13 +393,13 @@ ContigTable ContigTable::parse(const std::string &fname) {
         const std::string name = l.substr(0, i);
         if (t.index(name) != t.size()) {
             std::cerr << "error: " << name << " defined twice in contig table\n" << std::endl;
-            std::exit(1);
+            exit_now(1);
         }
         t.add(name, (uint32_t)v);
     }
     if (t.size() == 0) {
         std::cerr << "error: no contigs in table" << std::endl << std::endl;
-        std::exit(1);
+        exit_now(1);
     }
     std::cerr << t.size() << " contigs" << std::endl;
     return t;
@@ -390,7 +421,7 @@ void WigStream::bad(const char *what) const {
     if (t_defer_errors) throw DeferredError();
     std::cerr << "error: " << what << " in " << in_.display_name() << " line " << in_.line_no()
               << "\n" << std::endl;
-    std::exit(1);
+    exit_now(1);
 }
 
 // name="(.+?)"
@@ -491,38 +522,136 @@ void WigStream::parse(const std::string &l) {
     }
 }
 
-void WigStream::take(uint32_t pos, uint32_t cnt) {
-    a_.first = pos;
-    a_.count = cnt;
-    const uint32_t ext = use_length_ == 0 ? 0u : (uint32_t)(use_length_ - 1);
-    if (format_ == 6) a_.last = a_.first + (a_.forward ? ext : (uint32_t)(0u - ext));
-    else a_.last = a_.first + ext;
-    total_ += a_.count;
-    // offset and bounds (format.cpp:654-678)
-    if (a_.count != 0 && a_.contig != ct_->size()) {
-        if (use_length_ != 0) {
-            const uint32_t ext = (uint32_t)(use_length_ - 1);
-            a_.last = a_.first + (a_.forward ? ext : (uint32_t)(0u - ext));
-        }
-        if (offset_ != 0) {
-            if ((a_.forward && (int)a_.first > -offset_) || (!a_.forward && (int)a_.last > offset_)) {
-                const uint32_t sh = (uint32_t)(a_.forward ? (int)offset_ : -(int)offset_);
-                a_.first += sh;
-                a_.last += sh;
-            } else {
-                oob_ += a_.count;
-                a_.count = 0;
-                return;
-            }
-        }
-        const uint32_t size = ct_->length(a_.contig);
-        if (a_.first == 0 || a_.first > size || a_.last == 0 || a_.last > size) {
-            oob_ += a_.count;
-            a_.count = 0;
+// a data line's values under the stream's state (format.cpp:654-678): a.forward
+// and a.contig hold the state; a.count ends 0 when the tag is out of bounds
+static inline void place(uint32_t pos, uint32_t cnt, int format, uint16_t use_length, int16_t offset,
+                         uint32_t size, Align &a, uint64_t &total, uint64_t &oob, uint64_t &confident) {
+    a.first = pos;
+    a.count = cnt;
+    const uint32_t ext = use_length == 0 ? 0u : (uint32_t)(use_length - 1);
+    if (format == 6) a.last = a.first + (a.forward ? ext : (uint32_t)(0u - ext));
+    else a.last = a.first + ext;
+    total += a.count;
+    if (a.count == 0) return;
+    if (use_length != 0) a.last = a.first + (a.forward ? ext : (uint32_t)(0u - ext));
+    if (offset != 0) {
+        if ((a.forward && (int)a.first > -offset) || (!a.forward && (int)a.last > offset)) {
+            const uint32_t sh = (uint32_t)(a.forward ? (int)offset : -(int)offset);
+            a.first += sh;
+            a.last += sh;
+        } else {
+            oob += a.count;
+            a.count = 0;
             return;
         }
-        confident_ += a_.count;
     }
+    if (a.first == 0 || a.first > size || a.last == 0 || a.last > size) {
+        oob += a.count;
+        a.count = 0;
+        return;
+    }
+    confident += a.count;
+}
+
+void WigStream::take(uint32_t pos, uint32_t cnt) {
+    place(pos, cnt, format_, use_length_, offset_, ct_->length(a_.contig), a_, total_, oob_, confident_);
+}
+
+bool WigStream::decode_rest(std::vector<Tag> &out, unsigned threads) {
+    if (filter_ != 0 || !in_.lexed()) return false;
+    // (A) serially: text lines through parse(), runs of other lines cut out
+    // as segments with the state they start in
+    struct Seg {
+        const LexedFile::Chunk *ch;
+        size_t b, e;
+        Align state;
+        int format;
+        size_t at;  // insertion point in out (records before it come first)
+        std::vector<Tag> tags;
+        uint64_t total = 0, oob = 0, confident = 0;
+    };
+    std::vector<Seg> segs;
+    std::vector<std::pair<size_t, Tag>> texts;  // (segments before it, record)
+    while (in_.good()) {
+        const LexedFile::Chunk *ch;
+        size_t b, e;
+        if (in_.take_run(&ch, &b, &e)) {
+            Seg g;
+            g.ch = ch;
+            g.b = b;
+            g.e = e;
+            g.state = a_;
+            g.format = format_;
+            segs.push_back(std::move(g));
+            continue;
+        }
+        next_line();  // a text line (or end of file)
+        if (a_.count != 0 && a_.contig != ct_->size())
+            texts.push_back({segs.size(), Tag{a_.contig, a_.first, a_.count, a_.forward}});
+    }
+    // (B) the segments in parallel
+    std::atomic<size_t> next{0};
+    std::atomic<bool> unsupported{false};
+    auto decode = [&] {
+        for (size_t k; (k = next.fetch_add(1)) < segs.size();) {
+            Seg &g = segs[k];
+            Align a = g.state;
+            if (a.contig == ct_->size()) continue;  // lines of unknown contigs are skipped
+            const uint32_t size = ct_->length(a.contig);
+            g.tags.reserve(g.e - g.b);
+            for (size_t i = g.b; i < g.e; ++i) {
+                if (g.ch->kind[i] != LexedFile::kData) continue;
+                if (g.format == 0) {  // parse() would stop at this line
+                    unsupported = true;
+                    break;
+                }
+                place(g.ch->a[i], g.ch->b[i], g.format, use_length_, offset_, size, a, g.total, g.oob,
+                      g.confident);
+                if (a.count != 0) g.tags.push_back(Tag{a.contig, a.first, a.count, a.forward});
+            }
+        }
+    };
+    const unsigned T = (unsigned)std::min<size_t>(std::max(1u, threads), std::max<size_t>(1, segs.size()));
+    auto run = [&](const std::function<void()> &fn) {
+        next = 0;
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < T; ++t) pool.emplace_back(fn);
+        fn();
+        for (auto &th : pool) th.join();
+    };
+    run(decode);
+    if (unsupported) fatal("unsupported input format in " + fname_ + " (wiggle files only)");
+    // (C) place every record in line order: text records before the segment
+    // that follows them, segments copied in parallel
+    size_t n = out.size() + texts.size();
+    std::vector<size_t> dest(segs.size());
+    size_t ti = 0, w = out.size();
+    for (size_t k = 0; k < segs.size(); ++k) {
+        while (ti < texts.size() && texts[ti].first == k) ++ti, ++w;
+        dest[k] = w;
+        w += segs[k].tags.size();
+        total_ += segs[k].total;
+        oob_ += segs[k].oob;
+        confident_ += segs[k].confident;
+        n += segs[k].tags.size();
+    }
+    const size_t base = out.size();
+    out.resize(n);
+    w = base;
+    ti = 0;
+    for (size_t k = 0; k <= segs.size(); ++k) {
+        while (ti < texts.size() && texts[ti].first == k) out[w++] = texts[ti++].second;
+        if (k < segs.size()) w += segs[k].tags.size();
+    }
+    run([&] {
+        for (size_t k; (k = next.fetch_add(1)) < segs.size();) {
+            std::copy(segs[k].tags.begin(), segs[k].tags.end(), out.begin() + dest[k]);
+            std::vector<Tag>().swap(segs[k].tags);
+        }
+    });
+    a_.count = 0;
+    a_.contig = ct_->size();
+    return true;
 }
 
 // one line through the lexed fast path or the text parser; a lexed data

@@ -20,6 +20,8 @@
 namespace unipeak {
 
 [[noreturn]] void fatal(const std::string &msg);  // "error: ..." + exit(1)
+[[noreturn]] void exit_now(int code);             // g_exit_hook, then std::exit
+extern void (*g_exit_hook)();                     // e.g. join helper threads
 
 // While set on a thread, input errors (fatal(), WigStream::bad()) throw
 // DeferredError instead of printing and exiting: a read-ahead decode uses it
@@ -93,6 +95,10 @@ class LineReader {
     // lexed readers: the next line; true with *pos, *count set for a data
     // line, false with the text in line() otherwise
     bool next(uint32_t *pos, uint32_t *count);
+    // lexed readers: the run of non-text lines at the cursor (within one
+    // chunk) as [*b, *e) of *ch, consumed; false at a text line or the end
+    bool take_run(const LexedFile::Chunk **ch, size_t *b, size_t *e);
+    bool lexed() const { return (bool)lexed_; }
     const std::string &line() const { return line_; }
     void close();
     uint64_t line_no() const { return line_no_; }
@@ -118,6 +124,12 @@ struct Align {
     uint32_t count = 0;
 };
 
+// a decoded record: what read_align() returns, minus the extent
+struct Tag {
+    uint32_t contig, first, count;
+    bool forward;
+};
+
 // ParseAlignStream restricted to wiggle input; strand_filter 0: none,
 // 1: forward only, 2: reverse only (StrandParseAlignStream)
 class WigStream {
@@ -132,6 +144,11 @@ class WigStream {
     uint64_t out_of_bounds() const { return oob_; }
     uint64_t line_no() const { return in_.line_no(); }
     uint64_t size_hint() const { return in_.size_hint(); }
+    // every further record read_align() would return, appended to out, the
+    // stream left at end of input with the same counters; data lines are
+    // decoded in parallel between header lines.  false (nothing read) for
+    // strand-filtered handles and unlexed input.
+    bool decode_rest(std::vector<Tag> &out, unsigned threads);
 
   private:
     void parse(const std::string &line);
@@ -162,6 +179,10 @@ class SampleStream {
     // a second, independent stream over the same input (shares its lexed file)
     std::unique_ptr<SampleStream> reopen() const;
     uint64_t size_hint() const;  // lines in the input (0 if unknown)
+    // WigStream::decode_rest for a directional stream; false otherwise
+    bool decode_rest(std::vector<Tag> &out, unsigned threads) {
+        return !nondir_ && plain_->decode_rest(out, threads);
+    }
     const Align &read_align();
     const Align &last() const { return nondir_ ? merged_ : plain_->last(); }
     uint64_t expected_tags();
