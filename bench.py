@@ -129,8 +129,15 @@ def main():
     S, n_ctl, nondir = W["samples"], W["controls"], W["nondir"]
     s_nc = S - n_ctl
     nstr = 2 if nondir else 1
-    units, owner, mine_all = shard.plan(lens, nondir=nondir, world=world, n_samples=S)
-    mine = mine_all[rank]
+    # UNIPEAK_SIM_WORLD=N UNIPEAK_SIM_RANK=r (single process, measurement aid
+    # only): plan for N ranks and run rank r's shard alone, no collectives --
+    # the compute side of one rank of an N-GPU run on a one-GPU box
+    sim_world = int(os.environ.get("UNIPEAK_SIM_WORLD", "0"))
+    sim_rank = int(os.environ.get("UNIPEAK_SIM_RANK", "0"))
+    if sim_world > 1 and comm is not None:
+        raise SystemExit("UNIPEAK_SIM_WORLD is for single-process runs")
+    units, owner, mine_all = shard.plan(lens, nondir=nondir, world=sim_world or world, n_samples=S)
+    mine = mine_all[sim_rank if sim_world > 1 else rank]
     need = sum(lens[units[k][0]] * nstr * S for k in mine)
     if need > 250e9:
         raise SystemExit(f"workload {args.workload} needs {need / 1e9:.0f} GB of tracks per GPU at "
@@ -150,40 +157,59 @@ def main():
                 g.synth(u, st, smp, seed, ci, synth_strand, nondir=nondir, peaks=smp < s_nc)
     local_tags = sum(g.tag_total(i, st, smp) for i in range(len(mine)) for st in range(nstr)
                      for smp in range(s_nc))
+    if sim_world > 1:  # the background needs the genome-wide total: generate the other units too
+        g2 = capi.Lib(local)
+        g2.set_params(args.bw, S, 0.0029, nondir=nondir, control=control)
+        for k in range(len(units)):
+            if k in mine:
+                continue
+            ci, buf = units[k]
+            g2.reset_units()
+            u = g2.add_unit(lens[ci], buffer_id=buf)
+            for st in range(nstr):
+                for smp in range(s_nc):
+                    g2.synth(u, st, smp, args.seed + smp, ci, st if nondir else buf, nondir=nondir, peaks=True)
+                    local_tags += g2.tag_total(u, st, smp)
+        g2.close()
     gen_s = time.time() - t_gen
     # K1a algorithmic bytes: one uint8 count per bp per strand per non-control
     # sample
     alg_bytes = sum(lens[units[k][0]] * nstr * s_nc for k in mine)
     copy_gbps = g.hbm_copy_gbps(1 << 30, 5)
 
-    phase = {"allreduce": 0.0, "run": 0.0, "gather_merge": 0.0}
+    phase = {"allreduce": 0.0, "launch": 0.0, "wait": 0.0, "gather_merge": 0.0}
     # one node (torchrun --nnodes=1): records meet in node-shared host memory
     gather_mode = os.environ.get("UNIPEAK_GATHER") or (
         "shm" if int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world else "rccl")
     bg_set = [None]
     nr = rbuf = cap = None
-    pool = pending = None
+    pool = None
     # size the record slots once (the data are the same every step): one
     # untimed pass with host delivery, then K3 writes every later pass
-    # straight into the slots, and rank 0 reads step i-1's slots on a helper
-    # thread while step i runs (up_run releases the GIL)
+    # straight into the slots
     g.set_params(args.bw, S, (comm.global_tags(local_tags) if comm else local_tags) / mappable /
                  (1 if nondir else 2), region_thr=25.0, kurt_thr=W["kurt"], corr_thr=W["corr"],
                  hit_thr=10.0 * s_nc, nondir=nondir, control=control, want_corr=W["want_corr"])
     n0 = g.run()
     cap = int((comm.max_over_ranks(n0) if comm else n0) * 1.25) + 64
-    if comm is None or gather_mode == "shm":
+    # shm delivery: passes are pipelined -- step i launches pass i and then
+    # completes pass i-1 (up_run_async / up_run_wait), so the GPU never waits
+    # for the host between passes; four rotating record slots per rank
+    pipelined = comm is None or gather_mode == "shm"
+    if pipelined:
         tag = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}_{os.environ.get('MASTER_PORT', '0')}"
-        nr = shard.NodeRecords(comm, cap, S, capi.REGION_DTYPE.itemsize, tag)
+        nr = shard.NodeRecords(comm, cap, S, capi.REGION_DTYPE.itemsize, tag, nslots=4)
         g.host_register(*nr.my_range())
         if rank == 0:
             from concurrent.futures import ThreadPoolExecutor
             pool = ThreadPoolExecutor(1)
     else:
-            rbuf = comm.target_buffer(cap, S, capi.REGION_DTYPE.itemsize)
-            comm.torch.cuda.synchronize()
-            g.set_record_target(rbuf.data_ptr(), cap)
-    it = [0]
+        rbuf = comm.target_buffer(cap, S, capi.REGION_DTYPE.itemsize)
+        comm.torch.cuda.synchronize()
+        g.set_record_target(rbuf.data_ptr(), cap)
+    it = [0]           # steps launched
+    reads = []         # rank 0: (step, future) of record reads in flight
+    done_times = []    # per completed pass: library timings
 
     def consume(parts):
         """rank 0: every rank's records in global unit order (zero-copy blocks)"""
@@ -191,86 +217,116 @@ def main():
         return (sum(len(b[1]) for b in blocks),
                 sum(int(np.count_nonzero(b[1]["accepted"])) for b in blocks))
 
-    def step():
-        nonlocal pending
-        t0 = time.perf_counter()
-        res = None
-        if pending is not None:  # step i-2's slots are free again once rank 0 read them
-            res = pending.result()
-            pending = None
-        tags = comm.global_tags(local_tags) if comm else local_tags
-        if nr is not None and rank == 0 and it[0] > 0:
-            # every rank entered this step, so step i-1 is in its slots: read it
-            # while this step runs (up_run releases the GIL)
-            pending = pool.submit(lambda p=(it[0] - 1) & 1: consume(nr.read(capi.REGION_DTYPE, p)))
+    def read_step(j):
+        return pool.submit(lambda: consume(nr.read(capi.REGION_DTYPE, j)))
+
+    def set_background(tags):
         # regions.cpp:205-213: tags / mappable, per strand when directional
         background = tags / mappable / (1 if nondir else 2)
         if bg_set[0] != background:
+            while it[0] > len(done_times):  # parameters change only between passes
+                g.run_wait()
+                done_times.append(g.timings())
             g.set_params(args.bw, S, background, region_thr=25.0, kurt_thr=W["kurt"],
                          corr_thr=W["corr"], hit_thr=10.0 * s_nc, nondir=nondir, control=control,
                          want_corr=W["want_corr"])
             bg_set[0] = background
-        if nr is not None:
-            g.set_record_target(nr.my_slot_address(it[0] & 1), cap)
-        t1 = time.perf_counter()
-        n = g.run()
-        t2 = time.perf_counter()
-        if rbuf is not None:  # RCCL gather of the device record buffers
+
+    def step():
+        i = it[0]
+        t0 = time.perf_counter()
+        if not pipelined:  # multi-node: blocking pass + RCCL gather of device record buffers
+            set_background(comm.global_tags(local_tags))
+            t1 = time.perf_counter()
+            g.run()
+            done_times.append(g.timings())
+            t2 = time.perf_counter()
             raw = comm.gather_target(rbuf)
             if raw is not None:
-                res = consume([shard.parse_target(raw[i], cap, S, capi.REGION_DTYPE) for i in range(world)])
+                consume([shard.parse_target(raw[k], cap, S, capi.REGION_DTYPE) for k in range(world)])
+            it[0] += 1
+            t3 = time.perf_counter()
+            phase["allreduce"] += t1 - t0
+            phase["launch"] += t2 - t1
+            phase["gather_merge"] += t3 - t2
+            return
+        # slot i % 4 held step i-4: its read must be over before any rank
+        # passes this step's collective and launches into it
+        while reads and reads[0][0] <= i - 4:
+            reads.pop(0)[1].result()
+        set_background(comm.global_tags(local_tags) if comm else local_tags)
+        t1 = time.perf_counter()
+        # every rank has completed pass i-2 (it waited for it before entering
+        # this collective): rank 0 reads it while passes i-1 and i run
+        if rank == 0 and i >= 2:
+            reads.append((i - 2, read_step(i - 2)))
+        g.set_record_target(nr.my_slot_address(i), cap)
+        g.run_async()
         it[0] += 1
+        t2 = time.perf_counter()
+        if i >= 1:
+            g.run_wait()
+            done_times.append(g.timings())
         t3 = time.perf_counter()
         phase["allreduce"] += t1 - t0
-        phase["run"] += t2 - t1
-        phase["gather_merge"] += t3 - t2
-        return n, res, g.timings()
+        phase["launch"] += t2 - t1
+        phase["wait"] += t3 - t2
 
     def drain():
-        """the last step's records (shm: after every rank finished it)"""
-        nonlocal pending
-        if nr is None:
+        """complete every pass; rank 0 reads the records of the steps not yet
+        read (after every rank finished them)"""
+        while it[0] > len(done_times):
+            g.run_wait()
+            done_times.append(g.timings())
+        if not pipelined:
             return None
-        res = None
-        if pending is not None:
-            res = pending.result()
-            pending = None
         if comm is not None:
             comm.dist.barrier()
+        res = None
         if rank == 0:
-            res = consume(nr.read(capi.REGION_DTYPE, (it[0] - 1) & 1))
+            last = it[0] - 1
+            pend = [f for j, f in reads]
+            reads.clear()
+            for f in pend:
+                res = f.result()
+            for j in range(max(0, last - 1), last + 1):
+                if j <= last - 2:
+                    continue
+                res = consume(nr.read(capi.REGION_DTYPE, j))
         return res
 
     def barrier():
         if comm is not None:
             comm.dist.barrier()
 
+    g.set_timing(2)  # warm-up passes report every phase
     for _ in range(args.warmup):
-        st = step()
-        if rank == 0:
-            tt = st[2]
-            print(f"[bench] warmup: K1 {tt[0]:.3f} ms (exact part {tt[4]:.3f}), K2 {tt[1]:.3f} ms, "
-                  f"K3 {tt[2]:.3f} ms, up_run wall {tt[3]:.3f} ms", file=sys.stderr, flush=True)
+        step()
     drain()
+    warm = [float(x) for x in done_times[-1]] if done_times else [0.0] * 5
+    if rank == 0 and done_times:
+        tt = done_times[-1]
+        print(f"[bench] warmup: K1 {tt[0]:.3f} ms (exact part {tt[4]:.3f}), K2 {tt[1]:.3f} ms, "
+              f"K3 {tt[2]:.3f} ms, pass wall {tt[3]:.3f} ms", file=sys.stderr, flush=True)
+    g.set_timing(1)  # timed passes: HIP events around K1a only (each pair idles the GPU a few us)
     for k in phase:
         phase[k] = 0.0
+    done_times.clear()
+    it[0] = 0
     barrier()
     if comm is not None:
         comm.torch.cuda.synchronize()
     t0 = time.perf_counter()
-    k1, k1a = [], []
-    last = None
     for _ in range(args.steps):
-        last = step()
-        k1.append(last[2][0])
-        k1a.append(last[2][0] - last[2][4])  # K1a = K1 minus its exact part (K1b)
+        step()
     final = drain()  # inside the timed region: the last step's records reach rank 0
-    if final is not None:
-        last = (last[0], final, last[2])
     barrier()
     if comm is not None:
         comm.torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    last = (None, final if final is not None else (n0, 0), None)
+    k1a = [t[0] - t[4] for t in done_times]  # K1a = K1 minus its exact part (timing level 1: K1b = 0)
+    k1 = k1a
     k1_ms = float(np.mean(k1))
     k1a_ms = float(np.mean(k1a))
     my_achieved = alg_bytes / (k1a_ms * 1e-3) / 1e9
@@ -285,6 +341,16 @@ def main():
         print("[bench] per-step phases (ms): " + ", ".join(
             f"{k} {v / args.steps * 1e3:.3f}" for k, v in phase.items()), file=sys.stderr, flush=True)
         value = genome / dt / 1e9
+        if sim_world > 1:  # not a headline line: one rank's shard of an N-GPU plan
+            print(json.dumps({"sim_world": sim_world, "sim_rank": sim_rank, "ms_per_step": round(dt * 1e3, 4),
+                              "shard_bp": int(alg_bytes // max(s_nc, 1)), "k1a_ms": round(k1a_ms, 4),
+                              "k1_ms": round(k1_ms, 4), "warmup_timings_ms": [round(x, 4) for x in warm], "phases_ms": {k: round(v / args.steps * 1e3, 4)
+                                                                      for k, v in phase.items()}}), flush=True)
+            g.set_record_target(0, 0)
+            g.close()
+            if pool is not None:
+                pool.shutdown()
+            return
         traffic, traffic_src = (pmc_traffic(alg_bytes) if (world == 1 and args.workload == "hg19-dir1")
                                 else (None, None))
         res = {
@@ -314,8 +380,11 @@ def main():
                          "kernel_ms": round(k1a_ms, 4), "kernel_ms_max_rank": round(k1a_max, 4),
                          "bytes_per_launch": int(alg_bytes),
                          "bytes_rule": "1 B (uint8 count) per bp per strand per non-control sample",
-                         "k1_total_ms": round(k1_ms, 4),
-                         "k1b_exact_ms": round(k1_ms - k1a_ms, 4),
+                         "k1_total_ms": round(k1a_ms + warm[4], 4),
+                         "k1b_exact_ms": round(warm[4], 4),
+                         "k2_ms": round(warm[1], 4), "k3_ms": round(warm[2], 4),
+                         "phase_ms_note": "K1b/K2/K3 from the last warm-up pass (timing level 2); "
+                                          "timed passes carry HIP events around K1a only",
                          "hbm_copy_GBps": round(copy_gbps, 1),
                          "frac_of_copy_rate": round(achieved / copy_gbps, 4)},
             "setup_s": round(gen_s, 2),

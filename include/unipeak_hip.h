@@ -140,6 +140,19 @@ int up_reset_units(up_ctx *ctx);
 
 /* Run K1..K3 over every unit (stream-ordered, blocking). */
 int up_run(up_ctx *ctx, uint64_t *n_regions);
+/* Pipelined form of up_run: up_run_async enqueues one pass and returns
+ * (at most two passes in flight); up_run_wait completes the OLDEST pass in
+ * flight and makes its records current (as up_run would).  Each pass
+ * delivers into the record target that was set when it was launched, so a
+ * caller alternates two targets; with host delivery the view of a pass stays
+ * valid until the second following launch.  Units and parameters cannot
+ * change while a pass is in flight (UP_E_STATE). */
+int up_run_async(up_ctx *ctx);
+int up_run_wait(up_ctx *ctx, uint64_t *n_regions);
+/* device timing of passes: 0 = wall time only, 1 = + K1a (HIP events around
+ * the streaming kernel), 2 = every phase (default).  Each event pair costs a
+ * few microseconds of idle GPU between kernels. */
+int up_set_timing(up_ctx *ctx, int level);
 /* Copy region records (unit-major, left-ascending) and optionally the
  * per-sample exptSums [n][S]. */
 int up_get_regions(up_ctx *ctx, up_region *out, uint32_t *counts, size_t cap);

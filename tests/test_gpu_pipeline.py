@@ -1,0 +1,138 @@
+"""Pipelined passes (up_run_async / up_run_wait, include/unipeak_hip.h):
+two passes in flight, each delivering into the record target that was set
+when it was launched, give exactly the records of the blocking up_run; state
+cannot change under a pass in flight; the K2 segmentation (two launches,
+re-armed counters) stays exact across many passes and across units whose
+strip counts span several K2 blocks."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from tests.gen import random_unit
+
+pytestmark = pytest.mark.gpu
+
+UP_E_STATE = -4
+
+
+def _load(g, rng, lengths, bw):
+    for L in lengths:
+        u = g.add_unit(L)
+        pos, cnt = random_unit(rng, L, bw)
+        g.scatter(u, 0, 0, pos, cnt[:, 0])
+
+
+def _target(cap, S, rec):
+    nbytes = 8 + cap * (rec + 4 * S)
+    buf = np.zeros(nbytes + 4096, np.uint8)
+    off = (-buf.ctypes.data) % 4096
+    return buf, off
+
+
+def _parse(buf, off, cap, S, dtype):
+    raw = buf[off:]
+    n = int(raw[:8].view(np.uint64)[0])
+    recs = raw[8:8 + n * dtype.itemsize].view(dtype).copy()
+    c0 = 8 + cap * dtype.itemsize
+    cnt = raw[c0:c0 + n * S * 4].view(np.uint32).reshape(n, S).copy()
+    return recs, cnt
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_async_matches_blocking(gpu_lib, seed):
+    capi = gpu_lib
+    rng = np.random.default_rng(seed)
+    bw = 50
+    lengths = [int(x) for x in rng.integers(30_000, 2_500_000, size=7)]
+    with capi.Lib(0) as g:
+        g.set_params(bw, 1, 0.003)
+        _load(g, rng, lengths, bw)
+        n = g.run()
+        ref, rcnt = g.regions(n)
+        assert n > 0
+        cap = n + 16
+        bufs = [_target(cap, 1, capi.REGION_DTYPE.itemsize) for _ in range(2)]
+        for b, off in bufs:
+            g.host_register(b[off:].ctypes.data, len(b) - off)
+        for timing in (0, 1, 2):
+            g.set_timing(timing)
+            got = []
+            npass = 6
+            for i in range(npass):
+                b, off = bufs[i & 1]
+                g.set_record_target(b[off:].ctypes.data, cap)
+                g.run_async()
+                if i >= 1:
+                    m = g.run_wait()
+                    pb, poff = bufs[(i - 1) & 1]
+                    got.append((m,) + _parse(pb, poff, cap, 1, capi.REGION_DTYPE))
+                # state is frozen while passes are in flight
+                with pytest.raises(capi.UpError) as e:
+                    g.set_params(bw, 1, 0.003)
+                assert e.value.code == UP_E_STATE
+            m = g.run_wait()
+            b, off = bufs[(npass - 1) & 1]
+            got.append((m,) + _parse(b, off, cap, 1, capi.REGION_DTYPE))
+            with pytest.raises(capi.UpError):
+                g.run_wait()  # nothing in flight
+            assert len(got) == npass
+            for m, recs, cnt in got:
+                assert m == n
+                assert recs.tobytes() == ref.tobytes()
+                assert np.array_equal(cnt, rcnt)
+        g.set_record_target(0, 0)
+        g.set_timing(2)
+        assert g.run() == n
+
+
+def test_async_host_delivery_and_growth(gpu_lib):
+    """host delivery (no target), first pass grows the record areas while a
+    second pass is in flight"""
+    capi = gpu_lib
+    rng = np.random.default_rng(5)
+    bw = 5  # narrow windows: most tags are regions of their own
+    with capi.Lib(0) as g:
+        g.set_params(bw, 1, 0.0005)  # low background: every tag opens a region
+        for L in (3_000_000, 1_200_000):
+            u = g.add_unit(L)
+            pos, cnt = random_unit(rng, L, bw, n_bg=L // 25)
+            g.scatter(u, 0, 0, pos, cnt[:, 0])
+        g.run_async()
+        g.run_async()
+        n1 = g.run_wait()
+        r1, c1 = g.regions(n1)
+        n2 = g.run_wait()
+        r2, c2 = g.regions(n2)
+        n3 = g.run()
+        r3, c3 = g.regions(n3)
+    assert n1 == n2 == n3 and n1 > (1 << 16)  # beyond the initial record capacity
+    assert r1.tobytes() == r2.tobytes() == r3.tobytes()
+    assert np.array_equal(c1, c3) and np.array_equal(c2, c3)
+
+
+def test_many_units_many_blocks(gpu_lib, oracle):
+    """strip counts spanning several 256-strip K2 blocks; every unit checked
+    against the oracle"""
+    capi = gpu_lib
+    rng = np.random.default_rng(11)
+    bw, bg = 50, 0.003
+    lengths = [int(x) for x in rng.integers(1_000, 9_000_000, size=5)]
+    data = []
+    with capi.Lib(0) as g:
+        g.set_params(bw, 1, bg)
+        for L in lengths:
+            u = g.add_unit(L)
+            pos, cnt = random_unit(rng, L, bw)
+            g.scatter(u, 0, 0, pos, cnt[:, 0])
+            data.append((pos, cnt))
+        for _ in range(3):
+            n = g.run()
+        regs, gcnt = g.regions(n)
+    for u, (pos, cnt) in enumerate(data):
+        ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt)
+        m = regs["unit"] == u
+        for k in ("left", "right", "peak", "sum", "accepted"):
+            assert np.array_equal(ref[k], regs[m][k]), (u, k)
+        assert np.array_equal(ref_sums, gcnt[m])
+        assert ref["peak_score"].tobytes() == regs[m]["peak_score"].tobytes()

@@ -69,7 +69,7 @@ EXPORTS = [
     "up_unit_scatter", "up_unit_synth", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
     "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan",
     "up_timings", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
-    "up_host_register", "up_unit_profile_range",
+    "up_host_register", "up_unit_profile_range", "up_run_async", "up_run_wait", "up_set_timing",
 ]
 
 
@@ -103,6 +103,9 @@ def load_library(path=LIB_PATH):
         "up_unit_last_add": (c.c_int, [vp, c.c_uint32, u32p]),
         "up_reset_units": (c.c_int, [vp]),
         "up_run": (c.c_int, [vp, c.POINTER(c.c_uint64)]),
+        "up_run_async": (c.c_int, [vp]),
+        "up_run_wait": (c.c_int, [vp, c.POINTER(c.c_uint64)]),
+        "up_set_timing": (c.c_int, [vp, c.c_int]),
         "up_get_regions": (c.c_int, [vp, vp, vp, c.c_size_t]),
         "up_regions_view": (c.c_int, [vp, c.POINTER(vp), c.POINTER(vp), c.POINTER(c.c_uint64)]),
         "up_shift_scan": (c.c_int, [vp, vp, c.c_size_t, c.c_uint16, vp]),
@@ -226,6 +229,20 @@ class Lib:
         n = ctypes.c_uint64()
         _ck(self.L.up_run(self.ctx, ctypes.byref(n)))
         return n.value
+
+    def run_async(self):
+        """enqueue one pass (at most two in flight); see up_run_async"""
+        _ck(self.L.up_run_async(self.ctx))
+
+    def run_wait(self):
+        """complete the oldest pass in flight -> its region count"""
+        n = ctypes.c_uint64()
+        _ck(self.L.up_run_wait(self.ctx, ctypes.byref(n)))
+        return n.value
+
+    def set_timing(self, level):
+        """0: wall only, 1: + K1a events, 2: every phase (default)"""
+        _ck(self.L.up_set_timing(self.ctx, int(level)))
 
     def regions(self, n, with_counts=True):
         out = np.zeros(n, REGION_DTYPE)

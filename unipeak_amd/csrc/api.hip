@@ -2,7 +2,6 @@
 // device memory for the unit tracks, kernel launches and the glue between
 // them.  Host-side only; kernels live in kernels.hip.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -45,6 +44,8 @@ struct DevBuf {
     size_t n = 0;
     hipError_t ensure(size_t want) {
         if (want <= n && p) return hipSuccess;
+        // growth is rare (first passes); a pipelined pass may still read p
+        if (p) (void)hipDeviceSynchronize();
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
@@ -69,6 +70,7 @@ struct HostBuf {
     size_t n = 0;
     hipError_t ensure(size_t want) {
         if (want <= n && p) return hipSuccess;
+        if (p) (void)hipDeviceSynchronize();
         if (p) (void)hipHostFree(p);
         p = dev = nullptr;
         n = 0;
@@ -112,8 +114,7 @@ struct up_ctx {
     int bw_layout = -1;  // bw the strip layout was computed for
     DevBuf<uint64_t> d_info;
     DevBuf<uint32_t> d_rec, d_lastnz, d_ovf_count, d_ovf_rec, d_unit_last;
-    DevBuf<uint64_t> d_cnt, d_off, d_nreg;
-    DevBuf<unsigned char> d_tmp;
+    DevBuf<uint64_t> d_cnt, d_nreg;
     DevBuf<uint32_t> d_starts, d_ends, d_runit, d_peak_pos, d_xlist, d_xcount;
     DevBuf<double> d_peak_val;
     uint32_t ovf_cap = 256;
@@ -122,6 +123,21 @@ struct up_ctx {
     std::vector<uint32_t> unit_last;
     hipEvent_t ev[8] = {};
     double times[5] = {0, 0, 0, 0, 0};
+    int timing = 2;                  // up_set_timing: 0 wall only, 1 + K1a, 2 every phase
+    bool counters_armed = false;     // xcount / ovf_count are zero (re-armed by K2b)
+    // passes in flight (up_run_async); slot = sequence & 1
+    struct Pass {
+        uint8_t *target = nullptr;   // record target of this pass (device address) or null
+        void *target_hostp = nullptr;// host address of a host target
+        uint64_t target_cap = 0;
+        uint64_t cap = 0;            // reg_cap at launch
+        uint32_t ovf_cap = 0;
+        std::chrono::steady_clock::time_point t0;
+        hipEvent_t ev[5] = {};       // K1a begin, K1a end, K1b end, K2 end, K3 end
+        hipEvent_t done = nullptr;
+    } pass[2];
+    uint64_t seq_launched = 0, seq_done = 0;
+    int cur_slot = 0;                // slot of the last completed pass (host records)
     // head-hit (quirk Q1) replay
     DevBuf<uint32_t> d_head, d_resync, d_emu_n, d_emu_err, d_emu_counts, d_ring_hits, d_reg_hit, d_reg_hits;
     DevBuf<int32_t> d_unit_buffer;
@@ -131,10 +147,13 @@ struct up_ctx {
     std::vector<up_region> h_regions;
     std::vector<uint32_t> h_counts;
     std::vector<uint8_t> h_emulated;
-    HostBuf<uint32_t> hp_head;  // head-hit flags, written by head_detect_kernel
-    HostBuf<up_region> hp_regions;
-    HostBuf<uint32_t> hp_counts;
-    HostBuf<unsigned long long> hp_status;
+    // per pass slot: head-hit flags (head_detect_kernel), host records, status
+    HostBuf<uint32_t> hp_head[2];
+    HostBuf<up_region> hp_regions[2];
+    HostBuf<uint32_t> hp_counts[2];
+    HostBuf<unsigned long long> hp_status[2];
+    DevBuf<uint64_t> d_bsum;
+    void *target_hostp = nullptr;    // host address of the current host target
     // up_unit_scatter staging: two mapped host buffers the scatter kernel
     // reads directly, reused once the event of their previous use fired
     HostBuf<uint32_t> hp_scat[2];
@@ -147,6 +166,8 @@ struct up_ctx {
     std::vector<void *> host_regs; // up_host_register ranges (unregistered at close)
     uint64_t last_nreg = 0;
 };
+
+static bool busy(const up_ctx *c) { return c && c->seq_launched != c->seq_done; }
 
 #define HIPCHK(x)                                                                   \
     do {                                                                            \
@@ -211,6 +232,10 @@ int up_open(int hip_device, up_ctx **out) {
     HIPCHK(hipSetDevice(hip_device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
+    for (auto &ps : c->pass) {
+        for (auto &e : ps.ev) HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipEventCreateWithFlags(&ps.done, hipEventDisableTiming));
+    }
     for (auto &e : c->scat_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     *out = c;
     return UP_OK;
@@ -239,13 +264,18 @@ void up_close(up_ctx *c) {
     c->d_kern.release(); c->d_coef.release(); c->d_nc.release(); c->d_ctl.release();
     c->d_units.release(); c->d_info.release(); c->d_rec.release(); c->d_lastnz.release();
     c->d_ovf_count.release(); c->d_ovf_rec.release(); c->d_unit_last.release();
-    c->d_cnt.release(); c->d_off.release(); c->d_nreg.release(); c->d_tmp.release();
+    c->d_cnt.release(); c->d_nreg.release();
     c->d_starts.release(); c->d_ends.release(); c->d_runit.release();
     c->d_peak_pos.release(); c->d_peak_val.release(); c->d_xlist.release(); c->d_xcount.release();
     c->d_head.release(); c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
-    c->hp_regions.release(); c->hp_counts.release(); c->hp_status.release(); c->hp_head.release();
+    for (int k = 0; k < 2; ++k) {
+        c->hp_regions[k].release(); c->hp_counts[k].release(); c->hp_status[k].release(); c->hp_head[k].release();
+        for (auto &e : c->pass[k].ev) (void)hipEventDestroy(e);
+        (void)hipEventDestroy(c->pass[k].done);
+    }
+    c->d_bsum.release();
     for (auto &e : c->scat_ev) (void)hipEventSynchronize(e);
     c->hp_scat[0].release(); c->hp_scat[1].release();
     for (auto &e : c->scat_ev) (void)hipEventDestroy(e);
@@ -257,6 +287,7 @@ void up_close(up_ctx *c) {
 
 int up_set_params(up_ctx *c, const up_params *p) {
     if (!c || !p) return UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     if (p->n_samples == 0 || p->bw == 0) return UP_E_ARG;
     HIPCHK(hipSetDevice(c->dev));
     const int S = p->n_samples;
@@ -334,6 +365,7 @@ static uint64_t unit_stride(uint32_t len) {
 
 int up_add_unit(up_ctx *c, uint32_t len, int32_t nstrands, int32_t buffer_id, uint32_t *unit_id) {
     if (!c || !c->have_params || (nstrands != 1 && nstrands != 2)) return c && !c->have_params ? UP_E_STATE : UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     if (nstrands != (c->p.nondir ? 2 : 1)) return UP_E_ARG;
     HIPCHK(hipSetDevice(c->dev));
     Unit u;
@@ -361,6 +393,7 @@ int up_unit_count(up_ctx *c, uint32_t *n) {
 
 int up_reset_units(up_ctx *c) {
     if (!c) return UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->stream);
     free_units(c);
@@ -415,6 +448,7 @@ static int pack_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample,
 int up_unit_pack(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, const uint32_t *dev_counts) {
     int r = check_track(c, unit, strand, sample);
     if (r) return r;
+    if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     if (!dev_counts) return UP_E_ARG;
     HIPCHK(hipSetDevice(c->dev));
     if ((r = pack_track(c, unit, strand, sample, dev_counts))) return r;
@@ -426,6 +460,7 @@ int up_unit_scatter(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, s
                     const uint32_t *pos, const uint32_t *counts) {
     int r = check_track(c, unit, strand, sample);
     if (r) return r;
+    if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     if (n == 0) return UP_OK;
     if (!pos || !counts) return UP_E_ARG;
     const uint32_t len = c->units[unit].len;
@@ -474,6 +509,7 @@ int up_unit_synth(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uin
                   uint32_t contig_index, int32_t synth_strand, int32_t nondir, int32_t with_peaks) {
     int r = check_track(c, unit, strand, sample);
     if (r) return r;
+    if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     HIPCHK(hipSetDevice(c->dev));
     const uint32_t len = c->units[unit].len;
     const int bw = c->p.bw;
@@ -560,6 +596,7 @@ int up_unit_tag_total(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample,
 
 int up_unit_set_last_add(up_ctx *c, uint32_t unit, uint32_t last) {
     if (!c || unit >= c->units.size()) return UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     c->units[unit].last_override = last;
     c->units[unit].has_override = true;
     return UP_OK;
@@ -569,6 +606,7 @@ static int sync_units(up_ctx *c);
 
 int up_unit_last_add(up_ctx *c, uint32_t unit, uint32_t *last) {
     if (!c || !last || unit >= c->units.size()) return UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     if (c->units[unit].has_override) { *last = c->units[unit].last_override; return UP_OK; }
     if (!c->have_params) return UP_E_STATE;
     HIPCHK(hipSetDevice(c->dev));
@@ -748,30 +786,33 @@ static int check_runnable(up_ctx *c) {
 // Quirk Q1: units whose pooled hits include a position <= bw are replayed
 // by the exact state machine (emulate.hip); their early regions replace the
 // parallel path's, and the merged list moves to the host.
-static int launch_head_detect(up_ctx *c) {
+static int launch_head_detect(up_ctx *c, int slot) {
     const uint32_t nu = (uint32_t)c->units.size();
     HIPCHK(c->d_head.ensure(nu));
-    HIPCHK(c->hp_head.ensure(nu));
+    HIPCHK(c->hp_head[slot].ensure(nu));
     if (pool_mode(c) == 2)
         hipLaunchKernelGGL(head_detect_kernel<2>, dim3(nu), dim3(128), 0, c->stream, c->d_units.p,
                            (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw,
-                           c->d_head.p, c->hp_head.dev);
+                           c->d_head.p, c->hp_head[slot].dev);
     else
         hipLaunchKernelGGL(head_detect_kernel<1>, dim3(nu), dim3(128), 0, c->stream, c->d_units.p,
                            (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw,
-                           c->d_head.p, c->hp_head.dev);
+                           c->d_head.p, c->hp_head[slot].dev);
     HIPCHK(hipGetLastError());
     return UP_OK;
 }
 
-// after the stream sync that follows launch_head_detect
-static int replay_head_hits(up_ctx *c) {
+// after the pass of `slot` completed (stream idle)
+static int replay_head_hits(up_ctx *c, int slot) {
     c->host_regions = false;
     const uint32_t nu = (uint32_t)c->units.size();
-    const uint32_t *head = c->hp_head.p;
+    const uint32_t *head = c->hp_head[slot].p;
     bool any = false;
     for (uint32_t i = 0; i < nu; ++i) any |= head[i] != 0;
     if (!any) return UP_OK;
+    // the head flags are a function of the (unchanged) tracks, so d_head of
+    // a later pass still describes this one
+    HIPCHK(hipStreamSynchronize(c->stream));
 
     const int S = c->p.n_samples;
     const uint32_t W = 2u * c->p.bw + 1;
@@ -842,8 +883,26 @@ static int replay_head_hits(up_ctx *c) {
         HIPCHK(hipMemcpy(emu.data(), c->d_emu_out.p, nemu * sizeof(up_region), hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(ecnt.data(), c->d_emu_counts.p, ecnt.size() * 4, hipMemcpyDeviceToHost));
     }
-    const up_region *par = c->hp_regions.p;  // staged by up_run
-    const uint32_t *pcnt = c->hp_counts.p;
+    // the parallel path's records of this pass, wherever K3 wrote them
+    const up_ctx::Pass &ps = c->pass[slot];
+    const up_region *par = c->hp_regions[slot].p;
+    const uint32_t *pcnt = c->hp_counts[slot].p;
+    std::vector<up_region> dpar;
+    std::vector<uint32_t> dcnt;
+    if (ps.target && ps.target_hostp) {
+        par = (const up_region *)((const uint8_t *)ps.target_hostp + 8);
+        pcnt = (const uint32_t *)((const uint8_t *)ps.target_hostp + 8 + ps.target_cap * sizeof(up_region));
+    } else if (ps.target) {
+        dpar.resize(c->nreg);
+        dcnt.resize((size_t)c->nreg * S);
+        if (c->nreg) {
+            HIPCHK(hipMemcpy(dpar.data(), ps.target + 8, c->nreg * sizeof(up_region), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(dcnt.data(), ps.target + 8 + ps.target_cap * sizeof(up_region),
+                             dcnt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        }
+        par = dpar.data();
+        pcnt = dcnt.data();
+    }
     // merge: unit-major; within a unit the replayed regions, then the
     // parallel ones that start at or after the resync position
     std::vector<std::pair<uint64_t, int64_t>> keys;  // (unit<<32 | order, +par idx / -emu idx-1)
@@ -875,148 +934,240 @@ static int replay_head_hits(up_ctx *c) {
     }
     c->host_regions = true;
     c->nreg = c->h_regions.size();
-    if (c->target) {  // keep the caller's device buffer authoritative
-        if (c->nreg > c->target_cap) return UP_E_NOMEM;
+    if (ps.target) {  // keep the caller's buffer authoritative
+        if (c->nreg > ps.target_cap) return UP_E_NOMEM;
         const uint64_t hdr = c->nreg;
-        HIPCHK(hipMemcpy(c->target, &hdr, 8, hipMemcpyHostToDevice));
-        if (c->nreg) {
-            HIPCHK(hipMemcpy(c->target + 8, c->h_regions.data(), c->nreg * sizeof(up_region), hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(c->target + 8 + c->target_cap * sizeof(up_region), c->h_counts.data(),
-                             c->h_counts.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        const size_t cb = c->h_counts.size() * sizeof(uint32_t);
+        if (ps.target_hostp) {
+            uint8_t *h = (uint8_t *)ps.target_hostp;
+            std::memcpy(h, &hdr, 8);
+            if (c->nreg) {
+                std::memcpy(h + 8, c->h_regions.data(), c->nreg * sizeof(up_region));
+                std::memcpy(h + 8 + ps.target_cap * sizeof(up_region), c->h_counts.data(), cb);
+            }
+        } else {
+            HIPCHK(hipMemcpy(ps.target, &hdr, 8, hipMemcpyHostToDevice));
+            if (c->nreg) {
+                HIPCHK(hipMemcpy(ps.target + 8, c->h_regions.data(), c->nreg * sizeof(up_region), hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(ps.target + 8 + ps.target_cap * sizeof(up_region), c->h_counts.data(), cb,
+                                 hipMemcpyHostToDevice));
+            }
         }
     }
     return UP_OK;
 }
 
-int up_run(up_ctx *c, uint64_t *n_regions) {
+// Enqueue one pass K1a -> K1b -> K2a -> K2b -> K3 -> head detect into `slot`
+// with no host round trip: the region count stays on the device, the record
+// areas are pre-sized (reg_cap, ovf_cap) and K3 writes the records straight
+// into mapped pinned host memory (or the caller's record target).  An
+// undersized area is detected when the pass is finished; it is grown and
+// the pass rerun (first passes only).
+static int launch_pass(up_ctx *c, int slot) {
+    const uint32_t ns = c->nstrips;
+    const int S = c->p.n_samples;
+    up_ctx::Pass &ps = c->pass[slot];
+    const uint32_t nsb = (ns + kSegBlock - 1) / kSegBlock;
+    HIPCHK(c->d_info.ensure(ns));
+    HIPCHK(c->d_rec.ensure((size_t)ns * kRecStride));
+    HIPCHK(c->d_xlist.ensure((size_t)ns * kXEntry));
+    HIPCHK(c->d_cnt.ensure(ns));
+    HIPCHK(c->d_bsum.ensure(nsb));
+    HIPCHK(c->d_nreg.ensure(1));
+    HIPCHK(c->hp_status[slot].ensure(4));
+    if (!c->d_xcount.p || !c->d_ovf_count.p) c->counters_armed = false;
+    HIPCHK(c->d_xcount.ensure(1));
+    HIPCHK(c->d_ovf_count.ensure(1));
+    const uint64_t cap = c->reg_cap;
+    HIPCHK(c->d_ovf_rec.ensure((size_t)c->ovf_cap * kOvfStride));
+    HIPCHK(c->d_peak_pos.ensure(cap + 1));
+    HIPCHK(c->d_peak_val.ensure(cap + 1));
+    HIPCHK(c->d_starts.ensure(cap + 1));
+    HIPCHK(c->d_ends.ensure(cap + 1));
+    HIPCHK(c->d_runit.ensure(cap + 1));
+    if (!c->target) {
+        HIPCHK(c->hp_regions[slot].ensure(cap + 1));
+        HIPCHK(c->hp_counts[slot].ensure((cap + 1) * S));
+    }
+    ps.target = c->target;
+    ps.target_hostp = c->target_hostp;
+    ps.target_cap = c->target_cap;
+    ps.cap = cap;
+    ps.ovf_cap = c->ovf_cap;
+    if (!c->counters_armed) {  // K2b re-arms them at the end of every pass
+        HIPCHK(hipMemsetAsync(c->d_ovf_count.p, 0, sizeof(uint32_t), c->stream));
+        HIPCHK(hipMemsetAsync(c->d_xcount.p, 0, sizeof(uint32_t), c->stream));
+    }
+    c->counters_armed = false;  // until K2b is enqueued
+    ScanParams SP = scan_params(c);
+#ifdef UPK_DEBUG_COUNTS
+    static const bool dbg = getenv("UNIPEAK_DEBUG_COUNTS") != nullptr;
+    if (dbg) {
+        HIPCHK(c->d_dbg.ensure(8));
+        HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 8 * sizeof(unsigned long long), c->stream));
+        SP.dbg = c->d_dbg.p;
+    }
+#endif
+    const int tl = c->timing;
+    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[0], c->stream));
+    dispatch_scan<false, kModeScreen>(c, SP, 0, ns);   // K1a: stream + screen
+    HIPCHK(hipGetLastError());
+    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[1], c->stream));
+    dispatch_scan<false, kModeExact>(c, SP, 0, ns);    // K1b: exact blocks
+    HIPCHK(hipGetLastError());
+    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[2], c->stream));
+    unsigned long long *thdr = (unsigned long long *)ps.target;
+    hipLaunchKernelGGL(seg_count_kernel, dim3(nsb), dim3(kSegBlock), 0, c->stream, c->d_info.p, c->d_cnt.p,
+                       c->d_bsum.p, ns);
+    hipLaunchKernelGGL(seg_compact_kernel, dim3(nsb), dim3(kSegBlock), 0, c->stream, c->d_units.p,
+                       (uint32_t)c->units.size(), c->d_info.p, c->d_cnt.p, c->d_bsum.p, c->d_rec.p,
+                       c->d_ovf_rec.p, c->ovf_cap, c->d_starts.p, c->d_ends.p, c->d_runit.p, c->d_peak_pos.p,
+                       c->d_peak_val.p, ns, (uint64_t)cap, c->d_ovf_count.p, c->d_xcount.p, c->d_nreg.p,
+                       c->hp_status[slot].dev, thdr);
+    HIPCHK(hipGetLastError());
+    c->counters_armed = true;
+    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[3], c->stream));
+    StatParams P = stat_params(c);
+    P.cap = cap;
+    P.peak_pos = c->d_peak_pos.p;
+    P.peak_val = c->d_peak_val.p;
+    if (ps.target) {  // records into the caller's buffer instead
+        P.cap = std::min<uint64_t>(cap, ps.target_cap);
+        P.out = ps.target + 8;
+        P.out_counts = (uint32_t *)(ps.target + 8 + ps.target_cap * sizeof(up_region));
+    } else {
+        P.out = c->hp_regions[slot].dev;
+        P.out_counts = c->hp_counts[slot].dev;
+    }
+    dispatch_stats(c, P, std::max<uint64_t>(c->last_nreg, 1024));
+    HIPCHK(hipGetLastError());
+    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[4], c->stream));
+    int r = launch_head_detect(c, slot);
+    if (r) return r;
+    HIPCHK(hipEventRecord(ps.done, c->stream));
+    return UP_OK;
+}
+
+static int prepare_run(up_ctx *c) {
     int r = check_runnable(c);
     if (r) return r;
-    const auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipSetDevice(c->dev));
+    return sync_units(c);
+}
+
+int up_run_async(up_ctx *c) {
+    if (!c) return UP_E_ARG;
+    if (c->seq_launched - c->seq_done >= 2) return UP_E_STATE;  // at most two passes in flight
+    int r = prepare_run(c);
+    if (r) return r;
+    const int slot = (int)(c->seq_launched & 1);
+    c->pass[slot].t0 = std::chrono::steady_clock::now();
+    if (c->units.empty()) {
+        ++c->seq_launched;
+        return UP_OK;
+    }
+    if ((r = launch_pass(c, slot))) {
+        (void)hipStreamSynchronize(c->stream);
+        c->seq_done = c->seq_launched;  // drop whatever was in flight
+        return r;
+    }
+    ++c->seq_launched;
+    return UP_OK;
+}
+
+// complete the oldest pass in flight
+int up_run_wait(up_ctx *c, uint64_t *n_regions) {
+    if (!c) return UP_E_ARG;
+    if (!busy(c)) return UP_E_STATE;
+    HIPCHK(hipSetDevice(c->dev));
+    const int slot = (int)(c->seq_done & 1);
+    up_ctx::Pass &ps = c->pass[slot];
     c->ran = false;
     c->nreg = 0;
     c->host_regions = false;
+    c->cur_slot = slot;
     if (c->units.empty()) {
+        ++c->seq_done;
         if (n_regions) *n_regions = 0;
         c->ran = true;
         return UP_OK;
     }
-    if ((r = sync_units(c))) return r;
-    const uint32_t ns = c->nstrips;
-    const int S = c->p.n_samples;
-    HIPCHK(c->d_info.ensure(ns));
-    HIPCHK(c->d_rec.ensure((size_t)ns * kRecStride));
-    HIPCHK(c->d_xlist.ensure((size_t)ns * kXEntry));
-    HIPCHK(c->d_xcount.ensure(1));
-    HIPCHK(c->d_cnt.ensure(ns));
-    HIPCHK(c->d_off.ensure(ns));
-    HIPCHK(c->d_ovf_count.ensure(1));
-    HIPCHK(c->d_nreg.ensure(1));
-    HIPCHK(c->hp_status.ensure(4));
-    size_t tmp = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, c->d_cnt.p, c->d_off.p, (int)ns, c->stream));
-    HIPCHK(c->d_tmp.ensure(tmp + 16));
-#ifdef UPK_DEBUG_COUNTS  // build with -DUPK_DEBUG_COUNTS, run with UNIPEAK_DEBUG_COUNTS=1
-    static const bool dbg = getenv("UNIPEAK_DEBUG_COUNTS") != nullptr;
-#endif
-
-    // One stream-ordered pass K1 -> K2 -> K3 with no host round trip: the
-    // region count stays on the device, the record areas are pre-sized
-    // (reg_cap, ovf_cap) and K3 writes the records straight into mapped
-    // pinned host memory.  An undersized area is detected after the single
-    // sync; it is grown and the pass rerun (first runs only).
+    auto fail = [&](int rc) {
+        (void)hipStreamSynchronize(c->stream);
+        c->seq_done = c->seq_launched;
+        return rc;
+    };
+    if (hipEventSynchronize(ps.done) != hipSuccess) return fail(UP_E_HIP);
     uint64_t nreg = 0;
     for (int attempt = 0;; ++attempt) {
-        if (attempt == 3) return UP_E_INTERNAL;
-        const uint64_t cap = c->reg_cap;
-        HIPCHK(c->d_ovf_rec.ensure((size_t)c->ovf_cap * kOvfStride));
-        HIPCHK(c->d_peak_pos.ensure(cap + 1));
-        HIPCHK(c->d_peak_val.ensure(cap + 1));
-        HIPCHK(c->d_starts.ensure(cap + 1));
-        HIPCHK(c->d_ends.ensure(cap + 1));
-        HIPCHK(c->d_runit.ensure(cap + 1));
-        HIPCHK(c->hp_regions.ensure(cap + 1));
-        HIPCHK(c->hp_counts.ensure((cap + 1) * S));
-        HIPCHK(hipMemsetAsync(c->d_ovf_count.p, 0, sizeof(uint32_t), c->stream));
-        ScanParams SP = scan_params(c);
-#ifdef UPK_DEBUG_COUNTS
-        if (dbg) {
-            HIPCHK(c->d_dbg.ensure(8));
-            HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 8 * sizeof(unsigned long long), c->stream));
-            SP.dbg = c->d_dbg.p;
-        }
-#endif
-        HIPCHK(hipMemsetAsync(c->d_xcount.p, 0, sizeof(uint32_t), c->stream));
-        HIPCHK(hipEventRecord(c->ev[0], c->stream));
-        dispatch_scan<false, kModeScreen>(c, SP, 0, ns);   // K1a: stream + screen
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c->ev[4], c->stream));
-        dispatch_scan<false, kModeExact>(c, SP, 0, ns);    // K1b: exact blocks
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c->ev[1], c->stream));
-        hipLaunchKernelGGL(finalize_kernel, dim3((ns + 255) / 256), dim3(256), 0, c->stream,
-                           c->d_info.p, c->d_cnt.p, ns);
-        HIPCHK(hipGetLastError());
-        size_t tb = c->d_tmp.n;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->d_tmp.p, tb, c->d_cnt.p, c->d_off.p, (int)ns, c->stream));
-        hipLaunchKernelGGL(total_kernel, dim3(1), dim3(1), 0, c->stream, c->d_cnt.p, c->d_off.p, ns,
-                           c->d_ovf_count.p, c->d_nreg.p, c->hp_status.dev,
-                           (unsigned long long *)c->target);
-        hipLaunchKernelGGL(compact_kernel, dim3((ns + 255) / 256), dim3(256), 0, c->stream, c->d_units.p,
-                           (uint32_t)c->units.size(), c->d_info.p, c->d_cnt.p, c->d_off.p, c->d_rec.p,
-                           c->d_ovf_rec.p, c->ovf_cap, c->d_starts.p, c->d_ends.p, c->d_runit.p, c->d_peak_pos.p,
-                           c->d_peak_val.p, ns, (uint64_t)cap);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c->ev[2], c->stream));
-        StatParams P = stat_params(c);
-        P.cap = cap;
-        P.peak_pos = c->d_peak_pos.p;
-        P.peak_val = c->d_peak_val.p;
-        P.out = c->hp_regions.dev;
-        P.out_counts = c->hp_counts.dev;
-        if (c->target) {  // records into the caller's device buffer instead
-            P.cap = std::min<uint64_t>(cap, c->target_cap);
-            P.out = c->target + 8;
-            P.out_counts = (uint32_t *)(c->target + 8 + c->target_cap * sizeof(up_region));
-        }
-        dispatch_stats(c, P, std::max<uint64_t>(c->last_nreg, 1024));
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c->ev[3], c->stream));
-        if ((r = launch_head_detect(c))) return r;
-        HIPCHK(hipStreamSynchronize(c->stream));
-        const unsigned long long *st = c->hp_status.p;
-        if (st[2]) return UP_E_INTERNAL;  // starts and ends disagree
+        if (attempt == 3) return fail(UP_E_INTERNAL);
+        const unsigned long long *st = c->hp_status[slot].p;
+        if (st[2]) return fail(UP_E_INTERNAL);  // starts and ends disagree
         nreg = st[0];
         const uint64_t ovf = st[1];
         bool again = false;
-        if (ovf > c->ovf_cap) { c->ovf_cap = (uint32_t)(ovf + ovf / 2 + 64); again = true; }
-        if (nreg > cap) { c->reg_cap = nreg + nreg / 4 + 1024; again = true; }
-        if (c->target && nreg > c->target_cap) return UP_E_NOMEM;  // caller's buffer too small
+        if (ovf > ps.ovf_cap) { c->ovf_cap = std::max<uint32_t>(c->ovf_cap, (uint32_t)(ovf + ovf / 2 + 64)); again = true; }
+        if (nreg > ps.cap) { c->reg_cap = std::max<uint64_t>(c->reg_cap, nreg + nreg / 4 + 1024); again = true; }
+        if (ps.target && nreg > ps.target_cap) return fail(UP_E_NOMEM);  // caller's buffer too small
 #ifdef UPK_DEBUG_COUNTS
-        if (dbg) {
+        if (getenv("UNIPEAK_DEBUG_COUNTS")) {
             unsigned long long h[8];
             HIPCHK(hipMemcpy(h, c->d_dbg.p, sizeof h, hipMemcpyDeviceToHost));
             fprintf(stderr, "unipeak_hip: K1 strips %u exact blocks %llu live words %llu hits %llu "
-                            "cycles load %llu scatter %llu\n", ns, h[0], h[1], h[2], h[3], h[4]);
+                            "cycles load %llu scatter %llu\n", c->nstrips, h[0], h[1], h[2], h[3], h[4]);
         }
 #endif
         if (!again) break;
+        // rerun this pass alone with grown areas (a later pass in flight
+        // finishes first; its own status tells whether it needs the same)
+        if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(UP_E_HIP);
+        void *keep_t = c->target, *keep_h = c->target_hostp;
+        const uint64_t keep_cap = c->target_cap;
+        c->target = ps.target;
+        c->target_hostp = ps.target_hostp;
+        c->target_cap = ps.target_cap;
+        int r = launch_pass(c, slot);
+        c->target = (uint8_t *)keep_t;
+        c->target_hostp = keep_h;
+        c->target_cap = keep_cap;
+        if (r) return fail(r);
+        if (hipEventSynchronize(ps.done) != hipSuccess) return fail(UP_E_HIP);
     }
     c->nreg = nreg;
     c->last_nreg = nreg;
-    if ((r = replay_head_hits(c))) return r;
+    int r = replay_head_hits(c, slot);
+    if (r) return fail(r);
+    const int tl = c->timing;
     float a = 0, b = 0, d = 0, x = 0;
-    (void)hipEventElapsedTime(&x, c->ev[4], c->ev[1]);
-    c->times[4] = x;  // K1b share of K1
-    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
-    (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
-    (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
-    c->times[0] = a;
+    if (tl >= 1) (void)hipEventElapsedTime(&a, ps.ev[0], ps.ev[1]);
+    if (tl >= 2) {
+        (void)hipEventElapsedTime(&x, ps.ev[1], ps.ev[2]);
+        (void)hipEventElapsedTime(&b, ps.ev[2], ps.ev[3]);
+        (void)hipEventElapsedTime(&d, ps.ev[3], ps.ev[4]);
+    }
+    c->times[0] = (double)a + x;  // K1 = K1a + K1b (K1a alone when only it is timed)
+    c->times[4] = x;              // K1b share of K1
     c->times[1] = b;
     c->times[2] = d;
-    c->times[3] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->times[3] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ps.t0).count();
+    ++c->seq_done;
     c->ran = true;
     if (n_regions) *n_regions = c->nreg;
+    return UP_OK;
+}
+
+int up_run(up_ctx *c, uint64_t *n_regions) {
+    if (!c) return UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;
+    int r = up_run_async(c);
+    if (r) return r;
+    return up_run_wait(c, n_regions);
+}
+
+int up_set_timing(up_ctx *c, int level) {
+    if (!c || level < 0 || level > 2) return UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;
+    c->timing = level;
     return UP_OK;
 }
 
@@ -1033,9 +1184,11 @@ int up_get_regions(up_ctx *c, up_region *out, uint32_t *counts, size_t cap) {
 }
 
 static void drop_target(up_ctx *c) {
+    if (c->target_host && busy(c)) (void)hipStreamSynchronize(c->stream);  // a pass may still write it
     if (c->target_host) (void)hipHostUnregister(c->target_host);
     c->target_host = nullptr;
     c->target = nullptr;
+    c->target_hostp = nullptr;
     c->target_cap = 0;
 }
 
@@ -1061,6 +1214,7 @@ int up_set_record_target(up_ctx *c, void *buf, uint64_t cap) {
         void *dptr = nullptr;
         HIPCHK(hipHostGetDevicePointer(&dptr, buf, 0));
         c->target = (uint8_t *)dptr;
+        c->target_hostp = buf;
     }
     c->target_cap = cap;
     return UP_OK;
@@ -1083,14 +1237,15 @@ int up_regions_view(up_ctx *c, const up_region **regions, const uint32_t **count
         *regions = c->h_regions.data();
         if (counts) *counts = c->h_counts.data();
     } else {
-        *regions = c->hp_regions.p;
-        if (counts) *counts = c->hp_counts.p;
+        *regions = c->hp_regions[c->cur_slot].p;
+        if (counts) *counts = c->hp_counts[c->cur_slot].p;
     }
     return UP_OK;
 }
 
 int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, double *out) {
     if (!c || (n && (!idx || !out))) return UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     if (!c->ran) return UP_E_STATE;
     if (!c->p.nondir) return UP_E_UNSUPPORTED;
     if (n == 0) return UP_OK;
@@ -1163,6 +1318,7 @@ int up_unit_profile_range(up_ctx *c, uint32_t unit, uint64_t first, uint32_t cou
                           double *out_r) {
     int r = check_runnable(c);
     if (r) return r;
+    if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     if (unit >= c->units.size() || !out_f || first < 1 || count == 0) return UP_E_ARG;
     HIPCHK(hipSetDevice(c->dev));
     if ((r = sync_units(c))) return r;

@@ -782,36 +782,99 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
 }
 
 // ------------------------------------------------------------------------
-// K2a: resolve strip-boundary starts/ends, pack (starts, ends) as uint64
+// K2: segmentation in two launches (no library scan, no host round trip).
+// Per-strip (starts, ends) counts are packed into one uint64 (starts in the
+// low, ends in the high half; totals stay < 2^32, so packed sums never carry).
 // ------------------------------------------------------------------------
-__global__ void finalize_kernel(const uint64_t *__restrict__ info, uint64_t *__restrict__ cnt,
-                                uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+constexpr int kSegBlock = 256;
+
+// packed count of strip i: interior runs plus the run that starts at the
+// strip's first position / ends at its last one when the neighbour strip
+// (same unit) does not continue it
+__device__ __forceinline__ uint64_t seg_count(const uint64_t *__restrict__ info, uint32_t i) {
     const uint64_t v = info[i];
     const uint32_t prev_last = si_bit(v, 34) ? 0u : si_bit(info[i - 1], 33);
     const uint32_t next_first = si_bit(v, 35) ? 0u : si_bit(info[i + 1], 32);
     const uint32_t xs = si_bit(v, 32) & (prev_last ^ 1u);
     const uint32_t xe = si_bit(v, 33) & (next_first ^ 1u);
-    cnt[i] = (uint64_t)(si_starts(v) + xs) | ((uint64_t)(si_ends(v) + xe) << 32);
+    return (uint64_t)(si_starts(v) + xs) | ((uint64_t)(si_ends(v) + xe) << 32);
 }
 
-// K2c: compaction of run boundaries into region lists
-__global__ void compact_kernel(const UnitDesc *units, uint32_t nunits,
-                               const uint64_t *__restrict__ info, const uint64_t *__restrict__ cnt,
-                               const uint64_t *__restrict__ off, const uint32_t *__restrict__ rec,
-                               const uint32_t *__restrict__ ovf_rec, uint32_t ovf_cap,
-                               uint32_t *__restrict__ starts, uint32_t *__restrict__ ends,
-                               uint32_t *__restrict__ reg_unit, uint32_t *__restrict__ peak_pos,
-                               double *__restrict__ peak_val, uint32_t n, uint64_t cap) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t c = cnt[i];
+__device__ __forceinline__ uint64_t block_sum_u64(uint64_t v, uint64_t *red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((long long)v, o);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+
+// K2a: per-strip counts and one packed total per 256 strips
+__global__ void __launch_bounds__(kSegBlock) seg_count_kernel(const uint64_t *__restrict__ info,
+                                                              uint64_t *__restrict__ cnt,
+                                                              uint64_t *__restrict__ bsum, uint32_t n) {
+    __shared__ uint64_t red[4];
+    const uint32_t i = blockIdx.x * kSegBlock + threadIdx.x;
+    uint64_t c = 0;
+    if (i < n) {
+        c = seg_count(info, i);
+        cnt[i] = c;
+    }
+    const uint64_t t = block_sum_u64(c, red);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = t;
+}
+
+// K2b: each block adds up the totals of the blocks before it, scans its own
+// 256 counts and compacts its run boundaries into the region lists; the last
+// block publishes the region count (status[0] = regions, status[1] = spilled
+// strips, status[2] = start/end mismatch) and re-arms the pass counters
+__global__ void __launch_bounds__(kSegBlock) seg_compact_kernel(
+    const UnitDesc *units, uint32_t nunits, const uint64_t *__restrict__ info,
+    const uint64_t *__restrict__ cnt, const uint64_t *__restrict__ bsum, const uint32_t *__restrict__ rec,
+    const uint32_t *__restrict__ ovf_rec, uint32_t ovf_cap, uint32_t *__restrict__ starts,
+    uint32_t *__restrict__ ends, uint32_t *__restrict__ reg_unit, uint32_t *__restrict__ peak_pos,
+    double *__restrict__ peak_val, uint32_t n, uint64_t cap, uint32_t *ovf_count, uint32_t *xcount,
+    uint64_t *nreg, unsigned long long *status, unsigned long long *target_hdr) {
+    __shared__ uint64_t red[4];
+    __shared__ uint64_t wsum[4];
+    uint64_t part = 0;
+    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += kSegBlock) part += bsum[j];
+    const uint64_t base = block_sum_u64(part, red);
+    const uint32_t i = blockIdx.x * kSegBlock + threadIdx.x;
+    const uint64_t c = i < n ? cnt[i] : 0;
+    // block exclusive scan: wave inclusive scan, then the waves before
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = (uint64_t)__shfl_up((long long)inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint64_t before = 0;
+    for (int k = 0; k < w; ++k) before += wsum[k];
+    const uint64_t o = base + before + inc - c;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kSegBlock - 1) {
+        const uint64_t t = o + c;
+        const uint64_t nst = t & 0xFFFFFFFFull, nen = t >> 32;
+        const uint32_t ovf = *ovf_count;
+        // a pass whose record areas overflowed left gaps in the region lists:
+        // K3 must see no region at all (the host grows the areas and reruns)
+        const bool valid = nst <= cap && nst == nen && ovf <= ovf_cap;
+        *nreg = valid ? nst : 0;
+        status[0] = nst;
+        status[1] = ovf;
+        status[2] = nst != nen;
+        if (target_hdr) *target_hdr = valid ? nst : 0;  // caller's record buffer (up_set_record_target)
+        *ovf_count = 0u;                    // K1b has consumed the work list
+        *xcount = 0u;
+    }
     if (c == 0) return;
     const uint64_t v = info[i];
     const uint32_t ns = (uint32_t)c, ne = (uint32_t)(c >> 32);
     const uint32_t xs = ns - si_starts(v), xe = ne - si_ends(v);
-    const uint64_t o = off[i];
     uint32_t os = (uint32_t)o, oe = (uint32_t)(o >> 32);
     const uint32_t u = find_unit(units, nunits, i);
     const int64_t p0 = 1 + (int64_t)(i - units[u].strip0) * kStrip;
@@ -1184,20 +1247,6 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             ((uint64_t *)P.out)[ri * 7 + lane] = w;
         }
     }
-}
-
-// K2b': region count from the scan, on the device (no host round trip):
-// status[0] = regions, status[1] = spilled strips, status[2] = start/end mismatch
-__global__ void total_kernel(const uint64_t *cnt, const uint64_t *off, uint32_t ns,
-                             const uint32_t *ovf_count, uint64_t *nreg, unsigned long long *status,
-                             unsigned long long *target_hdr) {
-    const uint64_t t = cnt[ns - 1] + off[ns - 1];
-    const uint64_t nst = t & 0xFFFFFFFFull, nen = t >> 32;
-    *nreg = nst;
-    status[0] = nst;
-    status[1] = *ovf_count;
-    status[2] = nst != nen;
-    if (target_hdr) *target_hdr = nst;  // caller's device record buffer (up_set_record_target)
 }
 
 // ------------------------------------------------------------------------

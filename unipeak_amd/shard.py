@@ -231,23 +231,24 @@ class NodeRecords:
     """Node-shared pinned host segment that every rank's K3 writes its
     records into (up_set_record_target with a host pointer): on one node the
     records reach rank 0 without a gather collective or a device-to-host copy
-    on rank 0 -- each GPU writes its own slot over its own PCIe link.  Two
-    slots per rank (step parity) let rank 0 read step i-1 while step i runs;
-    the collective at the start of each step orders the writes.  Slot layout
-    = the record target layout of include/unipeak_hip.h."""
+    on rank 0 -- each GPU writes its own slot over its own PCIe link.  Slots
+    rotate with the step number (``nslots`` per rank), so rank 0 reads step i
+    while later steps run; the collective at the start of each step orders the
+    writes.  Slot layout = the record target layout of include/unipeak_hip.h."""
 
-    def __init__(self, comm, cap, n_samples, rec_bytes, tag):
+    def __init__(self, comm, cap, n_samples, rec_bytes, tag, nslots=2):
         from multiprocessing import resource_tracker, shared_memory
         self.comm, self.cap, self.S, self.rb = comm, cap, n_samples, rec_bytes
+        self.nslots = nslots
         slot = 8 + cap * (rec_bytes + 4 * n_samples)
         self.slot = (slot + 4095) // 4096 * 4096
         self.world = comm.world if comm is not None else 1
         if comm is None:  # one process: plain page-aligned host memory, no segment
             self.shm = None
             self.owner = True
-            self._mem = np.zeros(2 * self.slot + 4096, np.uint8)
+            self._mem = np.zeros(nslots * self.slot + 4096, np.uint8)
             off = (-self._mem.ctypes.data) % 4096
-            self.raw = self._mem[off:off + 2 * self.slot]
+            self.raw = self._mem[off:off + nslots * self.slot]
             self.mine = self.raw
             return
         name = f"unipeak_{tag}"
@@ -259,28 +260,28 @@ class NodeRecords:
                 old.unlink()
             except FileNotFoundError:
                 pass
-            self.shm = shared_memory.SharedMemory(name=name, create=True, size=2 * self.slot * comm.world)
+            self.shm = shared_memory.SharedMemory(name=name, create=True, size=nslots * self.slot * comm.world)
         comm.dist.barrier()
         if not self.owner:
             self.shm = shared_memory.SharedMemory(name=name)
             # attachers must not unlink it at exit (Python's resource tracker would)
             resource_tracker.unregister(self.shm._name, "shared_memory")
         self.raw = np.frombuffer(self.shm.buf, np.uint8)
-        self.mine = self.raw[2 * comm.rank * self.slot:2 * (comm.rank + 1) * self.slot]
+        self.mine = self.raw[nslots * comm.rank * self.slot:nslots * (comm.rank + 1) * self.slot]
 
     def my_range(self):
-        """(address, bytes) of this rank's two slots (register them once)"""
-        return self.mine.ctypes.data, 2 * self.slot
+        """(address, bytes) of this rank's slots (register them once)"""
+        return self.mine.ctypes.data, self.nslots * self.slot
 
-    def my_slot_address(self, parity=0):
-        return self.mine.ctypes.data + (parity & 1) * self.slot
+    def my_slot_address(self, step=0):
+        return self.mine.ctypes.data + (step % self.nslots) * self.slot
 
-    def read(self, dtype, parity=0):
-        """rank 0, once every rank's step of this parity is done:
-        [(records view, counts view)] per rank"""
+    def read(self, dtype, step=0):
+        """rank 0, once every rank finished `step`: [(records view, counts
+        view)] per rank"""
         out = []
         for w in range(self.world):
-            base = (2 * w + (parity & 1)) * self.slot
+            base = (self.nslots * w + step % self.nslots) * self.slot
             n = int(self.raw[base:base + 8].view(np.uint64)[0])
             if n > self.cap:
                 raise RuntimeError(f"rank {w} produced {n} records, the slot holds {self.cap}")
