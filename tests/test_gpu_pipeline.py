@@ -136,3 +136,4 @@ def test_many_units_many_blocks(gpu_lib, oracle):
             assert np.array_equal(ref[k], regs[m][k]), (u, k)
         assert np.array_equal(ref_sums, gcnt[m])
         assert ref["peak_score"].tobytes() == regs[m]["peak_score"].tobytes()
+
