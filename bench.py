@@ -208,6 +208,7 @@ def main():
         comm.torch.cuda.synchronize()
         g.set_record_target(rbuf.data_ptr(), cap)
     it = [0]           # steps launched
+    ar = [None]        # the next step's background all-reduce, in flight
     reads = []         # rank 0: (step, future) of record reads in flight
     done_times = []    # per completed pass: library timings
 
@@ -254,7 +255,14 @@ def main():
         # passes this step's collective and launches into it
         while reads and reads[0][0] <= i - 4:
             reads.pop(0)[1].result()
-        set_background(comm.global_tags(local_tags) if comm else local_tags)
+        if comm is not None:
+            # this step's all-reduce was started one step ahead (RCCL gets the
+            # device between the previous pass's kernels); start the next one
+            tags = comm.global_tags_finish(ar[0] if ar[0] is not None else comm.global_tags_start(local_tags))
+            ar[0] = comm.global_tags_start(local_tags)
+        else:
+            tags = local_tags
+        set_background(tags)
         t1 = time.perf_counter()
         # every rank has completed pass i-2 (it waited for it before entering
         # this collective): rank 0 reads it while passes i-1 and i run
@@ -278,6 +286,9 @@ def main():
         while it[0] > len(done_times):
             g.run_wait()
             done_times.append(g.timings())
+        if ar[0] is not None:  # the all-reduce started for a step that will not run
+            comm.global_tags_finish(ar[0])
+            ar[0] = None
         if not pipelined:
             return None
         if comm is not None:

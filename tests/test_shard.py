@@ -267,3 +267,29 @@ def test_node_records_world2(tmp_path):
     mp.spawn(_node_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     assert (tmp_path / "result").read_text() == "ok"
     assert not os.path.exists(f"/dev/shm/unipeak_test_{port}")
+
+
+def _async_tags_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = shard.Comm(dist, rank, world, "cpu")
+    # bench.py's order: the all-reduce of step i+1 is started before step i's
+    # result is used, every rank issuing the same sequence
+    pending = comm.global_tags_start(10 * (rank + 1))
+    got = []
+    for step in range(4):
+        v = comm.global_tags_finish(pending)
+        pending = comm.global_tags_start(10 * (rank + 1) + step + 1)
+        got.append(v)
+    got.append(comm.global_tags_finish(pending))
+    np.save(os.path.join(out_dir, f"t{rank}.npy"), np.array(got))
+    dist.destroy_process_group()
+
+
+def test_gloo_background_allreduce_one_step_ahead(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_async_tags_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        got = np.load(tmp_path / f"t{r}.npy")
+        assert got.tolist() == [30, 32, 34, 36, 38]

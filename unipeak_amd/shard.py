@@ -121,12 +121,45 @@ class Comm:
         self.device = device
 
     def global_tags(self, local_tags: int) -> int:
-        """The single data-path collective of the scan (regions.cpp:205-213)."""
+        """The single data-path collective of the scan (regions.cpp:205-213).
+        On GPUs it runs on a stream of its own, so neither it nor the host
+        read-back is ordered behind a pass running on the library's stream."""
+        torch = self.torch
         if getattr(self, "_tags", None) is None:
-            self._tags = self.torch.zeros(1, dtype=self.torch.int64, device=self.device)
-        self._tags.fill_(int(local_tags))
-        self.dist.all_reduce(self._tags)
-        return int(self._tags.item())
+            self._tags = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._side = torch.cuda.Stream(device=self.device) if self.device != "cpu" else None
+        if self._side is None:
+            self._tags.fill_(int(local_tags))
+            self.dist.all_reduce(self._tags)
+            return int(self._tags.item())
+        with torch.cuda.stream(self._side):
+            self._tags.fill_(int(local_tags))
+            self.dist.all_reduce(self._tags)
+            v = int(self._tags.item())
+        return v
+
+    def global_tags_start(self, local_tags: int):
+        """Start the same all-reduce without waiting for it (one step ahead):
+        its RCCL kernel runs whenever the device has room -- a pass holds
+        every CU while it streams -- and global_tags_finish() collects it."""
+        torch = self.torch
+        if self.device == "cpu":
+            t = torch.tensor([int(local_tags)], dtype=torch.int64)
+            return (self.dist.all_reduce(t, async_op=True), t)
+        if getattr(self, "_side", None) is None:
+            self._tags = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._side = torch.cuda.Stream(device=self.device)
+        with torch.cuda.stream(self._side):
+            t = torch.full((1,), int(local_tags), dtype=torch.int64, device=self.device)
+            return (self.dist.all_reduce(t, async_op=True), t)
+
+    def global_tags_finish(self, handle) -> int:
+        work, t = handle
+        work.wait()
+        if self.device == "cpu":
+            return int(t.item())
+        with self.torch.cuda.stream(self._side):
+            return int(t.item())
 
     def max_over_ranks(self, x: float) -> float:
         t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=self.device)
