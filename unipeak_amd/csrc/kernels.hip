@@ -1001,7 +1001,47 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
         // correlation is wanted, no score is needed here -- only the counts
         const bool known = P.peak_pos != nullptr && P.peak_pos[ri] != 0 && !(NONDIR && P.want_corr);
         int blk = 0;
-        if (known) {
+        bool counted = false;
+        if constexpr (POOL == 0) {
+            // one pooled sample: the region's count bytes (<= kStatCache
+            // words) are fetched with all loads in flight at once, then
+            // scored; escapes resolved at use
+            const int nw = (int)((right - left) / 64u) + 1;
+            if (known && S == 1 && nw <= kStatCache) {
+                best = P.peak_val[ri];
+                best_x = P.peak_pos[ri];
+                gu8 *t0 = track_u8(U, S, 0, P.nc[0]) + kPad + (int64_t)left - 1 + lane;
+                uint32_t r0[kStatCache], r1[NONDIR ? kStatCache : 1];
+#pragma unroll
+                for (int w = 0; w < kStatCache; ++w) r0[w] = w < nw ? t0[64 * w] : 0u;
+                if constexpr (NONDIR) {
+                    gu8 *t1 = track_u8(U, S, 1, P.nc[0]) + kPad + (int64_t)left - 1 + lane;
+#pragma unroll
+                    for (int w = 0; w < kStatCache; ++w) r1[w] = w < nw ? t1[64 * w] : 0u;
+                }
+#pragma unroll
+                for (int w = 0; w < kStatCache; ++w) {
+                    if (w >= nw) break;
+                    const int64_t x = (int64_t)left + 64 * w + lane;
+                    const bool valid = x <= (int64_t)right;
+                    uint32_t c0 = r0[w];
+                    if (c0 == kEsc) c0 = ovf_lookup(U, (uint32_t)P.nc[0], (uint32_t)x);
+                    uint32_t pc = valid ? c0 : 0u;
+                    if constexpr (NONDIR) {
+                        uint32_t c1 = r1[w];
+                        if (c1 == kEsc) c1 = ovf_lookup(U, (uint32_t)(S + P.nc[0]), (uint32_t)x);
+                        pc += valid ? c1 : 0u;
+                    }
+                    esum1 += pc;
+                    pcache[64 * w + lane] = pc;
+                    cnt_acc += pc;
+                    sum_acc += pc * (uint32_t)(uint16_t)(x - left);
+                }
+                blk = nw;
+                counted = true;
+            }
+        }
+        if (known && !counted) {
             best = P.peak_val[ri];
             best_x = P.peak_pos[ri];
             for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64, ++blk) {
@@ -1177,15 +1217,17 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
                     if (h1) pc += count_at(U, S, 1, s, x);
                 }
             }
+            // every lane forms its own terms; only the two sums stay
+            // sequential, in position order (data.cpp:166-177)
+            const double d = (double)(uint16_t)(x - left) - x_bar;
+            const double d2 = d * d;
+            const double t2 = (double)pc * d2, t4 = (double)pc * (d2 * d2);
             uint64_t m = __ballot(pc != 0u);  // positions holding a stored hit vector
             while (m) {
                 const int l = __builtin_ctzll(m);
                 m &= m - 1;
-                const uint32_t q = rl_u(pc, l);
-                const double d = (double)(uint16_t)(x0 + l - left) - x_bar;
-                const double d2 = d * d;
-                sum2 = sum2 + (double)q * d2;
-                sum4 = sum4 + (double)q * (d2 * d2);
+                sum2 = sum2 + rl_d(t2, l);
+                sum4 = sum4 + rl_d(t4, l);
             }
         }
         const double kurt = ((double)count - 1) * sum4 / (sum2 * sum2);
