@@ -138,7 +138,12 @@ int up_unit_set_last_add(up_ctx *ctx, uint32_t unit, uint32_t last_add);
 int up_unit_last_add(up_ctx *ctx, uint32_t unit, uint32_t *last_add);
 int up_reset_units(up_ctx *ctx);
 
-/* Run K1..K3 over every unit (stream-ordered, blocking). */
+/* Run K1..K3 over every unit (stream-ordered, blocking).  Configurations
+ * the parallel scan does not represent -- region threshold <= 0 (the leap
+ * branch of processPosition is live, quirk Q11) or bw > 127 -- run the exact
+ * state machine over every unit instead (K0 replay, sequential per buffer:
+ * exact, slow); up_run_async, up_unit_profile* and up_shift_scan refuse them
+ * (UP_E_UNSUPPORTED). */
 int up_run(up_ctx *ctx, uint64_t *n_regions);
 /* Pipelined form of up_run: up_run_async enqueues one pass and returns
  * (at most two passes in flight); up_run_wait completes the OLDEST pass in

@@ -84,6 +84,13 @@ REGION_CASES = [
     ("nondir_corr", HG_LIKE, 1, ["-D", "-y", "-f", "-s", "60"], {"shift_rev": 120}),
     ("nondir_two_samples", HG_LIKE, 2, ["-D", "-y", "-u", "0.5"], {"shift_rev": 100}),
     ("mappable_override", HG_LIKE, 1, ["-f", "-m", "3095693983"], {}),
+    # outside the parallel scan: exact replay of every unit (K0)
+    ("replay_threshold_zero_q11", HG_LIKE, 1, ["-f", "-r", "0"], {}),
+    ("replay_negative_threshold", HG_LIKE, 2, ["-r", "-2", "-k", "0"], {}),
+    ("replay_bandwidth_200", HG_LIKE, 1, ["-f", "-b", "200"], {}),
+    ("replay_bandwidth_600_nondir", HG_LIKE, 1, ["-D", "-y", "-f", "-b", "600", "-u", "-1", "-r", "4",
+                                                         "-k", "0"],
+     {"shift_rev": 100}),
 ]
 
 
@@ -263,6 +270,9 @@ Q1_CASES = [
     ("dir_bw100_coeffs", 100, 3, ["-e", "3", "-z", "0.5,2", "-k", "0"], ("c1",)),
     ("nondir_bw50_corr", 50, 1, ["-D", "-y", "-f", "-k", "0"], ("c2",)),
     ("nondir_bw90_two", 90, 2, ["-D", "-f", "-k", "0"], ("c1", "c2")),
+    # outside the parallel scan: the whole-buffer replay carries the leaks too
+    ("replay_dir_bw200_leak", 200, 1, ["-f", "-k", "0"], ("c1",)),
+    ("replay_dir_r0_leak", 50, 1, ["-f", "-k", "0", "-r", "0"], ("c3",)),
 ]
 
 

@@ -1,0 +1,113 @@
+"""Configurations outside the parallel scan run the exact state machine on
+the GPU over every unit (K0 replay, unipeak_amd/csrc/emulate.hip):
+
+* region threshold <= 0 -- processPosition's leap branch is live (quirk Q11:
+  the leap position joins the region without setting its left end,
+  misc/peakcall.cpp:76-78), so regions are not maximal runs of flags;
+* kernel bandwidth > 127 -- wider than the scan's register-resident halo;
+  windows up to 64 KiB live in LDS, wider ones in global scratch.
+
+Every candidate region (accepted and rejected), peak, counts and FP64 peak
+score bit-exact against the oracle; kurtosis/correlation within 1e-12."""
+import numpy as np
+import pytest
+
+from tests.gen import random_unit
+
+pytestmark = pytest.mark.gpu
+
+
+def close(a, b, rel=1e-12):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    ok = (np.isnan(a) & np.isnan(b)) | (a == b) | (np.abs(a - b) <= rel * np.maximum(np.abs(a), np.abs(b)))
+    return bool(np.all(ok))
+
+
+def run_units(capi, bw, bg, units, *, nondir=False, **kw):
+    """units: [(length, pos, cf, cr)] of one buffer -> records + counts"""
+    S = units[0][2].shape[1]
+    with capi.Lib(0) as g:
+        g.set_params(bw, S, bg, nondir=nondir, **kw)
+        for length, pos, cf, cr in units:
+            u = g.add_unit(length)
+            for st, c in enumerate([cf] if not nondir else [cf, cr]):
+                for s in range(S):
+                    m = c[:, s] != 0
+                    if m.any():
+                        g.scatter(u, st, s, pos[m], c[m, s])
+        n = g.run()
+        return g.regions(n)
+
+
+def compare(ref, ref_sums, regs, cnt, corr=False):
+    assert len(ref) == len(regs), (len(ref), len(regs))
+    for k in ("left", "right", "peak", "sum", "accepted"):
+        assert np.array_equal(ref[k], regs[k]), k
+    assert np.array_equal(ref_sums, cnt)
+    assert ref["peak_score"].tobytes() == regs["peak_score"].tobytes()
+    assert close(ref["kurtosis"], regs["kurtosis"])
+    if corr:
+        assert close(ref["corr"], regs["corr"])
+
+
+@pytest.mark.parametrize("thr", [0.0, -1.0, -1e-300])
+@pytest.mark.parametrize("seed", range(3))
+def test_threshold_le_zero_q11(gpu_lib, oracle, thr, seed):
+    rng = np.random.default_rng(700 + seed)
+    length, bw, bg = 60_000, 50, 0.003
+    pos, cnt = random_unit(rng, length, bw)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, region_thr=thr)
+    regs, gcnt = run_units(gpu_lib, bw, bg, [(length, pos, cnt, None)], region_thr=thr)
+    assert len(ref) > 3
+    compare(ref, ref_sums, regs, gcnt)
+
+
+@pytest.mark.parametrize("bw", [128, 150, 300, 1000, 2500])
+def test_wide_bandwidth(gpu_lib, oracle, bw):
+    rng = np.random.default_rng(bw)
+    length, bg = 400_000, 0.002
+    pos, cnt = random_unit(rng, length, bw, n_clusters=40)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt)
+    regs, gcnt = run_units(gpu_lib, bw, bg, [(length, pos, cnt, None)])
+    assert len(ref) > 0
+    compare(ref, ref_sums, regs, gcnt)
+
+
+def test_wide_bandwidth_nondirectional_corr(gpu_lib, oracle):
+    rng = np.random.default_rng(77)
+    length, bw, bg = 200_000, 200, 0.004
+    pos_f, cnt_f = random_unit(rng, length, bw)
+    pos_r, cnt_r = random_unit(rng, length, bw)
+    allp = np.union1d(pos_f, pos_r).astype(np.uint32)
+    cf = np.zeros((allp.size, 1), np.uint32)
+    cr = np.zeros((allp.size, 1), np.uint32)
+    cf[np.searchsorted(allp, pos_f)] = cnt_f
+    cr[np.searchsorted(allp, pos_r)] = cnt_r
+    ref, ref_sums = oracle.run_unit(bw, bg, allp, cf, cr, nondir=True, corr_thr=0.3)
+    regs, gcnt = run_units(gpu_lib, bw, bg, [(length, allp, cf, cr)], nondir=True, corr_thr=0.3,
+                           want_corr=True)
+    compare(ref, ref_sums, regs, gcnt, corr=True)
+
+
+def test_replay_multi_sample_control_and_coeffs(gpu_lib, oracle):
+    rng = np.random.default_rng(78)
+    length, bw, bg, S = 150_000, 180, 0.004, 3
+    pos, cnt = random_unit(rng, length, bw, S=S)
+    control = [0, 1, 0]
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, control=control, coeffs=[0.6, 1.7])
+    regs, gcnt = run_units(gpu_lib, bw, bg, [(length, pos, cnt, None)], control=control,
+                           coeffs=[0.6, 1.7])
+    compare(ref, ref_sums, regs, gcnt)
+
+
+def test_replay_refuses_pipelined_and_profile(gpu_lib):
+    capi = gpu_lib
+    with capi.Lib(0) as g:
+        g.set_params(200, 1, 0.003)
+        u = g.add_unit(10_000)
+        g.scatter(u, 0, 0, np.array([5000], np.uint32), np.array([3], np.uint32))
+        assert g.run() >= 0
+        with pytest.raises(capi.UpError):
+            g.run_async()  # replay configurations run blocking only
+        with pytest.raises(capi.UpError):
+            g.profile(u, 10_000)

@@ -143,6 +143,10 @@ struct up_ctx {
     DevBuf<int32_t> d_unit_buffer;
     DevBuf<double> d_reg_f, d_reg_r;
     DevBuf<up_region> d_emu_out;
+    DevBuf<double> d_ring_f, d_ring_r;   // K0 window in global memory (very wide kernels)
+    DevBuf<uint8_t> d_ring_has;
+    uint32_t emu_reg_cap = 1u << 18;     // K0: positions of one open region
+    uint32_t emu_out_cap = 1u << 16;     // K0: region records
     bool host_regions = false;  // merged list lives on the host
     std::vector<up_region> h_regions;
     std::vector<uint32_t> h_counts;
@@ -270,6 +274,7 @@ void up_close(up_ctx *c) {
     c->d_head.release(); c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
+    c->d_ring_f.release(); c->d_ring_r.release(); c->d_ring_has.release();
     for (int k = 0; k < 2; ++k) {
         c->hp_regions[k].release(); c->hp_counts[k].release(); c->hp_status[k].release(); c->hp_head[k].release();
         for (auto &e : c->pass[k].ev) (void)hipEventDestroy(e);
@@ -632,7 +637,8 @@ static int sync_units(up_ctx *c) {
     uint32_t strip = 0;
     for (size_t i = 0; i < c->units.size(); ++i) {
         Unit &u = c->units[i];
-        const uint64_t dom = (uint64_t)u.len + c->p.bw;
+        // strips only serve the parallel scan (bw <= kMaxBw; wider kernels replay)
+        const uint64_t dom = (uint64_t)u.len + std::min<int>(c->p.bw, kMaxBw);
         u.nstrips = (uint32_t)((dom + kStrip - 1) / kStrip);
         u.strip0 = strip;
         strip += u.nstrips;
@@ -774,13 +780,24 @@ static void dispatch_stats(up_ctx *c, const StatParams &P, uint64_t nreg) {
 #undef UPK_ST
 }
 
-static int check_runnable(up_ctx *c) {
+// Configurations the parallel scan does not represent run through the
+// exact state machine over every unit (K0 replay, emulate.hip): a threshold
+// <= 0 makes the leap branch of processPosition live (quirk Q11, the leap
+// position joins a region without setting its left end), and kernels wider
+// than kMaxBw exceed the scan's register-resident halo.
+static bool replay_mode(const up_ctx *c) { return c->p.bw > kMaxBw || !(c->p.region_thr > 0); }
+
+static int check_params(up_ctx *c) {
     if (!c || !c->have_params) return UP_E_STATE;
-    if (c->p.bw < 1 || c->p.bw > kMaxBw) return UP_E_UNSUPPORTED;
+    if (c->p.bw < 1) return UP_E_ARG;
     if (c->p.n_samples > 256) return UP_E_UNSUPPORTED;
-    // thresholds <= 0 make the leap path of processPosition (Q11) live
-    if (!(c->p.region_thr > 0)) return UP_E_UNSUPPORTED;
     return UP_OK;
+}
+
+static int check_runnable(up_ctx *c) {  // the parallel scan
+    int r = check_params(c);
+    if (r) return r;
+    return replay_mode(c) ? UP_E_UNSUPPORTED : UP_OK;
 }
 
 // Quirk Q1: units whose pooled hits include a position <= bw are replayed
@@ -802,6 +819,139 @@ static int launch_head_detect(up_ctx *c, int slot) {
     return UP_OK;
 }
 
+// K0: run the exact state machine (emulate.hip) over the units flagged in
+// d_head (replay_all: over every unit, never resynced) -> its regions, their
+// exptSums and the per-unit resync positions.  Capacity of the region
+// record area and of one open region grow until the replay fits.
+static int emulate_units(up_ctx *c, bool replay_all, std::vector<up_region> &emu, std::vector<uint32_t> &ecnt,
+                         std::vector<uint32_t> &resync) {
+    const uint32_t nu = (uint32_t)c->units.size();
+    const int S = c->p.n_samples;
+    const uint32_t W = 2u * c->p.bw + 1;
+    std::vector<int32_t> ub(nu);
+    for (uint32_t i = 0; i < nu; ++i) ub[i] = c->units[i].buffer;
+    HIPCHK(c->d_unit_buffer.ensure(nu));
+    HIPCHK(hipMemcpy(c->d_unit_buffer.p, ub.data(), nu * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(c->d_resync.ensure(nu));
+    HIPCHK(c->d_emu_n.ensure(1));
+    HIPCHK(c->d_emu_err.ensure(1));
+    HIPCHK(c->d_ring_hits.ensure(2ull * W * S));
+    // the window in LDS when it fits (64 KiB), else in global scratch
+    const size_t ring_bytes = (size_t)W * (2 * sizeof(double) + 1);
+    const bool ring_lds = ring_bytes <= 65536 - 64;
+    if (!ring_lds) {
+        HIPCHK(c->d_ring_f.ensure(2ull * W));
+        HIPCHK(c->d_ring_r.ensure(2ull * W));
+        HIPCHK(c->d_ring_has.ensure(2ull * W));
+    }
+    for (int attempt = 0;; ++attempt) {
+        if (attempt == 6) return UP_E_NOMEM;
+        const uint32_t reg_cap = c->emu_reg_cap, out_cap = c->emu_out_cap;
+        HIPCHK(hipMemsetAsync(c->d_resync.p, 0, nu * sizeof(uint32_t), c->stream));
+        HIPCHK(hipMemsetAsync(c->d_emu_n.p, 0, 4, c->stream));
+        HIPCHK(hipMemsetAsync(c->d_emu_err.p, 0, 4, c->stream));
+        if (!ring_lds) {
+            HIPCHK(hipMemsetAsync(c->d_ring_f.p, 0, 2ull * W * sizeof(double), c->stream));
+            HIPCHK(hipMemsetAsync(c->d_ring_r.p, 0, 2ull * W * sizeof(double), c->stream));
+            HIPCHK(hipMemsetAsync(c->d_ring_has.p, 0, 2ull * W, c->stream));
+        }
+        HIPCHK(c->d_emu_out.ensure(out_cap));
+        HIPCHK(c->d_emu_counts.ensure((size_t)out_cap * S));
+        HIPCHK(c->d_reg_f.ensure(2ull * reg_cap));
+        HIPCHK(c->d_reg_r.ensure(2ull * reg_cap));
+        HIPCHK(c->d_reg_hit.ensure(2ull * reg_cap));
+        HIPCHK(c->d_reg_hits.ensure(2ull * reg_cap * S));
+        EmuParams E{};
+        E.units = c->d_units.p;
+        E.nunits = nu;
+        E.unit_buffer = c->d_unit_buffer.p;
+        E.unit_head = c->d_head.p;
+        E.S = S;
+        E.nnc = (int32_t)c->nc.size();
+        E.nc = c->d_nc.p;
+        E.is_control = c->d_ctl.p;
+        E.coef = c->d_coef.p;
+        E.ncoef = (int32_t)c->coef.size();
+        E.kern = c->d_kern.p;
+        E.bw = c->p.bw;
+        E.nondir = c->p.nondir;
+        E.region_thr = c->p.region_thr;
+        E.kurt_thr = c->p.kurt_thr;
+        E.corr_thr = c->p.corr_thr;
+        E.hit_thr = c->p.hit_thr;
+        E.want_corr = c->p.want_corr || c->p.corr_thr > -1;
+        E.resync = c->d_resync.p;
+        E.out = c->d_emu_out.p;
+        E.out_counts = c->d_emu_counts.p;
+        E.nout = c->d_emu_n.p;
+        E.out_cap = out_cap;
+        E.ring_hits = c->d_ring_hits.p;
+        E.reg_f = c->d_reg_f.p;
+        E.reg_r = c->d_reg_r.p;
+        E.reg_hit = c->d_reg_hit.p;
+        E.reg_hits = c->d_reg_hits.p;
+        E.reg_cap = reg_cap;
+        E.err = c->d_emu_err.p;
+        E.replay_all = replay_all ? 1 : 0;
+        E.ring_lds = ring_lds ? 1 : 0;
+        E.ring_f = c->d_ring_f.p;
+        E.ring_r = c->d_ring_r.p;
+        E.ring_has = c->d_ring_has.p;
+        hipLaunchKernelGGL(emulate_kernel, dim3(2), dim3(64), ring_lds ? ring_bytes : 0, c->stream, E);
+        HIPCHK(hipGetLastError());
+        uint32_t nemu = 0, err = 0;
+        resync.assign(nu, 0);
+        HIPCHK(hipMemcpyAsync(&nemu, c->d_emu_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(&err, c->d_emu_err.p, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(resync.data(), c->d_resync.p, nu * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (err & 4u) {
+            fprintf(stderr, "unipeak_hip: exact replay: positions out of order\n");
+            return UP_E_ARG;
+        }
+        if (err & 3u) {  // 1: a region longer than reg_cap positions, 2: more than out_cap regions
+            if (err & 1u) c->emu_reg_cap *= 4;
+            if (err & 2u) c->emu_out_cap = std::max<uint32_t>(c->emu_out_cap * 4, nemu + nemu / 4);
+            continue;
+        }
+        emu.resize(nemu);
+        ecnt.resize((size_t)nemu * S);
+        if (nemu) {
+            HIPCHK(hipMemcpy(emu.data(), c->d_emu_out.p, nemu * sizeof(up_region), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(ecnt.data(), c->d_emu_counts.p, ecnt.size() * 4, hipMemcpyDeviceToHost));
+        }
+        return UP_OK;
+    }
+}
+
+// regions -> the host list (unit-major, emission order within a unit) and,
+// if set, the caller's record target
+static int publish_host_regions(up_ctx *c, const up_ctx::Pass &ps) {
+    c->host_regions = true;
+    c->nreg = c->h_regions.size();
+    if (ps.target) {  // keep the caller's buffer authoritative
+        if (c->nreg > ps.target_cap) return UP_E_NOMEM;
+        const uint64_t hdr = c->nreg;
+        const size_t cb = c->h_counts.size() * sizeof(uint32_t);
+        if (ps.target_hostp) {
+            uint8_t *h = (uint8_t *)ps.target_hostp;
+            std::memcpy(h, &hdr, 8);
+            if (c->nreg) {
+                std::memcpy(h + 8, c->h_regions.data(), c->nreg * sizeof(up_region));
+                std::memcpy(h + 8 + ps.target_cap * sizeof(up_region), c->h_counts.data(), cb);
+            }
+        } else {
+            HIPCHK(hipMemcpy(ps.target, &hdr, 8, hipMemcpyHostToDevice));
+            if (c->nreg) {
+                HIPCHK(hipMemcpy(ps.target + 8, c->h_regions.data(), c->nreg * sizeof(up_region), hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(ps.target + 8 + ps.target_cap * sizeof(up_region), c->h_counts.data(), cb,
+                                 hipMemcpyHostToDevice));
+            }
+        }
+    }
+    return UP_OK;
+}
+
 // after the pass of `slot` completed (stream idle)
 static int replay_head_hits(up_ctx *c, int slot) {
     c->host_regions = false;
@@ -813,76 +963,12 @@ static int replay_head_hits(up_ctx *c, int slot) {
     // the head flags are a function of the (unchanged) tracks, so d_head of
     // a later pass still describes this one
     HIPCHK(hipStreamSynchronize(c->stream));
-
     const int S = c->p.n_samples;
-    const uint32_t W = 2u * c->p.bw + 1;
-    const uint32_t reg_cap = 1u << 18, out_cap = 1u << 16;
-    std::vector<int32_t> ub(nu);
-    for (uint32_t i = 0; i < nu; ++i) ub[i] = c->units[i].buffer;
-    HIPCHK(c->d_unit_buffer.ensure(nu));
-    HIPCHK(hipMemcpy(c->d_unit_buffer.p, ub.data(), nu * sizeof(int32_t), hipMemcpyHostToDevice));
-    HIPCHK(c->d_resync.ensure(nu));
-    HIPCHK(hipMemsetAsync(c->d_resync.p, 0, nu * sizeof(uint32_t), c->stream));
-    HIPCHK(c->d_emu_n.ensure(1));
-    HIPCHK(c->d_emu_err.ensure(1));
-    HIPCHK(hipMemsetAsync(c->d_emu_n.p, 0, 4, c->stream));
-    HIPCHK(hipMemsetAsync(c->d_emu_err.p, 0, 4, c->stream));
-    HIPCHK(c->d_emu_out.ensure(out_cap));
-    HIPCHK(c->d_emu_counts.ensure((size_t)out_cap * S));
-    HIPCHK(c->d_ring_hits.ensure(2ull * W * S));
-    HIPCHK(c->d_reg_f.ensure(2ull * reg_cap));
-    HIPCHK(c->d_reg_r.ensure(2ull * reg_cap));
-    HIPCHK(c->d_reg_hit.ensure(2ull * reg_cap));
-    HIPCHK(c->d_reg_hits.ensure(2ull * reg_cap * S));
-    EmuParams E{};
-    E.units = c->d_units.p;
-    E.nunits = nu;
-    E.unit_buffer = c->d_unit_buffer.p;
-    E.unit_head = c->d_head.p;
-    E.S = S;
-    E.nnc = (int32_t)c->nc.size();
-    E.nc = c->d_nc.p;
-    E.is_control = c->d_ctl.p;
-    E.coef = c->d_coef.p;
-    E.ncoef = (int32_t)c->coef.size();
-    E.kern = c->d_kern.p;
-    E.bw = c->p.bw;
-    E.nondir = c->p.nondir;
-    E.region_thr = c->p.region_thr;
-    E.kurt_thr = c->p.kurt_thr;
-    E.corr_thr = c->p.corr_thr;
-    E.hit_thr = c->p.hit_thr;
-    E.want_corr = c->p.want_corr || c->p.corr_thr > -1;
-    E.resync = c->d_resync.p;
-    E.out = c->d_emu_out.p;
-    E.out_counts = c->d_emu_counts.p;
-    E.nout = c->d_emu_n.p;
-    E.out_cap = out_cap;
-    E.ring_hits = c->d_ring_hits.p;
-    E.reg_f = c->d_reg_f.p;
-    E.reg_r = c->d_reg_r.p;
-    E.reg_hit = c->d_reg_hit.p;
-    E.reg_hits = c->d_reg_hits.p;
-    E.reg_cap = reg_cap;
-    E.err = c->d_emu_err.p;
-    hipLaunchKernelGGL(emulate_kernel, dim3(2), dim3(64), 0, c->stream, E);
-    HIPCHK(hipGetLastError());
-    uint32_t nemu = 0, err = 0;
-    std::vector<uint32_t> resync(nu);
-    HIPCHK(hipMemcpyAsync(&nemu, c->d_emu_n.p, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(&err, c->d_emu_err.p, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(resync.data(), c->d_resync.p, nu * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if (err) {
-        fprintf(stderr, "unipeak_hip: head-hit replay failed (flags %u)\n", err);
-        return err & 4u ? UP_E_ARG : UP_E_NOMEM;
-    }
-    std::vector<up_region> emu(nemu);
-    std::vector<uint32_t> ecnt((size_t)nemu * S);
-    if (nemu) {
-        HIPCHK(hipMemcpy(emu.data(), c->d_emu_out.p, nemu * sizeof(up_region), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(ecnt.data(), c->d_emu_counts.p, ecnt.size() * 4, hipMemcpyDeviceToHost));
-    }
+    std::vector<up_region> emu;
+    std::vector<uint32_t> ecnt, resync;
+    int rc = emulate_units(c, false, emu, ecnt, resync);
+    if (rc) return rc;
+    const uint32_t nemu = (uint32_t)emu.size();
     // the parallel path's records of this pass, wherever K3 wrote them
     const up_ctx::Pass &ps = c->pass[slot];
     const up_region *par = c->hp_regions[slot].p;
@@ -932,29 +1018,7 @@ static int replay_head_hits(up_ctx *c, int slot) {
             c->h_emulated.push_back(0);
         }
     }
-    c->host_regions = true;
-    c->nreg = c->h_regions.size();
-    if (ps.target) {  // keep the caller's buffer authoritative
-        if (c->nreg > ps.target_cap) return UP_E_NOMEM;
-        const uint64_t hdr = c->nreg;
-        const size_t cb = c->h_counts.size() * sizeof(uint32_t);
-        if (ps.target_hostp) {
-            uint8_t *h = (uint8_t *)ps.target_hostp;
-            std::memcpy(h, &hdr, 8);
-            if (c->nreg) {
-                std::memcpy(h + 8, c->h_regions.data(), c->nreg * sizeof(up_region));
-                std::memcpy(h + 8 + ps.target_cap * sizeof(up_region), c->h_counts.data(), cb);
-            }
-        } else {
-            HIPCHK(hipMemcpy(ps.target, &hdr, 8, hipMemcpyHostToDevice));
-            if (c->nreg) {
-                HIPCHK(hipMemcpy(ps.target + 8, c->h_regions.data(), c->nreg * sizeof(up_region), hipMemcpyHostToDevice));
-                HIPCHK(hipMemcpy(ps.target + 8 + ps.target_cap * sizeof(up_region), c->h_counts.data(), cb,
-                                 hipMemcpyHostToDevice));
-            }
-        }
-    }
-    return UP_OK;
+    return publish_host_regions(c, ps);
 }
 
 // Enqueue one pass K1a -> K1b -> K2a -> K2b -> K3 -> head detect into `slot`
@@ -1156,9 +1220,54 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
     return UP_OK;
 }
 
+// every unit through K0, never resynced (replay_mode configurations)
+static int run_replay(up_ctx *c, uint64_t *n_regions) {
+    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(hipSetDevice(c->dev));
+    c->ran = false;
+    c->nreg = 0;
+    c->host_regions = false;
+    c->h_regions.clear();
+    c->h_counts.clear();
+    c->h_emulated.clear();
+    int r = sync_units(c);
+    if (r) return r;
+    const uint32_t nu = (uint32_t)c->units.size();
+    up_ctx::Pass ps;
+    ps.target = c->target;
+    ps.target_hostp = c->target_hostp;
+    ps.target_cap = c->target_cap;
+    if (nu) {
+        HIPCHK(c->d_head.ensure(nu));
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)c->d_head.p, 1, nu, c->stream));
+        std::vector<up_region> emu;
+        std::vector<uint32_t> ecnt, resync;
+        if ((r = emulate_units(c, true, emu, ecnt, resync))) return r;
+        const int S = c->p.n_samples;
+        std::vector<uint32_t> order(emu.size());
+        for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](uint32_t a, uint32_t b) { return emu[a].unit < emu[b].unit; });
+        for (uint32_t i : order) {
+            c->h_regions.push_back(emu[i]);
+            c->h_counts.insert(c->h_counts.end(), ecnt.begin() + (size_t)i * S, ecnt.begin() + (size_t)(i + 1) * S);
+            c->h_emulated.push_back(1);
+        }
+    }
+    if ((r = publish_host_regions(c, ps))) return r;
+    for (double &t : c->times) t = 0;
+    c->times[3] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->ran = true;
+    if (n_regions) *n_regions = c->nreg;
+    return UP_OK;
+}
+
 int up_run(up_ctx *c, uint64_t *n_regions) {
     if (!c) return UP_E_ARG;
     if (busy(c)) return UP_E_STATE;
+    int rc = check_params(c);
+    if (rc) return rc;
+    if (replay_mode(c)) return run_replay(c, n_regions);
     int r = up_run_async(c);
     if (r) return r;
     return up_run_wait(c, n_regions);

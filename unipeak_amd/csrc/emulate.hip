@@ -48,6 +48,15 @@ struct EmuParams {
     uint32_t *reg_hits;          // [2][reg_cap][S]
     uint32_t reg_cap;
     uint32_t *err;               // nonzero: capacity exceeded / contract violated
+    // whole-buffer replay (configurations outside the parallel scan: -r <= 0
+    // makes the leap branch of processPosition live, quirk Q11; bw > kMaxBw):
+    // every unit is replayed, never resynced
+    int32_t replay_all;
+    // the deque window: dynamic LDS (ring_lds) or, for very wide kernels,
+    // global scratch [2][W] per array
+    int32_t ring_lds;
+    double *ring_f, *ring_r;
+    uint8_t *ring_has;
 };
 
 struct EmuState {
@@ -195,7 +204,7 @@ __device__ static void emu_process(const EmuParams &P, EmuState &E, uint32_t pos
     }
     E.last_pos = pos;
     // resync: aligned, leftovers retired, nothing open
-    if (E.aligned && (uint64_t)pos > E.horizon && E.n == 0) E.resynced = true;
+    if (!P.replay_all && E.aligned && (uint64_t)pos > E.horizon && E.n == 0) E.resynced = true;
 }
 
 // ProfileBuffer::add (peakcall.cpp:161-222) without the contig switch
@@ -247,24 +256,29 @@ __device__ static void emu_add(const EmuParams &P, EmuState &E, const uint32_t *
 }
 
 __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
-    __shared__ double rf[2 * kMaxBw + 1], rr[2 * kMaxBw + 1];
-    __shared__ uint8_t rhas[2 * kMaxBw + 1];
-    __shared__ uint32_t cnt_buf[64 * 4];
+    extern __shared__ double emu_lds[];  // the window when P.ring_lds: rf[W], rr[W], rhas[W]
     __shared__ int stop_flag;
     const int lane = threadIdx.x;
     const int buffer = blockIdx.x;
     const int S = P.S;
     EmuState E;
     E.W = 2 * P.bw + 1;
-    E.rf = rf;
-    E.rr = rr;
-    E.rhas = rhas;
+    if (P.ring_lds) {
+        E.rf = emu_lds;
+        E.rr = emu_lds + E.W;
+        E.rhas = (uint8_t *)(emu_lds + 2 * E.W);
+    } else {
+        E.rf = P.ring_f + (uint64_t)buffer * E.W;
+        E.rr = P.ring_r + (uint64_t)buffer * E.W;
+        E.rhas = P.ring_has + (uint64_t)buffer * E.W;
+    }
+    double *rf = E.rf, *rr = E.rr;
+    uint8_t *rhas = E.rhas;
     E.rhits = P.ring_hits + (uint64_t)buffer * E.W * S;
     E.gf = P.reg_f + (uint64_t)buffer * P.reg_cap;
     E.gr = P.reg_r + (uint64_t)buffer * P.reg_cap;
     E.ghit = P.reg_hit + (uint64_t)buffer * P.reg_cap;
     E.ghits = P.reg_hits + (uint64_t)buffer * P.reg_cap * S;
-    (void)cnt_buf;
 
     bool in_chain = false;
     for (uint32_t u = 0; u < P.nunits; ++u) {
