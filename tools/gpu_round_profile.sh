@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round profile set (results under gpurun_out/final/, copied into
+# profiles/r01/ afterwards): bench with CPU baseline, rocprofv3 kernel-trace
+# stats and K1a PMC traffic of the same bench, simulated ranks of 2/4/8-GPU
+# plans, the other BASELINE workloads at N=1, and pytest -m gpu.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+F=$R/gpurun_out/final
+mkdir -p $F
+cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $F/pytest_gpu.log 2>&1 || { tail -20 $F/pytest_gpu.log; exit 1; }
+tail -1 $F/pytest_gpu.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $F/bench_full.json 2> $F/bench_full.err || exit 1
+tail -1 $F/bench_full.json | cut -c1-300
+for wl in hg19-nondir1 hg19-8s1c; do
+  timeout -k 10 300 python bench.py --workload $wl --no-cpu-baseline > $F/bench_$wl.json 2> $F/bench_$wl.err || exit 1
+done
+OUT=$F/sim NS="2 4 8" STEPS=20 tools/sim_ranks.sh > $F/sim.log 2>&1 || exit 1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $F/trace -o p -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $F/trace.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $F/fetch -o p -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $F/fetch.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $F/write -o p -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $F/write.log 2>&1 || exit 1
+echo profile-ok
