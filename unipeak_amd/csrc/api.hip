@@ -1079,6 +1079,9 @@ static int launch_pass(up_ctx *c, int slot) {
     if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[1], c->stream));
     dispatch_scan<false, kModeExact>(c, SP, 0, ns);    // K1b: exact blocks
     HIPCHK(hipGetLastError());
+#ifdef UPK_EXP_K1B_TWICE  // experiment: a second (idempotent) K1b over warm caches/TLBs
+    dispatch_scan<false, kModeExact>(c, SP, 0, ns);
+#endif
     if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[2], c->stream));
     unsigned long long *thdr = (unsigned long long *)ps.target;
     hipLaunchKernelGGL(seg_count_kernel, dim3(nsb), dim3(kSegBlock), 0, c->stream, c->d_info.p, c->d_cnt.p,

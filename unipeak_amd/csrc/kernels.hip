@@ -138,7 +138,10 @@ __device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], const UnitDesc &
     }
 }
 
-constexpr int kHB = 4;  // hits per batch in the KDE walks
+#ifndef UPK_KHB
+#define UPK_KHB 4
+#endif
+constexpr int kHB = UPK_KHB;  // hits per batch in the KDE walks
 // Kernel weights live in LDS with kKPad zero doubles on both sides, so every
 // (lane, hit) index of a window walk is a valid read and out-of-window pairs
 // add exactly +0 (accumulators start at +0 and never become -0, so x + 0 == x
@@ -489,9 +492,11 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
         if constexpr (MODE == kModeExact) {
             const uint32_t *e = P.xlist + (uint64_t)it * kXEntry;
             strip = e[0];
-            exact_blocks = e[1];
+            exact_blocks = e[1] & 0xFFFFu;
             mchunk = (e[2 + (lane >> 1)] >> (16 * (lane & 1))) & 0xFFFFu;
-            cur = find_unit(P.units, P.nunits, strip);
+            // K1a stored the unit with the entry (no dependent binary search)
+            cur = e[1] >> 16;
+            if (cur == 0xFFFFu) cur = find_unit(P.units, P.nunits, strip);
         } else {
             if (!have) { cur = find_unit(P.units, P.nunits, strip); have = true; }
             while (strip >= P.units[cur].strip0 + P.units[cur].nstrips) ++cur;
@@ -571,7 +576,7 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_
                 uint32_t *e = P.xlist + (uint64_t)slot * kXEntry;
                 const uint32_t hi = (uint32_t)__shfl_down((int)mchunk, 1);
                 if ((lane & 1) == 0) e[2 + (lane >> 1)] = mchunk | (hi << 16);
-                if (lane == 0) { e[0] = strip; e[1] = exact_blocks; }
+                if (lane == 0) { e[0] = strip; e[1] = exact_blocks | ((cur < 0xFFFFu ? cur : 0xFFFFu) << 16); }
             }
             continue;
         }
