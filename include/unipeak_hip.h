@@ -142,8 +142,9 @@ int up_reset_units(up_ctx *ctx);
  * the parallel scan does not represent -- region threshold <= 0 (the leap
  * branch of processPosition is live, quirk Q11) or bw > 127 -- run the exact
  * state machine over every unit instead (K0 replay, sequential per buffer:
- * exact, slow); up_run_async, up_unit_profile* and up_shift_scan refuse them
- * (UP_E_UNSUPPORTED). */
+ * exact, slow); up_run_async and up_unit_profile* refuse them
+ * (UP_E_UNSUPPORTED).  up_shift_scan correlates a replayed region's stored
+ * scores (Region::scores), as strandCorr does. */
 int up_run(up_ctx *ctx, uint64_t *n_regions);
 /* Pipelined form of up_run: up_run_async enqueues one pass and returns
  * (at most two passes in flight); up_run_wait completes the OLDEST pass in

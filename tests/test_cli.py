@@ -294,3 +294,30 @@ def test_regions_cli_q1_head_hits(orc_bin, gpu_lib, tmp_path, case, thr_m):
     out = compare_tool(orc_bin, tmp_path, "regions",
                        ["-q", "-c", str(ct), "-b", str(bw), "-m", thr_m] + args + files)
     assert out.count("\n") > 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["q1_heads_bw50", "replay_bw150", "replay_r0_small"])
+def test_strand_shift_cli_replayed_regions(orc_bin, gpu_lib, tmp_path, case):
+    """strand_shift over regions that come from the exact replay (Q1 head
+    hits, bw > 127, -r <= 0): strandCorr(shift) runs on the scores the state
+    machine stored, byte-identical reports"""
+    rng = np.random.default_rng(zlib.crc32(case.encode()))
+    contigs = [("c0", 60_000), ("c1", 40_000), ("c2", 30_000)]
+    ct = tmp_path / "contigs.txt"
+    write_contigs(ct, contigs)
+    bw = 150 if case == "replay_bw150" else 50
+    fwd, rev = gen_sample(rng, contigs, lo=bw + 1, n_cl=12, shift_rev=40, sd=80)
+    if case == "q1_heads_bw50":  # heavy stacks inside the first bw positions of every contig
+        for d in (fwd, rev):
+            for name, _ in contigs:
+                dense = dict(d.get(name, []))
+                for p in rng.integers(1, bw + 1, 8):
+                    dense[int(p)] = dense.get(int(p), 0) + int(rng.integers(20, 60))
+                d[name] = sorted(dense.items())
+    write_wig(tmp_path / "s0.wig", "s0", fwd, rev)
+    args = ["-c", str(ct), "-x", "20", "-n", "2", "-u", "-1", "-g", "30", "-m", "3000000", "-b", str(bw)]
+    if case == "replay_r0_small":
+        args += ["-r", "0"]
+    out = compare_tool(orc_bin, tmp_path, "strand_shift", args + ["s0.wig"])
+    assert "# best_shift=" in out

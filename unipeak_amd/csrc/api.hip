@@ -144,6 +144,11 @@ struct up_ctx {
     DevBuf<double> d_reg_f, d_reg_r;
     DevBuf<up_region> d_emu_out;
     DevBuf<double> d_ring_f, d_ring_r;   // K0 window in global memory (very wide kernels)
+    DevBuf<double> d_emu_scores;         // K0: stored scores of the replayed regions (f, r)
+    DevBuf<uint64_t> d_emu_score_off;
+    DevBuf<unsigned long long> d_emu_nscores;
+    uint64_t emu_scores_cap = 1ull << 22;
+    std::vector<uint64_t> h_score_off;   // per host region: offset in d_emu_scores or ~0
     DevBuf<uint8_t> d_ring_has;
     uint32_t emu_reg_cap = 1u << 18;     // K0: positions of one open region
     uint32_t emu_out_cap = 1u << 16;     // K0: region records
@@ -275,6 +280,7 @@ void up_close(up_ctx *c) {
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
     c->d_ring_f.release(); c->d_ring_r.release(); c->d_ring_has.release();
+    c->d_emu_scores.release(); c->d_emu_score_off.release(); c->d_emu_nscores.release();
     for (int k = 0; k < 2; ++k) {
         c->hp_regions[k].release(); c->hp_counts[k].release(); c->hp_status[k].release(); c->hp_head[k].release();
         for (auto &e : c->pass[k].ev) (void)hipEventDestroy(e);
@@ -824,7 +830,7 @@ static int launch_head_detect(up_ctx *c, int slot) {
 // exptSums and the per-unit resync positions.  Capacity of the region
 // record area and of one open region grow until the replay fits.
 static int emulate_units(up_ctx *c, bool replay_all, std::vector<up_region> &emu, std::vector<uint32_t> &ecnt,
-                         std::vector<uint32_t> &resync) {
+                         std::vector<uint32_t> &resync, std::vector<uint64_t> &soff) {
     const uint32_t nu = (uint32_t)c->units.size();
     const int S = c->p.n_samples;
     const uint32_t W = 2u * c->p.bw + 1;
@@ -850,6 +856,10 @@ static int emulate_units(up_ctx *c, bool replay_all, std::vector<up_region> &emu
         HIPCHK(hipMemsetAsync(c->d_resync.p, 0, nu * sizeof(uint32_t), c->stream));
         HIPCHK(hipMemsetAsync(c->d_emu_n.p, 0, 4, c->stream));
         HIPCHK(hipMemsetAsync(c->d_emu_err.p, 0, 4, c->stream));
+        HIPCHK(c->d_emu_nscores.ensure(1));
+        HIPCHK(hipMemsetAsync(c->d_emu_nscores.p, 0, sizeof(unsigned long long), c->stream));
+        HIPCHK(c->d_emu_scores.ensure(c->emu_scores_cap));
+        HIPCHK(c->d_emu_score_off.ensure(out_cap));
         if (!ring_lds) {
             HIPCHK(hipMemsetAsync(c->d_ring_f.p, 0, 2ull * W * sizeof(double), c->stream));
             HIPCHK(hipMemsetAsync(c->d_ring_r.p, 0, 2ull * W * sizeof(double), c->stream));
@@ -897,6 +907,10 @@ static int emulate_units(up_ctx *c, bool replay_all, std::vector<up_region> &emu
         E.ring_f = c->d_ring_f.p;
         E.ring_r = c->d_ring_r.p;
         E.ring_has = c->d_ring_has.p;
+        E.out_scores = c->d_emu_scores.p;
+        E.out_score_off = c->d_emu_score_off.p;
+        E.nscores = c->d_emu_nscores.p;
+        E.scores_cap = c->d_emu_scores.n;
         hipLaunchKernelGGL(emulate_kernel, dim3(2), dim3(64), ring_lds ? ring_bytes : 0, c->stream, E);
         HIPCHK(hipGetLastError());
         uint32_t nemu = 0, err = 0;
@@ -909,16 +923,24 @@ static int emulate_units(up_ctx *c, bool replay_all, std::vector<up_region> &emu
             fprintf(stderr, "unipeak_hip: exact replay: positions out of order\n");
             return UP_E_ARG;
         }
-        if (err & 3u) {  // 1: a region longer than reg_cap positions, 2: more than out_cap regions
+        if (err & 11u) {  // 1: a region longer than reg_cap positions, 2: more than out_cap
+                          // regions, 8: the region-score slab is full
             if (err & 1u) c->emu_reg_cap *= 4;
             if (err & 2u) c->emu_out_cap = std::max<uint32_t>(c->emu_out_cap * 4, nemu + nemu / 4);
+            if (err & 8u) {
+                unsigned long long used = 0;
+                HIPCHK(hipMemcpy(&used, c->d_emu_nscores.p, sizeof used, hipMemcpyDeviceToHost));
+                c->emu_scores_cap = std::max<uint64_t>(c->emu_scores_cap * 4, used + used / 4);
+            }
             continue;
         }
         emu.resize(nemu);
         ecnt.resize((size_t)nemu * S);
+        soff.resize(nemu);
         if (nemu) {
             HIPCHK(hipMemcpy(emu.data(), c->d_emu_out.p, nemu * sizeof(up_region), hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(ecnt.data(), c->d_emu_counts.p, ecnt.size() * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(soff.data(), c->d_emu_score_off.p, nemu * 8, hipMemcpyDeviceToHost));
         }
         return UP_OK;
     }
@@ -966,7 +988,8 @@ static int replay_head_hits(up_ctx *c, int slot) {
     const int S = c->p.n_samples;
     std::vector<up_region> emu;
     std::vector<uint32_t> ecnt, resync;
-    int rc = emulate_units(c, false, emu, ecnt, resync);
+    std::vector<uint64_t> soff;
+    int rc = emulate_units(c, false, emu, ecnt, resync, soff);
     if (rc) return rc;
     const uint32_t nemu = (uint32_t)emu.size();
     // the parallel path's records of this pass, wherever K3 wrote them
@@ -1005,17 +1028,20 @@ static int replay_head_hits(up_ctx *c, int slot) {
     c->h_regions.clear();
     c->h_counts.clear();
     c->h_emulated.clear();
+    c->h_score_off.clear();
     for (auto &k : keys) {
         if (k.second < 0) {
             const uint32_t i = (uint32_t)(-k.second - 1);
             c->h_regions.push_back(emu[i]);
             c->h_counts.insert(c->h_counts.end(), ecnt.begin() + (size_t)i * S, ecnt.begin() + (size_t)(i + 1) * S);
             c->h_emulated.push_back(1);
+            c->h_score_off.push_back(soff[i]);
         } else {
             const uint64_t i = (uint64_t)k.second;
             c->h_regions.push_back(par[i]);
             c->h_counts.insert(c->h_counts.end(), pcnt + i * S, pcnt + (i + 1) * S);
             c->h_emulated.push_back(0);
+            c->h_score_off.push_back(~0ull);
         }
     }
     return publish_host_regions(c, ps);
@@ -1233,6 +1259,7 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
     c->h_regions.clear();
     c->h_counts.clear();
     c->h_emulated.clear();
+    c->h_score_off.clear();
     int r = sync_units(c);
     if (r) return r;
     const uint32_t nu = (uint32_t)c->units.size();
@@ -1245,7 +1272,8 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
         HIPCHK(hipMemsetD32Async((hipDeviceptr_t)c->d_head.p, 1, nu, c->stream));
         std::vector<up_region> emu;
         std::vector<uint32_t> ecnt, resync;
-        if ((r = emulate_units(c, true, emu, ecnt, resync))) return r;
+        std::vector<uint64_t> soff;
+        if ((r = emulate_units(c, true, emu, ecnt, resync, soff))) return r;
         const int S = c->p.n_samples;
         std::vector<uint32_t> order(emu.size());
         for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
@@ -1255,6 +1283,7 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
             c->h_regions.push_back(emu[i]);
             c->h_counts.insert(c->h_counts.end(), ecnt.begin() + (size_t)i * S, ecnt.begin() + (size_t)(i + 1) * S);
             c->h_emulated.push_back(1);
+            c->h_score_off.push_back(soff[i]);
         }
     }
     if ((r = publish_host_regions(c, ps))) return r;
@@ -1372,8 +1401,8 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
             en[i] = c->h_regions[i].right;
             un[i] = c->h_regions[i].unit;
         }
-        for (size_t j = 0; j < n; ++j)
-            if (idx[j] < c->nreg && c->h_emulated[idx[j]]) return UP_E_UNSUPPORTED;
+        // replayed regions (Q1 heads, whole-buffer replay) correlate the
+        // scores the state machine stored (Region::scores), copied below
         HIPCHK(c->d_starts.ensure(c->nreg + 1));
         HIPCHK(c->d_ends.ensure(c->nreg + 1));
         HIPCHK(c->d_runit.ensure(c->nreg + 1));
@@ -1393,12 +1422,28 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
     }
     uint64_t *d_idx = nullptr, *d_off = nullptr;
     double *d_slab = nullptr, *d_out = nullptr;
+    uint8_t *d_pref = nullptr;
     HIPCHK(hipMalloc(&d_idx, n * 8));
     HIPCHK(hipMalloc(&d_off, n * 8));
     HIPCHK(hipMalloc(&d_slab, (tot + 1) * 8));
     HIPCHK(hipMalloc(&d_out, n * ((size_t)max_shift + 1) * 8));
+    HIPCHK(hipMalloc(&d_pref, n + 1));
     HIPCHK(hipMemcpy(d_idx, idx, n * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_off, off.data(), n * 8, hipMemcpyHostToDevice));
+    {
+        std::vector<uint8_t> pref(n + 1, 0);
+        for (size_t j = 0; j < n && c->host_regions; ++j) {
+            if (!c->h_emulated[idx[j]]) continue;
+            const uint64_t so = c->h_score_off[idx[j]];
+            if (so == ~0ull) return UP_E_INTERNAL;
+            const uint64_t len = (uint64_t)en[idx[j]] - st[idx[j]] + 1;
+            HIPCHK(hipMemcpyAsync(d_slab + off[j], c->d_emu_scores.p + so, 2 * len * sizeof(double),
+                                  hipMemcpyDeviceToDevice, c->stream));
+            pref[j] = 1;
+        }
+        HIPCHK(hipMemcpyAsync(d_pref, pref.data(), n + 1, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
     StatParams P = stat_params(c);
     const int nh = P.bw <= 63 ? 1 : 2;
     const int pool = pool_mode(c);
@@ -1407,7 +1452,7 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
 #define UPK_SH(NH, PL)                                                                        \
     if (nh == NH && pool == PL)                                                               \
         hipLaunchKernelGGL((shift_kernel<NH, PL>), dim3(blocks), dim3(64), lds, c->stream, P, \
-                           d_idx, (uint32_t)n, (int)max_shift, d_off, d_slab, d_out);
+                           d_idx, (uint32_t)n, (int)max_shift, d_off, d_slab, d_pref, d_out);
     UPK_SH(1, 0) UPK_SH(1, 1) UPK_SH(1, 2) UPK_SH(2, 0) UPK_SH(2, 1) UPK_SH(2, 2)
 #undef UPK_SH
     HIPCHK(hipGetLastError());
@@ -1417,6 +1462,7 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
     (void)hipFree(d_off);
     (void)hipFree(d_slab);
     (void)hipFree(d_out);
+    (void)hipFree(d_pref);
     return UP_OK;
 }
 

@@ -57,6 +57,12 @@ struct EmuParams {
     int32_t ring_lds;
     double *ring_f, *ring_r;
     uint8_t *ring_has;
+    // every replayed region's stored scores (Region::scores, data.cpp:92-96),
+    // f then r, for strandCorr(shift) in strand_shift: slab + per-region offset
+    double *out_scores;
+    uint64_t *out_score_off;     // [out_cap], ~0 when the slab was full
+    unsigned long long *nscores;
+    uint64_t scores_cap;
 };
 
 struct EmuState {
@@ -140,6 +146,19 @@ __device__ static void emu_region(const EmuParams &P, EmuState &E) {
     bool acc = (double)nonctl >= P.hit_thr;
     if (acc) acc = P.kurt_thr == 0 || (E.n > 1 && kurt <= P.kurt_thr);
     if (acc) acc = P.corr_thr <= -1 || corr >= P.corr_thr;
+    if (keep && P.out_scores) {
+        const unsigned long long off = atomicAdd(P.nscores, 2ull * E.n);
+        if (off + 2ull * E.n <= P.scores_cap) {
+            for (uint32_t i = 0; i < E.n; ++i) {
+                P.out_scores[off + i] = E.gf[i];
+                P.out_scores[off + E.n + i] = E.gr[i];
+            }
+            P.out_score_off[slot] = off;
+        } else {
+            P.out_score_off[slot] = ~0ull;
+            atomicOr(P.err, 8u);
+        }
+    }
     if (keep) {
         up_region &o = P.out[slot];
         o.unit = E.cur_unit;

@@ -1305,7 +1305,7 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
 template <int NH, int POOL>
 __global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t *idx, uint32_t n,
                                                    int max_shift, const uint64_t *slab_off,
-                                                   double *slab, double *out) {
+                                                   double *slab, const uint8_t *prefilled, double *out) {
     extern __shared__ double lds_[];
     const int bw = P.bw;
     const double *ktab = load_ktab(lds_, P.kern, bw);
@@ -1320,7 +1320,9 @@ __global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t 
         const UnitDesc U = P.units[u];
         const uint32_t len = right - left + 1;
         double *fs = slab + slab_off[j], *rs = fs + len;
-        for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
+        // replayed regions arrive with their stored scores; the others are
+        // materialised from the dense KDE
+        for (int64_t x0 = left; !prefilled[j] && x0 <= (int64_t)right; x0 += 64) {
             WinT<POOL> cf[NWT], cr[NWT];
             uint64_t hf[NWT], hr[NWT];
             region_words<NH, POOL>(cf, hf, U, 0, x0, lane, P);
