@@ -442,8 +442,15 @@ __device__ __forceinline__ bool has_big(u32x4 v) {
 // MODE kModeExact (K1b): run the exact blocks of the listed strips, so the
 // latency-bound KDE never stalls the streaming waves.  kModeFused: both in
 // one pass (the PROF profile variant, every block exact).
+// K1b runs 4 waves per SIMD (the LDS limit of its 38 KiB blocks) instead of
+// the 2-3 its register count allows: 128 VGPRs with a few spilled registers
+// beat the lower occupancy (hg19 0.35 -> 0.29 ms; nondirectional 0.42 ->
+// 0.30 ms; 8 samples 4.1 -> 2.7 ms).  K1a keeps the compiler's choice.
+#ifndef UPK_SCAN_ATTR
+#define UPK_SCAN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == kModeExact ? 4 : 1)))
+#endif
 template <int NH, int POOL, bool NONDIR, bool PROF, int MODE>
-__global__ void __launch_bounds__(256) scan_kernel(ScanParams P, uint32_t strip_begin,
+__global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, uint32_t strip_begin,
                                                    uint32_t strip_end) {
     extern __shared__ double lds_[];
     const int bw = P.bw;
@@ -1004,7 +1011,11 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
         };
         // K1 saw the whole run: its peak is known and, unless the strand
         // correlation is wanted, no score is needed here -- only the counts
+#ifdef UPK_EXP_ALLKNOWN
+        const bool known = P.peak_pos != nullptr && !(NONDIR && P.want_corr);
+#else
         const bool known = P.peak_pos != nullptr && P.peak_pos[ri] != 0 && !(NONDIR && P.want_corr);
+#endif
         int blk = 0;
         bool counted = false;
         if constexpr (POOL == 0) {
@@ -1185,7 +1196,11 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
         const double x_bar = (double)psum / (double)count;
         double sum2 = 0.0, sum4 = 0.0;
         int blk2 = 0;
+#ifdef UPK_EXP_NOPASS2
+        for (int64_t x0 = left; x0 < left; x0 += 64, ++blk2) {
+#else
         for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64, ++blk2) {
+#endif
             const int64_t x = x0 + lane;
             const bool valid = x <= (int64_t)right;
             uint32_t pc = 0;
