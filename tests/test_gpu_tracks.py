@@ -137,3 +137,58 @@ def test_nondir_large_counts_corr(gpu_lib, oracle):
                              want_corr=True)
     compare(ref, ref_sums, regs, gcnt)
     assert close(ref["corr"], regs["corr"])
+
+
+def _edge_cluster(oracle, bw, bg, length, edge, want):
+    """a tag cluster shifted until the oracle's region ends at `edge`
+    (want='right') or starts at edge + 1 (want='left'): a run that K2 closes
+    or opens at a strip boundary"""
+    base = np.array([-30, -12, -5, 0, 4, 9, 21, 33])
+    for d in range(-200, 200):
+        pos = np.unique(edge + d + base).astype(np.uint32)
+        cnt = np.full((len(pos), 1), 3, np.uint32)
+        ref, _ = oracle.run_unit(bw, bg, pos, cnt)
+        if any((r["right"] == edge) if want == "right" else (r["left"] == edge + 1) for r in ref):
+            return pos, cnt
+    raise AssertionError("no shift puts the region edge on the strip boundary")
+
+
+def test_runs_across_whole_strips_peak_merge(gpu_lib, oracle):
+    """runs spanning several 16384-position strips: K3 merges the peaks of
+    their per-strip parts (first maximum, ties across strips included) and runs
+    closed/opened exactly at a strip boundary"""
+    rng = np.random.default_rng(99)
+    length, bw, bg = 200_000, 50, 0.003
+    dense = {}
+    # constant density over 3+ strips: equal scores everywhere inside (ties)
+    for p in range(10_000, 60_000):
+        dense[p] = 1
+    # random density over 4 strips with the maximum in a middle strip
+    for p in range(70_000, 140_000, 3):
+        dense[p] = int(rng.integers(1, 4))
+    for p in range(101_000, 101_040):
+        dense[p] = 40
+    # a run whose maximum sits in its first (partial) strip, one in its last
+    for p in range(146_000, 170_000, 2):
+        dense[p] = 2
+    for p in range(146_100, 146_130):
+        dense[p] = 30
+    for p in range(175_000, 196_000, 2):
+        dense[p] = 2
+    for p in range(195_900, 195_930):
+        dense[p] = 30
+    pos = np.array(sorted(dense), np.uint32)
+    cnt = np.array([[dense[int(p)]] for p in pos], np.uint32)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, kurt_thr=0.0)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, kurt_thr=0.0)
+    compare(ref, ref_sums, regs, gcnt)
+    assert (ref["right"] - ref["left"] >= 16384).sum() >= 3
+
+
+@pytest.mark.parametrize("want", ["right", "left"])
+def test_run_edge_on_strip_boundary(gpu_lib, oracle, want):
+    length, bw, bg = 60_000, 50, 0.003
+    pos, cnt = _edge_cluster(oracle, bw, bg, length, 16384 * 2, want)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt)
+    compare(ref, ref_sums, regs, gcnt)

@@ -117,6 +117,7 @@ struct up_ctx {
     DevBuf<uint64_t> d_cnt, d_nreg;
     DevBuf<uint32_t> d_starts, d_ends, d_runit, d_peak_pos, d_xlist, d_xcount;
     DevBuf<double> d_peak_val;
+    DevBuf<uint64_t> d_spk;          // K1 per-strip partial peaks (ScanParams::spk)
     uint32_t ovf_cap = 256;
     uint64_t nreg = 0;
     bool ran = false;
@@ -276,6 +277,7 @@ void up_close(up_ctx *c) {
     c->d_cnt.release(); c->d_nreg.release();
     c->d_starts.release(); c->d_ends.release(); c->d_runit.release();
     c->d_peak_pos.release(); c->d_peak_val.release(); c->d_xlist.release(); c->d_xcount.release();
+    c->d_spk.release();
     c->d_head.release(); c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
@@ -705,6 +707,7 @@ static ScanParams scan_params(up_ctx *c) {
     P.ovf_cap = c->ovf_cap;
     P.xlist = c->d_xlist.p;
     P.xcount = c->d_xcount.p;
+    P.spk = c->d_spk.p;
     return P;
 }
 
@@ -1061,6 +1064,7 @@ static int launch_pass(up_ctx *c, int slot) {
     HIPCHK(c->d_info.ensure(ns));
     HIPCHK(c->d_rec.ensure((size_t)ns * kRecStride));
     HIPCHK(c->d_xlist.ensure((size_t)ns * kXEntry));
+    HIPCHK(c->d_spk.ensure((size_t)ns * 4));
     HIPCHK(c->d_cnt.ensure(ns));
     HIPCHK(c->d_bsum.ensure(nsb));
     HIPCHK(c->d_nreg.ensure(1));
@@ -1124,6 +1128,7 @@ static int launch_pass(up_ctx *c, int slot) {
     P.cap = cap;
     P.peak_pos = c->d_peak_pos.p;
     P.peak_val = c->d_peak_val.p;
+    P.spk = c->d_spk.p;
     if (ps.target) {  // records into the caller's buffer instead
         P.cap = std::min<uint64_t>(cap, ps.target_cap);
         P.out = ps.target + 8;

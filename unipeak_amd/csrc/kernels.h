@@ -73,6 +73,10 @@ struct ScanParams {
     uint32_t *ovf_rec;      // [ovf_cap][kOvfStride]
     uint32_t *xlist;        // K1a -> K1b work list: [nstrips][kXEntry]
     uint32_t *xcount;       // entries in xlist
+    uint64_t *spk;          // [nstrips][4]: peak (f+r bits, position) of the run open at
+                            // the strip's first position ([0..1], written when it closes
+                            // inside the strip) and of the run open at its last position
+                            // ([2..3], from its start or the strip's first position)
     uint32_t ovf_cap;
 #ifdef UPK_DEBUG_COUNTS
     unsigned long long *dbg;  // counters: exact blocks, live words
@@ -94,7 +98,8 @@ struct StatParams {
     int32_t want_corr;
     double region_thr, kurt_thr, corr_thr, hit_thr;
     const uint32_t *starts, *ends, *reg_unit;
-    const uint32_t *peak_pos;  // from K1 (0: unknown -> K3 computes it)
+    const uint32_t *peak_pos;  // from K1 (0: the run crossed a strip edge -> spk)
+    const uint64_t *spk;       // K1's per-strip partial peaks (ScanParams::spk)
     const double *peak_val;
     const uint64_t *nreg;
     uint64_t cap;         // records the output areas hold

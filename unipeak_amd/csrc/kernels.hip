@@ -602,6 +602,10 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             const uint32_t pp = wave_min_u32(lb == m ? lp : 0xFFFFFFFFu);
 #endif
             rec_end(R_, end_pos, pk_ok ? pp : 0u, m, P, strip, lane);
+            if (!pk_ok && lane == 0) {  // the run open at p0: its part in this strip
+                P.spk[4ull * strip] = (uint64_t)__double_as_longlong(m);
+                P.spk[4ull * strip + 1] = pp;
+            }
             lb = -__builtin_inf();
         };
 
@@ -784,6 +788,14 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             }
         }
         if constexpr (PROF) continue;
+        if (prevF >> 63) {  // the run open at the strip's last position: its part here
+            const double m = wave_max_d(lb);
+            const uint32_t pp = wave_min_u32(lb == m ? lp : 0xFFFFFFFFu);
+            if (lane == 0) {
+                P.spk[4ull * strip + 2] = (uint64_t)__double_as_longlong(m);
+                P.spk[4ull * strip + 3] = pp;
+            }
+        }
         // a run open at the strip's last position has no interior end (K2)
         const uint64_t info = (uint64_t)R_.ns | ((uint64_t)R_.ne << 16) | ((F0 & 1ull) << 32) |
                               ((prevF >> 63) << 33) | ((uint64_t)(local == 0) << 34) |
@@ -1011,11 +1023,35 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
         };
         // K1 saw the whole run: its peak is known and, unless the strand
         // correlation is wanted, no score is needed here -- only the counts
-#ifdef UPK_EXP_ALLKNOWN
         const bool known = P.peak_pos != nullptr && !(NONDIR && P.want_corr);
+        uint32_t kpos = 0;
+        double kval = 0.0;
+        if (known) {
+            kpos = P.peak_pos[ri];
+            kval = P.peak_val[ri];
+#ifdef UPK_EXP_NOCOMBINE
+            if (false) {
 #else
-        const bool known = P.peak_pos != nullptr && P.peak_pos[ri] != 0 && !(NONDIR && P.want_corr);
+            if (kpos == 0) {
 #endif
+                // the run crossed a strip edge: first maximum over its parts,
+                // in position order -- the part of the run open at a strip's
+                // first position that closes inside it, else the part open at
+                // the strip's last position (from the run start or the strip's
+                // first position)
+                const uint32_t sa = U.strip0 + (left - 1) / kStrip, sb = U.strip0 + (right - 1) / kStrip;
+                for (uint32_t s = sa; s <= sb; ++s) {
+                    const uint32_t sp0 = 1 + (s - U.strip0) * kStrip;
+                    const bool pre = (s > sa || left == sp0) && s == sb && right < sp0 + kStrip - 1;
+                    const uint64_t *e = P.spk + 4ull * s + (pre ? 0 : 2);
+                    const double v = __longlong_as_double((long long)e[0]);
+                    if (s == sa || v > kval) {
+                        kval = v;
+                        kpos = (uint32_t)e[1];
+                    }
+                }
+            }
+        }
         int blk = 0;
         bool counted = false;
         if constexpr (POOL == 0) {
@@ -1024,8 +1060,8 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             // scored; escapes resolved at use
             const int nw = (int)((right - left) / 64u) + 1;
             if (known && S == 1 && nw <= kStatCache) {
-                best = P.peak_val[ri];
-                best_x = P.peak_pos[ri];
+                best = kval;
+                best_x = kpos;
                 gu8 *t0 = track_u8(U, S, 0, P.nc[0]) + kPad + (int64_t)left - 1 + lane;
                 uint32_t r0[kStatCache], r1[NONDIR ? kStatCache : 1];
 #pragma unroll
@@ -1058,8 +1094,8 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             }
         }
         if (known && !counted) {
-            best = P.peak_val[ri];
-            best_x = P.peak_pos[ri];
+            best = kval;
+            best_x = kpos;
             for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64, ++blk) {
                 const int64_t x = x0 + lane;
                 const bool valid = x <= (int64_t)right;
