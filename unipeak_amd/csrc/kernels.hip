@@ -159,7 +159,14 @@ __device__ __forceinline__ double *load_ktab(double *lds, const double *kern, in
     return lds + kKPad;
 }
 constexpr int kStatCache = 16;  // K3: 64-position blocks of pass-1 totals kept in LDS
-constexpr size_t kStatLds = kKTab * sizeof(double) + 4 * kStatCache * 64 * sizeof(uint32_t);
+// + per wave one word's kurtosis terms, compacted (pass 2's ordered sums read
+// them back with broadcast LDS loads)
+#ifndef UPK_TB
+#define UPK_TB 4
+#endif
+constexpr int kTermBatch = UPK_TB;  // pass-2 term pairs loaded per batch
+constexpr size_t kStatLds = kKTab * sizeof(double) + 4 * kStatCache * 64 * sizeof(uint32_t) +
+                            4 * 64 * 2 * sizeof(double);
 
 // next batch of up to kHB set bits of m (ascending) with their broadcast counts
 template <typename T>
@@ -1001,6 +1008,7 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
 
     // per-wave cache of the pass-1 hit totals pc (pass 2 reads them back)
     uint32_t *pcache = (uint32_t *)(lds_ + kKTab) + (threadIdx.x >> 6) * (kStatCache * 64);
+    double2 *terms = (double2 *)((uint32_t *)(lds_ + kKTab) + 4 * kStatCache * 64) + (threadIdx.x >> 6) * 64;
 
     for (uint64_t ri = wave; ri < nreg; ri += nwaves) {
         const uint32_t left = P.starts[ri], right = P.ends[ri], u = P.reg_unit[ri];
@@ -1278,13 +1286,36 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             const double d = (double)(uint16_t)(x - left) - x_bar;
             const double d2 = d * d;
             const double t2 = (double)pc * d2, t4 = (double)pc * (d2 * d2);
-            uint64_t m = __ballot(pc != 0u);  // positions holding a stored hit vector
-            while (m) {
-                const int l = __builtin_ctzll(m);
-                m &= m - 1;
-                sum2 = sum2 + rl_d(t2, l);
-                sum4 = sum4 + rl_d(t4, l);
+            // positions holding a stored hit vector, compacted in position
+            // order; the two chains then read them back as wave-uniform LDS
+            // broadcasts (one ds_read_b128 per term pair, a batch in flight)
+            const uint64_t m = __ballot(pc != 0u);
+            const int nh = __builtin_popcountll(m);
+            if (pc != 0u) {
+                const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                terms[k] = make_double2(t2, t4);
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            int k = 0;
+            for (; k + kTermBatch <= nh; k += kTermBatch) {
+                double2 v[kTermBatch];
+#pragma unroll
+                for (int i = 0; i < kTermBatch; ++i) v[i] = terms[k + i];
+#pragma unroll
+                for (int i = 0; i < kTermBatch; ++i) {
+                    sum2 = sum2 + v[i].x;
+                    sum4 = sum4 + v[i].y;
+                }
+            }
+            for (; k < nh; ++k) {
+                const double2 a = terms[k];
+                sum2 = sum2 + a.x;
+                sum4 = sum4 + a.y;
+            }
+            __builtin_amdgcn_wave_barrier();  // terms reused by the next word
         }
         const double kurt = ((double)count - 1) * sum4 / (sum2 * sum2);
 
