@@ -1070,7 +1070,7 @@ static int launch_pass(up_ctx *c, int slot) {
     HIPCHK(c->d_nreg.ensure(1));
     HIPCHK(c->hp_status[slot].ensure(4));
     if (!c->d_xcount.p || !c->d_ovf_count.p) c->counters_armed = false;
-    HIPCHK(c->d_xcount.ensure(1));
+    HIPCHK(c->d_xcount.ensure(2));  // front / back ends of the work list
     HIPCHK(c->d_ovf_count.ensure(1));
     const uint64_t cap = c->reg_cap;
     HIPCHK(c->d_ovf_rec.ensure((size_t)c->ovf_cap * kOvfStride));
@@ -1090,7 +1090,7 @@ static int launch_pass(up_ctx *c, int slot) {
     ps.ovf_cap = c->ovf_cap;
     if (!c->counters_armed) {  // K2b re-arms them at the end of every pass
         HIPCHK(hipMemsetAsync(c->d_ovf_count.p, 0, sizeof(uint32_t), c->stream));
-        HIPCHK(hipMemsetAsync(c->d_xcount.p, 0, sizeof(uint32_t), c->stream));
+        HIPCHK(hipMemsetAsync(c->d_xcount.p, 0, 2 * sizeof(uint32_t), c->stream));
     }
     c->counters_armed = false;  // until K2b is enqueued
     ScanParams SP = scan_params(c);

@@ -72,7 +72,7 @@ struct ScanParams {
     uint32_t *ovf_count;
     uint32_t *ovf_rec;      // [ovf_cap][kOvfStride]
     uint32_t *xlist;        // K1a -> K1b work list: [nstrips][kXEntry]
-    uint32_t *xcount;       // entries in xlist
+    uint32_t *xcount;       // [2] entries listed from the front / from the back of xlist
     uint64_t *spk;          // [nstrips][4]: peak (f+r bits, position) of the run open at
                             // the strip's first position ([0..1], written when it closes
                             // inside the strip) and of the run open at its last position

@@ -416,6 +416,10 @@ __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], 
 constexpr int kScrWords = 8 + kBlocks * kWave + 8;  // chunk sums of one strip + halos
 constexpr size_t kScreenLds = kKTab * sizeof(double) + 4 * kScrWords * sizeof(uint32_t);
 constexpr size_t kScanLds = kScreenLds + 4 * kStepWords * kWave * sizeof(double);
+#ifndef UPK_XFRONT
+#define UPK_XFRONT 2
+#endif
+constexpr int kXFront = UPK_XFRONT;  // K1b work items with >= this many exact blocks go first
 constexpr size_t kExactLds = kKTab * sizeof(double) + 4 * kStepWords * kWave * sizeof(double);
 
 // chunk i (0..15) of this lane: window a[8+i-R .. 8+i+R] > wskip
@@ -486,7 +490,11 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 
     uint32_t cur = 0;
     bool have = false;
-    uint32_t it_end = MODE == kModeExact ? *P.xcount : strip_end;
+    // K1b: multi-block entries were listed from the front, single-block ones
+    // from the back, so the first resident waves take the long items
+    const uint32_t nfront = MODE == kModeExact ? P.xcount[0] : 0u;
+    const uint32_t nback = MODE == kModeExact ? P.xcount[1] : 0u;
+    uint32_t it_end = MODE == kModeExact ? nfront + nback : strip_end;
     uint32_t it0 = (MODE == kModeExact ? 0u : strip_begin) + wave, istep = nwaves;
 #ifdef UPK_EXP_CONTIG
     if constexpr (MODE == kModeExact) {  // contiguous item ranges per wave (locality experiment)
@@ -504,7 +512,8 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         uint32_t mchunk = 0xFFFFu;
         uint32_t exact_blocks = 0xFFFFu;
         if constexpr (MODE == kModeExact) {
-            const uint32_t *e = P.xlist + (uint64_t)it * kXEntry;
+            const uint32_t ei = it < nfront ? it : P.nstrips - nback + (it - nfront);
+            const uint32_t *e = P.xlist + (uint64_t)ei * kXEntry;
             strip = e[0];
             exact_blocks = e[1] & 0xFFFFu;
             mchunk = (e[2 + (lane >> 1)] >> (16 * (lane & 1))) & 0xFFFFu;
@@ -585,7 +594,8 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 if (lane == 0) P.strip_info[strip] = info;
             } else {
                 uint32_t slot = 0;
-                if (lane == 0) slot = atomicAdd(P.xcount, 1u);
+                const bool front = __builtin_popcount(exact_blocks) >= kXFront;
+                if (lane == 0) slot = front ? atomicAdd(P.xcount, 1u) : P.nstrips - 1u - atomicAdd(P.xcount + 1, 1u);
                 slot = rl_u(slot, 0);
                 uint32_t *e = P.xlist + (uint64_t)slot * kXEntry;
                 const uint32_t hi = (uint32_t)__shfl_down((int)mchunk, 1);
@@ -900,7 +910,8 @@ __global__ void __launch_bounds__(kSegBlock) seg_compact_kernel(
         status[2] = nst != nen;
         if (target_hdr) *target_hdr = valid ? nst : 0;  // caller's record buffer (up_set_record_target)
         *ovf_count = 0u;                    // K1b has consumed the work list
-        *xcount = 0u;
+        xcount[0] = 0u;
+        xcount[1] = 0u;
     }
     if (c == 0) return;
     const uint64_t v = info[i];
