@@ -3,7 +3,7 @@ import csv
 import re
 import sys
 
-short = [("scan_kernel<.*, 1>", "K1a"), ("scan_kernel<.*, 2>", "K1b"), ("seg_count", "K2a"),
+short = [("scan_kernel<.*, 1>", "K1a"), ("scan_kernel<.*, 2>", "K1b"), ("seg_count_kernel", "K2a"), ("seg_count_head", "K2a+K0d"),
          ("seg_compact", "K2b"), ("stats_kernel", "K3"), ("head_detect|unit_last", "K0d")]
 rows = list(csv.DictReader(open(sys.argv[1])))
 out = []

@@ -157,7 +157,7 @@ struct up_ctx {
     std::vector<up_region> h_regions;
     std::vector<uint32_t> h_counts;
     std::vector<uint8_t> h_emulated;
-    // per pass slot: head-hit flags (head_detect_kernel), host records, status
+    // per pass slot: head-hit flags (seg_count_head_kernel), host records, status
     HostBuf<uint32_t> hp_head[2];
     HostBuf<up_region> hp_regions[2];
     HostBuf<uint32_t> hp_counts[2];
@@ -812,18 +812,25 @@ static int check_runnable(up_ctx *c) {  // the parallel scan
 // Quirk Q1: units whose pooled hits include a position <= bw are replayed
 // by the exact state machine (emulate.hip); their early regions replace the
 // parallel path's, and the merged list moves to the host.
-static int launch_head_detect(up_ctx *c, int slot) {
+// K2a (segment counts of every strip) + quirk-Q1 head detection (units with
+// pooled tags at positions <= bw, misc/peakcall.cpp:177-183) in one launch
+static int launch_seg_count_head(up_ctx *c, int slot) {
     const uint32_t nu = (uint32_t)c->units.size();
+    const uint32_t ns = c->nstrips;
+    const uint32_t nsb = (ns + kSegBlock - 1) / kSegBlock;
     HIPCHK(c->d_head.ensure(nu));
     HIPCHK(c->hp_head[slot].ensure(nu));
+    if (c->p.bw > kSegBlock) return UP_E_INTERNAL;  // one thread per head position
     if (pool_mode(c) == 2)
-        hipLaunchKernelGGL(head_detect_kernel<2>, dim3(nu), dim3(128), 0, c->stream, c->d_units.p,
-                           (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw,
-                           c->d_head.p, c->hp_head[slot].dev);
+        hipLaunchKernelGGL(seg_count_head_kernel<2>, dim3(nsb + nu), dim3(kSegBlock), 0, c->stream, c->d_info.p,
+                           c->d_cnt.p, c->d_bsum.p, ns, nsb, c->d_units.p, (int)c->p.n_samples,
+                           (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw, c->d_head.p,
+                           c->hp_head[slot].dev);
     else
-        hipLaunchKernelGGL(head_detect_kernel<1>, dim3(nu), dim3(128), 0, c->stream, c->d_units.p,
-                           (int)c->p.n_samples, (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw,
-                           c->d_head.p, c->hp_head[slot].dev);
+        hipLaunchKernelGGL(seg_count_head_kernel<1>, dim3(nsb + nu), dim3(kSegBlock), 0, c->stream, c->d_info.p,
+                           c->d_cnt.p, c->d_bsum.p, ns, nsb, c->d_units.p, (int)c->p.n_samples,
+                           (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw, c->d_head.p,
+                           c->hp_head[slot].dev);
     HIPCHK(hipGetLastError());
     return UP_OK;
 }
@@ -1114,8 +1121,7 @@ static int launch_pass(up_ctx *c, int slot) {
 #endif
     if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[2], c->stream));
     unsigned long long *thdr = (unsigned long long *)ps.target;
-    hipLaunchKernelGGL(seg_count_kernel, dim3(nsb), dim3(kSegBlock), 0, c->stream, c->d_info.p, c->d_cnt.p,
-                       c->d_bsum.p, ns);
+    if (int r = launch_seg_count_head(c, slot)) return r;
     hipLaunchKernelGGL(seg_compact_kernel, dim3(nsb), dim3(kSegBlock), 0, c->stream, c->d_units.p,
                        (uint32_t)c->units.size(), c->d_info.p, c->d_cnt.p, c->d_bsum.p, c->d_rec.p,
                        c->d_ovf_rec.p, c->ovf_cap, c->d_starts.p, c->d_ends.p, c->d_runit.p, c->d_peak_pos.p,
@@ -1140,8 +1146,6 @@ static int launch_pass(up_ctx *c, int slot) {
     dispatch_stats(c, P, std::max<uint64_t>(c->last_nreg, 1024));
     HIPCHK(hipGetLastError());
     if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[4], c->stream));
-    int r = launch_head_detect(c, slot);
-    if (r) return r;
     HIPCHK(hipEventRecord(ps.done, c->stream));
     return UP_OK;
 }

@@ -387,9 +387,10 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
 
 // head-hit detection: any pooled countSum != 0 at positions 1..bw
 template <int POOL>
-__global__ void head_detect_kernel(const UnitDesc *units, int S, int nnc, const int32_t *nc,
-                                   const double *coef, int bw, uint32_t *head, uint32_t *mirror) {
-    const UnitDesc U = units[blockIdx.x];
+__device__ __forceinline__ void head_detect_unit(const UnitDesc *units, uint32_t unit, int S, int nnc,
+                                                 const int32_t *nc, const double *coef, int bw,
+                                                 uint32_t *head, uint32_t *mirror) {
+    const UnitDesc U = units[unit];
     const int p = 1 + (int)threadIdx.x;
     uint32_t hit = 0;
     if (p <= bw && (uint32_t)p <= U.len) {
@@ -406,9 +407,23 @@ __global__ void head_detect_kernel(const UnitDesc *units, int S, int nnc, const 
     }
     const uint32_t v = __syncthreads_or(hit) ? 1u : 0u;
     if (threadIdx.x == 0) {
-        head[blockIdx.x] = v;
-        if (mirror) mirror[blockIdx.x] = v;  // mapped host copy: no read-back copy
+        head[unit] = v;
+        if (mirror) mirror[unit] = v;  // mapped host copy: no read-back copy
     }
+}
+
+// K2a with the head detection in its trailing blocks (one block per unit;
+// threads 0..bw-1 = positions 1..bw): one launch fewer per pass
+template <int POOL>
+__global__ void __launch_bounds__(kSegBlock) seg_count_head_kernel(
+    const uint64_t *__restrict__ info, uint64_t *__restrict__ cnt, uint64_t *__restrict__ bsum,
+    uint32_t n, uint32_t nsb, const UnitDesc *units, int S, int nnc, const int32_t *nc,
+    const double *coef, int bw, uint32_t *head, uint32_t *mirror) {
+    if (blockIdx.x >= nsb) {  // block-uniform
+        head_detect_unit<POOL>(units, blockIdx.x - nsb, S, nnc, nc, coef, bw, head, mirror);
+        return;
+    }
+    seg_count_block(info, cnt, bsum, n);
 }
 
 }  // namespace upk

@@ -852,9 +852,8 @@ __device__ __forceinline__ uint64_t block_sum_u64(uint64_t v, uint64_t *red) {
 }
 
 // K2a: per-strip counts and one packed total per 256 strips
-__global__ void __launch_bounds__(kSegBlock) seg_count_kernel(const uint64_t *__restrict__ info,
-                                                              uint64_t *__restrict__ cnt,
-                                                              uint64_t *__restrict__ bsum, uint32_t n) {
+__device__ __forceinline__ void seg_count_block(const uint64_t *__restrict__ info, uint64_t *__restrict__ cnt,
+                                                uint64_t *__restrict__ bsum, uint32_t n) {
     __shared__ uint64_t red[4];
     const uint32_t i = blockIdx.x * kSegBlock + threadIdx.x;
     uint64_t c = 0;
