@@ -155,9 +155,10 @@ int up_run(up_ctx *ctx, uint64_t *n_regions);
  * change while a pass is in flight (UP_E_STATE). */
 int up_run_async(up_ctx *ctx);
 int up_run_wait(up_ctx *ctx, uint64_t *n_regions);
-/* device timing of passes: 0 = wall time only, 1 = + K1a (HIP events around
- * the streaming kernel), 2 = every phase (default).  Each event pair costs a
- * few microseconds of idle GPU between kernels. */
+/* device timing of passes launched from now on (passes in flight keep
+ * theirs): 0 = wall time only, 1 = + K1a (HIP events around the streaming
+ * kernel), 2 = every phase (default).  Each event pair costs a few
+ * microseconds of idle GPU between kernels. */
 int up_set_timing(up_ctx *ctx, int level);
 /* Copy region records (unit-major, left-ascending) and optionally the
  * per-sample exptSums [n][S]. */

@@ -133,6 +133,7 @@ struct up_ctx {
         uint64_t target_cap = 0;
         uint64_t cap = 0;            // reg_cap at launch
         uint32_t ovf_cap = 0;
+        int tl = 0;                  // timing level at launch
         std::chrono::steady_clock::time_point t0;
         hipEvent_t ev[5] = {};       // K1a begin, K1a end, K1b end, K2 end, K3 end
         hipEvent_t done = nullptr;
@@ -1110,6 +1111,7 @@ static int launch_pass(up_ctx *c, int slot) {
     }
 #endif
     const int tl = c->timing;
+    ps.tl = tl;
     if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[0], c->stream));
     dispatch_scan<false, kModeScreen>(c, SP, 0, ns);   // K1a: stream + screen
     HIPCHK(hipGetLastError());
@@ -1239,7 +1241,7 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
     c->last_nreg = nreg;
     int r = replay_head_hits(c, slot);
     if (r) return fail(r);
-    const int tl = c->timing;
+    const int tl = ps.tl;
     float a = 0, b = 0, d = 0, x = 0;
     if (tl >= 1) (void)hipEventElapsedTime(&a, ps.ev[0], ps.ev[1]);
     if (tl >= 2) {
@@ -1316,8 +1318,7 @@ int up_run(up_ctx *c, uint64_t *n_regions) {
 
 int up_set_timing(up_ctx *c, int level) {
     if (!c || level < 0 || level > 2) return UP_E_ARG;
-    if (busy(c)) return UP_E_STATE;
-    c->timing = level;
+    c->timing = level;  // passes already in flight keep the level they were launched with
     return UP_OK;
 }
 
