@@ -93,8 +93,6 @@ struct HostBuf {
 struct up_ctx {
     int dev = 0;
     hipStream_t stream = nullptr;
-    hipStream_t cstream = nullptr;   // record copies (device staging -> host records)
-    bool stage_records = false;      // UNIPEAK_STAGE=1: K3 writes device staging, a DMA copy delivers (A/B: within noise)
     bool have_params = false;
     up_params p{};
     std::vector<uint8_t> ctl;
@@ -136,7 +134,6 @@ struct up_ctx {
         uint64_t cap = 0;            // reg_cap at launch
         uint32_t ovf_cap = 0;
         int tl = 0;                  // timing level at launch
-        hipEvent_t k3done = nullptr; // K3 finished (the record copy waits for it)
         std::chrono::steady_clock::time_point t0;
         hipEvent_t ev[5] = {};       // K1a begin, K1a end, K1b end, K2 end, K3 end
         hipEvent_t done = nullptr;
@@ -164,7 +161,6 @@ struct up_ctx {
     // per pass slot: head-hit flags (seg_count_head_kernel), host records, status
     HostBuf<uint32_t> hp_head[2];
     HostBuf<up_region> hp_regions[2];
-    DevBuf<uint8_t> d_recstage[2];   // per pass slot: K3's records before the copy to host
     HostBuf<uint32_t> hp_counts[2];
     HostBuf<unsigned long long> hp_status[2];
     DevBuf<uint64_t> d_bsum;
@@ -246,13 +242,10 @@ int up_open(int hip_device, up_ctx **out) {
     c->dev = hip_device;
     HIPCHK(hipSetDevice(hip_device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
-    if (const char *e = getenv("UNIPEAK_STAGE")) c->stage_records = e[0] == '1';
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     for (auto &ps : c->pass) {
         for (auto &e : ps.ev) HIPCHK(hipEventCreate(&e));
         HIPCHK(hipEventCreateWithFlags(&ps.done, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&ps.k3done, hipEventDisableTiming));
     }
     for (auto &e : c->scat_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     *out = c;
@@ -276,7 +269,6 @@ void up_close(up_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->stream);
-    (void)hipStreamSynchronize(c->cstream);
     free_units(c);
     drop_target(c);
     for (void *h : c->host_regs) (void)hipHostUnregister(h);
@@ -296,8 +288,6 @@ void up_close(up_ctx *c) {
         c->hp_regions[k].release(); c->hp_counts[k].release(); c->hp_status[k].release(); c->hp_head[k].release();
         for (auto &e : c->pass[k].ev) (void)hipEventDestroy(e);
         (void)hipEventDestroy(c->pass[k].done);
-        (void)hipEventDestroy(c->pass[k].k3done);
-        c->d_recstage[k].release();
     }
     c->d_bsum.release();
     for (auto &e : c->scat_ev) (void)hipEventSynchronize(e);
@@ -306,7 +296,6 @@ void up_close(up_ctx *c) {
     c->d_wscreen.release(); c->d_stage.release(); c->d_dbg.release(); c->d_pack_ovf.release(); c->d_pack_n.release();
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
-    (void)hipStreamDestroy(c->cstream);
     delete c;
 }
 
@@ -1148,25 +1137,14 @@ static int launch_pass(up_ctx *c, int slot) {
     P.peak_pos = c->d_peak_pos.p;
     P.peak_val = c->d_peak_val.p;
     P.spk = c->d_spk.p;
-    // Records that end in host memory are written by K3 into a device staging
-    // area and delivered by one DMA copy on the copy stream (K3 writing them
-    // across PCIe itself took 0.103 instead of 0.067 ms on hg19); the copy
-    // overlaps the next pass, and the pass completes when it lands.
-    const bool staged = c->stage_records && (!ps.target || ps.target_hostp);
-    const uint64_t area = ps.target ? ps.target_cap : cap + 1;  // records area stride of the layout
-    uint8_t *stage = nullptr;
-    if (staged) {
-        HIPCHK(c->d_recstage[slot].ensure(area * (sizeof(up_region) + 4ull * S)));
-        stage = c->d_recstage[slot].p;
-    }
+    // K3 writes the records straight into mapped pinned host memory (or the
+    // caller's record target).  Staging them in device memory and delivering
+    // them with a DMA copy on a second stream measured within run-to-run
+    // noise, so there is one delivery path.
     if (ps.target) {  // records into the caller's buffer instead
         P.cap = std::min<uint64_t>(cap, ps.target_cap);
-        uint8_t *base = staged ? stage : ps.target + 8;
-        P.out = (up_region *)base;
-        P.out_counts = (uint32_t *)(base + ps.target_cap * sizeof(up_region));
-    } else if (staged) {
-        P.out = (up_region *)stage;
-        P.out_counts = (uint32_t *)(stage + area * sizeof(up_region));
+        P.out = (up_region *)(ps.target + 8);
+        P.out_counts = (uint32_t *)(ps.target + 8 + ps.target_cap * sizeof(up_region));
     } else {
         P.out = c->hp_regions[slot].dev;
         P.out_counts = c->hp_counts[slot].dev;
@@ -1174,23 +1152,7 @@ static int launch_pass(up_ctx *c, int slot) {
     dispatch_stats(c, P, std::max<uint64_t>(c->last_nreg, 1024));
     HIPCHK(hipGetLastError());
     if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[4], c->stream));
-    if (!staged) {
-        HIPCHK(hipEventRecord(ps.done, c->stream));
-        return UP_OK;
-    }
-    HIPCHK(hipEventRecord(ps.k3done, c->stream));
-    HIPCHK(hipStreamWaitEvent(c->cstream, ps.k3done, 0));
-    if (ps.target) {  // [target_cap records][P.cap x S counts] after the 8-byte header K2b wrote
-        HIPCHK(hipMemcpyAsync((uint8_t *)ps.target_hostp + 8, stage,
-                              ps.target_cap * sizeof(up_region) + P.cap * 4ull * S, hipMemcpyDeviceToHost,
-                              c->cstream));
-    } else {
-        HIPCHK(hipMemcpyAsync(c->hp_regions[slot].p, stage, cap * sizeof(up_region), hipMemcpyDeviceToHost,
-                              c->cstream));
-        HIPCHK(hipMemcpyAsync(c->hp_counts[slot].p, stage + area * sizeof(up_region), cap * 4ull * S,
-                              hipMemcpyDeviceToHost, c->cstream));
-    }
-    HIPCHK(hipEventRecord(ps.done, c->cstream));
+    HIPCHK(hipEventRecord(ps.done, c->stream));
     return UP_OK;
 }
 
@@ -1214,7 +1176,6 @@ int up_run_async(up_ctx *c) {
     }
     if ((r = launch_pass(c, slot))) {
         (void)hipStreamSynchronize(c->stream);
-        (void)hipStreamSynchronize(c->cstream);
         c->seq_done = c->seq_launched;  // drop whatever was in flight
         return r;
     }
@@ -1241,7 +1202,6 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
     }
     auto fail = [&](int rc) {
         (void)hipStreamSynchronize(c->stream);
-        (void)hipStreamSynchronize(c->cstream);
         c->seq_done = c->seq_launched;
         return rc;
     };
@@ -1379,10 +1339,8 @@ int up_get_regions(up_ctx *c, up_region *out, uint32_t *counts, size_t cap) {
 }
 
 static void drop_target(up_ctx *c) {
-    if (c->target_host && busy(c)) {  // a pass (or its record copy) may still write it
+    if (c->target_host && busy(c))  // a pass in flight may still write it
         (void)hipStreamSynchronize(c->stream);
-        (void)hipStreamSynchronize(c->cstream);
-    }
     if (c->target_host) (void)hipHostUnregister(c->target_host);
     c->target_host = nullptr;
     c->target = nullptr;
