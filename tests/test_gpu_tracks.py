@@ -1,6 +1,7 @@
-"""The uint8 track layout and K1's integer screen against
-the oracle: counts >= 128 (screen escape) and >= 255 (overflow table) at
-peaks and in the background, thresholds from "almost everything is a region"
+"""The 4-bit track layout and K1's integer screen against
+the oracle: counts >= 8 (the screen sends the chunk to the exact path) and
+>= 15 (escape nibble, overflow table) at peaks and in the background, with
+counts on both sides of each boundary, thresholds from "almost everything is a region"
 to "almost nothing is", every bandwidth class of the screen window, scaled
 pooling with large and negative coefficients, and device-resident input
 through up_unit_pack."""
@@ -25,7 +26,8 @@ def with_big_counts(rng, pos, cnt, n, lo, hi):
     return p, np.array([dense[int(x)] for x in p], np.uint32).reshape(len(p), S)
 
 
-@pytest.mark.parametrize("lo,hi", [(128, 255), (255, 256), (255, 100_000), (1 << 20, 1 << 24)])
+@pytest.mark.parametrize("lo,hi", [(6, 10), (13, 18), (15, 16), (128, 255), (255, 256), (255, 100_000),
+                                   (1 << 20, 1 << 24)])
 def test_large_counts_exact(gpu_lib, oracle, lo, hi):
     rng = np.random.default_rng(lo)
     length, bw, bg = 200_000, 50, 0.003
@@ -50,16 +52,17 @@ def test_large_counts_multi_sample_controls(gpu_lib, oracle):
 
 
 def test_tag_total_counts_escapes(gpu_lib):
-    pos = np.array([10, 20, 30, 40], np.uint32)
-    cnt = np.array([1, 254, 255, 70_000], np.uint32)
+    pos = np.array([10, 11, 20, 30, 39, 40], np.uint32)
+    cnt = np.array([1, 14, 254, 15, 7, 70_000], np.uint32)
     with gpu_lib.Lib(0) as g:
         g.set_params(50, 1, 0.003)
         u = g.add_unit(1000)
         g.scatter(u, 0, 0, pos, cnt)
         assert g.tag_total(u, 0, 0) == int(cnt.sum())
-        # overwrite: the escape at 40 becomes a plain byte, 20 becomes an escape
-        g.scatter(u, 0, 0, np.array([20, 40], np.uint32), np.array([999, 3], np.uint32))
-        assert g.tag_total(u, 0, 0) == 1 + 999 + 255 + 3
+        # overwrite: the escape at 40 becomes a plain nibble, 11 becomes an
+        # escape, 39 (the other nibble of 40's byte) is cleared
+        g.scatter(u, 0, 0, np.array([11, 39, 40], np.uint32), np.array([999, 0, 3], np.uint32))
+        assert g.tag_total(u, 0, 0) == 1 + 999 + 254 + 15 + 3
 
 
 @pytest.mark.parametrize("thr", [0.05, 1.0, 25.0, 400.0])

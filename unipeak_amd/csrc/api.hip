@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <vector>
 
 #include "../../include/unipeak_hip.h"
@@ -25,13 +26,13 @@ struct Unit {
     uint32_t len = 0;
     int32_t nstrands = 1;
     int32_t buffer = 0;
-    uint8_t *dptr = nullptr;   // uint8 tracks (kernels.h)
+    uint8_t *dptr = nullptr;   // 4-bit tracks (kernels.h)
     uint64_t stride = 0;       // bytes per track
     uint32_t nstrips = 0;
     uint32_t strip0 = 0;
     uint32_t last_override = 0;
     bool has_override = false;
-    // counts >= 255 per track: position -> count (authoritative copy)
+    // counts >= kEsc per track: position -> count (authoritative copy)
     std::vector<std::map<uint32_t, uint32_t>> ovf;
     uint64_t *d_ovf = nullptr;     // uploaded entries, sorted by (track, pos)
     uint32_t *d_ovf_off = nullptr; // [ntracks + 1]
@@ -92,6 +93,7 @@ struct HostBuf {
 
 struct up_ctx {
     int dev = 0;
+    int ncu = 0;                     // compute units of the device
     hipStream_t stream = nullptr;
     bool have_params = false;
     up_params p{};
@@ -115,7 +117,8 @@ struct up_ctx {
     DevBuf<uint64_t> d_info;
     DevBuf<uint32_t> d_rec, d_lastnz, d_ovf_count, d_ovf_rec, d_unit_last;
     DevBuf<uint64_t> d_cnt, d_nreg;
-    DevBuf<uint32_t> d_starts, d_ends, d_runit, d_peak_pos, d_xlist, d_xcount;
+    DevBuf<uint32_t> d_starts, d_ends, d_runit, d_peak_pos, d_xlist, d_xcount, d_xwcount, d_xref;
+    uint32_t k1a_waves = 0, k1a_xcap = 0;  // grid and per-wave stash size of the last K1a launch
     DevBuf<double> d_peak_val;
     DevBuf<uint64_t> d_spk;          // K1 per-strip partial peaks (ScanParams::spk)
     uint32_t ovf_cap = 256;
@@ -241,6 +244,7 @@ int up_open(int hip_device, up_ctx **out) {
     up_ctx *c = new up_ctx();
     c->dev = hip_device;
     HIPCHK(hipSetDevice(hip_device));
+    HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     for (auto &ps : c->pass) {
@@ -278,6 +282,7 @@ void up_close(up_ctx *c) {
     c->d_cnt.release(); c->d_nreg.release();
     c->d_starts.release(); c->d_ends.release(); c->d_runit.release();
     c->d_peak_pos.release(); c->d_peak_val.release(); c->d_xlist.release(); c->d_xcount.release();
+    c->d_xwcount.release(); c->d_xref.release();
     c->d_spk.release();
     c->d_head.release(); c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
@@ -370,11 +375,12 @@ int up_set_params(up_ctx *c, const up_params *p) {
 }
 
 // track geometry (bytes): positions 1..len plus the scan domain up to
-// len+bw (Q16), rounded to whole strips, with kPad zero bytes on both sides
+// len+bw (Q16), rounded to whole strips, two positions per byte, with
+// kPadBytes zero bytes on both sides
 static uint64_t unit_stride(uint32_t len) {
     const uint64_t dom = (uint64_t)len + kMaxBw + 1;
     const uint64_t strips = (dom + kStrip - 1) / kStrip;
-    return (uint64_t)kPad + strips * kStrip + kPad;
+    return (uint64_t)kPadBytes + strips * kStripBytes + kPadBytes;
 }
 
 int up_add_unit(up_ctx *c, uint32_t len, int32_t nstrands, int32_t buffer_id, uint32_t *unit_id) {
@@ -427,7 +433,7 @@ static int check_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample
     return UP_OK;
 }
 
-// dense device uint32 counts -> the track (uint8 + overflow table)
+// dense device uint32 counts -> the track (4-bit + overflow table)
 static int pack_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, const uint32_t *src) {
     Unit &u = c->units[unit];
     const uint64_t len = u.len;
@@ -437,7 +443,7 @@ static int pack_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample,
     for (int attempt = 0; attempt < 2; ++attempt) {
         HIPCHK(c->d_pack_ovf.ensure(cap));
         HIPCHK(hipMemsetAsync(c->d_pack_n.p, 0, 4, c->stream));
-        const uint64_t groups = (len + 3) / 4;
+        const uint64_t groups = (len + 7) / 8;  // 8 positions (one dword) per thread
         hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, c->stream,
                            track_ptr(c, unit, strand, sample), src, len, c->d_pack_ovf.p, c->d_pack_n.p, cap);
         HIPCHK(hipGetLastError());
@@ -481,7 +487,7 @@ int up_unit_scatter(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, s
     for (size_t i = 0; i < n; ++i)
         if (pos[i] == 0 || pos[i] > len) return UP_E_ARG;
     HIPCHK(hipSetDevice(c->dev));
-    {   // escapes: the host map holds every count >= 255 of the track
+    {   // escapes: the host map holds every count >= kEsc of the track
         Unit &u = c->units[unit];
         auto &m = u.ovf[(size_t)strand * c->p.n_samples + sample];
         for (size_t i = 0; i < n; ++i) {
@@ -707,23 +713,59 @@ static ScanParams scan_params(up_ctx *c) {
     P.ovf_rec = c->d_ovf_rec.p;
     P.ovf_cap = c->ovf_cap;
     P.xlist = c->d_xlist.p;
+    P.xwcount = c->d_xwcount.p;
+    P.xref = c->d_xref.p;
     P.xcount = c->d_xcount.p;
     P.spk = c->d_spk.p;
     return P;
 }
 
+// Workgroups of `kernel` (256 threads, `lds` bytes of dynamic LDS) that are
+// resident on the whole device at once.  The grid-stride kernels launch
+// exactly this many: a larger grid leaves its last workgroups waiting for a
+// slot and finishing their share of the work list after everyone else (a
+// tail of up to one whole per-workgroup share).
+static uint32_t resident_blocks(const up_ctx *c, const void *kernel, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::pair<const void *, size_t>, int> per_cu;
+    int n = 0;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = per_cu.find({kernel, lds});
+        if (it != per_cu.end()) {
+            n = it->second;
+        } else {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, 256, lds) != hipSuccess || n < 1) n = 1;
+            per_cu[{kernel, lds}] = n;
+        }
+    }
+    return (uint32_t)n * (uint32_t)(c->ncu > 0 ? c->ncu : 256);
+}
+
 template <int NH, int POOL, bool ND, bool PROF, int MODE>
 static void launch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e) {
-    uint32_t blocks;
+    const size_t lds = MODE == kModeScreen ? kScreenLds : MODE == kModeExact ? kExactLds : kScanLds;
+    const void *k = (const void *)scan_kernel<NH, POOL, ND, PROF, MODE>;
+    uint32_t blocks = resident_blocks(c, k, lds);
     if (MODE == kModeExact) {
-        blocks = 2048;  // grid-stride over the device-side work-list count
+        // K1b: grid-stride over the device-side work-list count; twice the
+        // resident grid measured better (the 8-GPU plan's rank: 57 vs 82 us):
+        // a workgroup that retires early hands its slot to one whose waves
+        // start at later (cheaper, single-block) items
+        blocks *= 2;
     } else {
-        const uint32_t waves = e - b;
-        blocks = (waves + 3) / 4;
-        if (blocks > 2048) blocks = 2048;
+        const uint32_t need = (e - b + 3) / 4;  // one wave per strip at most
+        if (need < blocks) blocks = need;
+        if (blocks > kMaxK1aWaves / 4) blocks = kMaxK1aWaves / 4;
         if (blocks == 0) return;
     }
-    const size_t lds = MODE == kModeScreen ? kScreenLds : MODE == kModeExact ? kExactLds : kScanLds;
+    if (MODE == kModeScreen) {  // per-wave work-list stash regions (ScanParams::xlist)
+        ScanParams Q = P;
+        c->k1a_waves = 4 * blocks;
+        c->k1a_xcap = Q.xcap = (e - b + c->k1a_waves - 1) / c->k1a_waves;
+        hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF, MODE>), dim3(blocks), dim3(256), lds, c->stream, Q, b, e);
+        return;
+    }
     hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF, MODE>), dim3(blocks), dim3(256), lds, c->stream, P, b, e);
 }
 
@@ -773,15 +815,15 @@ static void dispatch_stats(up_ctx *c, const StatParams &P, uint64_t nreg) {
     const int nh = P.bw <= 63 ? 1 : 2;
     const int pool = pool_mode(c);
     const bool nd = c->p.nondir != 0;
-    uint64_t blocks = (nreg + 3) / 4;
-    if (blocks > 4096) blocks = 4096;
-    if (blocks == 0) return;
     const size_t lds = kStatLds;
-#define UPK_ST(NH, PL, ND)                                                                   \
-    if (nh == NH && pool == PL && nd == ND) {                                                \
-        hipLaunchKernelGGL((stats_kernel<NH, PL, ND>), dim3((unsigned)blocks), dim3(256), lds, \
-                           c->stream, P);                                                     \
-        return;                                                                              \
+#define UPK_ST(NH, PL, ND)                                                                       \
+    if (nh == NH && pool == PL && nd == ND) {                                                    \
+        uint64_t blocks = std::min<uint64_t>((nreg + 3) / 4,                                     \
+                                             resident_blocks(c, (const void *)stats_kernel<NH, PL, ND>, lds)); \
+        if (blocks == 0) return;                                                                 \
+        hipLaunchKernelGGL((stats_kernel<NH, PL, ND>), dim3((unsigned)blocks), dim3(256), lds,     \
+                           c->stream, P);                                                         \
+        return;                                                                                  \
     }
     UPK_ST(1, 0, false) UPK_ST(1, 1, false) UPK_ST(1, 2, false)
     UPK_ST(1, 0, true) UPK_ST(1, 1, true) UPK_ST(1, 2, true)
@@ -1071,7 +1113,9 @@ static int launch_pass(up_ctx *c, int slot) {
     const uint32_t nsb = (ns + kSegBlock - 1) / kSegBlock;
     HIPCHK(c->d_info.ensure(ns));
     HIPCHK(c->d_rec.ensure((size_t)ns * kRecStride));
-    HIPCHK(c->d_xlist.ensure((size_t)ns * kXEntry));
+    HIPCHK(c->d_xlist.ensure(((size_t)ns + kMaxK1aWaves) * kXEntry));  // K1a stash regions
+    HIPCHK(c->d_xwcount.ensure(2 * kMaxK1aWaves));
+    HIPCHK(c->d_xref.ensure(ns));
     HIPCHK(c->d_spk.ensure((size_t)ns * 4));
     HIPCHK(c->d_cnt.ensure(ns));
     HIPCHK(c->d_bsum.ensure(nsb));
@@ -1113,9 +1157,15 @@ static int launch_pass(up_ctx *c, int slot) {
     const int tl = c->timing;
     ps.tl = tl;
     if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[0], c->stream));
+    c->k1a_waves = 0;
     dispatch_scan<false, kModeScreen>(c, SP, 0, ns);   // K1a: stream + screen
     HIPCHK(hipGetLastError());
     if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[1], c->stream));
+    if (c->k1a_waves) {  // K1x: list the stashed work-list entries for K1b
+        hipLaunchKernelGGL(xref_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_xwcount.p, c->k1a_waves,
+                           c->k1a_xcap, c->d_xref.p, c->d_xcount.p);
+        HIPCHK(hipGetLastError());
+    }
     dispatch_scan<false, kModeExact>(c, SP, 0, ns);    // K1b: exact blocks
     HIPCHK(hipGetLastError());
 #ifdef UPK_EXP_K1B_TWICE  // experiment: a second (idempotent) K1b over warm caches/TLBs

@@ -2,13 +2,15 @@
 // kernels (kernels.hip) and the C-ABI implementation (api.hip).
 //
 // HBM layout (DESIGN.md "Data layout"): every (unit, strand, sample) track is
-// a dense uint8 array of tag counts; position p (1-based) of a track lives at
-// byte kPad + p - 1, with kPad zero bytes in front and at least kPad behind
-// the unit's scan domain [1, len + bw], so every halo load is in bounds and
-// reads zeros outside the contig.  A count >= 255 is stored as the escape
-// byte 255 and its value in the unit's overflow table (entries
-// (pos << 32 | count), sorted by track then position).  Tracks of one unit
-// are contiguous: track(s, k) = base + (s * S + k) * stride bytes.
+// a dense array of 4-bit tag counts, two positions per byte: position p
+// (1-based) is nibble n = kPadPos + p - 1, i.e. bits 4*(n & 1) .. +3 of byte
+// n >> 1 (odd positions in the low nibble).  kPadPos zero positions (kPadBytes
+// bytes) sit in front and at least as many behind the unit's scan domain
+// [1, len + bw], so every halo load is in bounds and reads zeros outside the
+// contig.  A count >= 15 is stored as the escape nibble 15 and its value in
+// the unit's overflow table (entries (pos << 32 | count), sorted by track
+// then position).  Tracks of one unit are contiguous: track(s, k) = base +
+// (s * S + k) * stride bytes.
 #pragma once
 #include <stdint.h>
 
@@ -20,7 +22,9 @@ constexpr int kStrip = kStripWords * kWave;  // 16384 positions per wave task
 constexpr int kStepWords = 16;      // words per block (= one 1024-position dwordx4 wave load)
 constexpr int kBlocks = kStripWords / kStepWords;  // 16 blocks per strip
 constexpr int kChunk = 16;          // positions per lane in the screening load (dwordx4)
-constexpr int kPad = 256;           // zero bytes before position 1 and after the domain
+constexpr int kPadBytes = 256;      // zero bytes before position 1 and after the domain
+constexpr int kPadPos = 2 * kPadBytes;  // the same padding in positions (nibbles)
+constexpr int kStripBytes = kStrip / 2;  // one strip of one track
 constexpr int kMaxBw = 127;         // register-resident halo: NH <= 2 words
 constexpr int kCap = 32;            // inline run records per strip (starts, ends each)
 constexpr int kOvfHalf = kStrip / 2 + 1;  // max starts (= max ends) of one strip
@@ -29,10 +33,11 @@ constexpr int kOvfHalf = kStrip / 2 + 1;  // max starts (= max ends) of one stri
 // inline per strip, kOvfHalf per spilled strip's overflow slot
 constexpr int kRecStride = 6 * kCap;
 constexpr int kOvfStride = 6 * kOvfHalf;
-constexpr uint32_t kEsc = 255;
+constexpr uint32_t kEsc = 15;       // escape nibble: the count lives in the overflow table
 constexpr int kXEntry = 2 + kWave / 2;  // strip, exact-block mask, 64 x 16-bit chunk masks
-constexpr int kModeFused = 0, kModeScreen = 1, kModeExact = 2;  // K1 variants      // escape byte: count lives in the overflow table
-constexpr uint32_t kBig = 1u << 22; // screen value of a chunk holding a byte >= 128
+constexpr int kMaxK1aWaves = 16384;     // K1a grid cap (stash regions)
+constexpr int kModeFused = 0, kModeScreen = 1, kModeExact = 2;  // K1 variants
+constexpr uint32_t kBig = 1u << 22; // screen value of a chunk holding a nibble >= 8
 
 struct UnitDesc {
     uint64_t base;      // device address of track (0, 0)
@@ -71,8 +76,16 @@ struct ScanParams {
     uint32_t *rec;          // [nstrips][kRecStride]: starts, ends, end peaks (0: unknown)
     uint32_t *ovf_count;
     uint32_t *ovf_rec;      // [ovf_cap][kOvfStride]
-    uint32_t *xlist;        // K1a -> K1b work list: [nstrips][kXEntry]
-    uint32_t *xcount;       // [2] entries listed from the front / from the back of xlist
+    // K1a -> K1b work list.  Every K1a wave stashes the entries of its strips
+    // that need exact blocks in its own xcap-entry region of xlist (multi-block
+    // strips from the front, single-block ones from the back) and their counts
+    // in xwcount -- no atomics on shared counters; xref_kernel then lists the
+    // stash indices (front entries first) in xref and the totals in xcount.
+    uint32_t *xlist;        // [K1a waves][xcap][kXEntry]
+    uint32_t *xwcount;      // [K1a waves][2]: front / back entries stashed
+    uint32_t *xref;         // [nstrips]: stash index of every listed entry
+    uint32_t *xcount;       // [2] front / back entries in xref
+    uint32_t xcap;          // stash entries per K1a wave
     uint64_t *spk;          // [nstrips][4]: peak (f+r bits, position) of the run open at
                             // the strip's first position ([0..1], written when it closes
                             // inside the strip) and of the run open at its last position

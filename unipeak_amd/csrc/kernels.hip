@@ -55,6 +55,18 @@ typedef const __attribute__((address_space(1))) uint32_t gu32;
 typedef const __attribute__((address_space(1))) uint8_t gu8;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+// read-only kernel inputs through the constant address space: a uniform
+// index then compiles to scalar loads (s_load, lgkmcnt) instead of vector
+// loads whose vmcnt waits would also wait for the streaming loads in flight
+#ifdef __HIP_DEVICE_COMPILE__
+#define UPK_CONST __attribute__((address_space(4)))
+#else
+#define UPK_CONST  // the host pass only type-checks the kernels
+#endif
+template <typename T>
+__device__ __forceinline__ const UPK_CONST T *cptr(const T *p) {
+    return (const UPK_CONST T *)p;
+}
 
 // window word storage: raw counts when the pooled count is the single
 // non-control sample's count, otherwise the FP64 pooled count
@@ -66,9 +78,20 @@ __device__ __forceinline__ double rl_cs(double v, int l) { return rl_d(v, l); }
 __device__ __forceinline__ bool nz(uint32_t v) { return v != 0u; }
 __device__ __forceinline__ bool nz(double v) { return v != 0.0; }
 
-// ---- track access (layout in kernels.h) ----
+// ---- track access (layout in kernels.h: 4-bit counts, two per byte) ----
 __device__ __forceinline__ gu8 *track_u8(const UnitDesc &U, int S, int strand, int sample) {
     return (gu8 *)U.base + ((uint64_t)strand * S + sample) * U.stride;
+}
+
+// nibble (stored count, escape 15) of position p, 1-based
+__device__ __forceinline__ uint32_t nib_at(gu8 *t, int64_t p) {
+    const int64_t n = kPadPos + p - 1;
+    return ((uint32_t)t[n >> 1] >> (4 * (uint32_t)(n & 1))) & 15u;
+}
+
+// sum of the eight 4-bit counts of a dword (v_dot8_u32_u4 against all-ones)
+__device__ __forceinline__ uint32_t nsum8(uint32_t x, uint32_t acc) {
+    return __builtin_amdgcn_udot8(x, 0x11111111u, acc, false);
 }
 
 // count >= 255: binary search of the track's overflow entries
@@ -88,7 +111,7 @@ __device__ __noinline__ uint32_t ovf_lookup(const UnitDesc &U, uint32_t track, u
 // exact count of (strand, sample) at position p (1-based)
 __device__ __forceinline__ uint32_t count_at(const UnitDesc &U, int S, int strand, int sample,
                                              int64_t p) {
-    const uint32_t b = track_u8(U, S, strand, sample)[kPad + p - 1];
+    const uint32_t b = nib_at(track_u8(U, S, strand, sample), p);
     return b == kEsc ? ovf_lookup(U, (uint32_t)(strand * S + sample), (uint32_t)p) : b;
 }
 
@@ -102,9 +125,14 @@ __device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], const UnitDesc &
                                            const double *coef) {
     uint32_t c[N];
     auto fetch = [&](int k) {
-        gu8 *t = track_u8(U, S, strand, nc[k]) + kPad + x0 - 1 + lane;
+        // lane's nibble n0 + 64w = byte (n0 >> 1) + 32w, same half for every w
+        const int64_t n0 = kPadPos + x0 - 1 + lane;
+        gu8 *t = track_u8(U, S, strand, nc[k]) + (n0 >> 1);
+        const uint32_t sh = 4 * (uint32_t)(n0 & 1);
 #pragma unroll
-        for (int w = 0; w < N; ++w) c[w] = t[64 * w];
+        for (int w = 0; w < N; ++w) c[w] = t[32 * w];
+#pragma unroll
+        for (int w = 0; w < N; ++w) c[w] = (c[w] >> sh) & 15u;
 #pragma unroll
         for (int w = 0; w < N; ++w)
             if (c[w] == kEsc)
@@ -184,31 +212,32 @@ __device__ __forceinline__ void next_hits(uint64_t &m, T v, int (&b)[kHB], doubl
     }
 }
 
-// Same as load_words, but the N*64 bytes of each track are fetched with
-// 16-byte lane loads (one 1 KiB wave load per 16 words) and turned into the
-// lane = position layout through this wave's LDS stage (N*64 <= 2048 bytes).
-// x0 - 1 + kPad must be 16-byte aligned.
+// Same as load_words, but the N*32 bytes of each track are fetched with
+// 16-byte lane loads (one 1 KiB wave load per 32 words) and turned into the
+// lane = position layout through this wave's LDS stage (N*32 <= 1024 bytes).
+// x0 - 1 must be a multiple of 64 (the bytes are then 16-byte aligned).
 template <int N, int POOL>
 __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const UnitDesc &U, int S, int strand,
                                                   int64_t x0, int lane, int nnc, const int32_t *nc,
                                                   const double *coef, uint8_t *stage) {
-    constexpr int NV = (N * 64 + 1023) / 1024;  // wave loads per track
+    constexpr int NV = (N * 32 + 1023) / 1024;  // wave loads per track
     uint32_t c[N];
     auto fetch = [&](int k) {
-        gu32x4 *t = (gu32x4 *)(track_u8(U, S, strand, nc[k]) + kPad + x0 - 1);
+        gu32x4 *t = (gu32x4 *)(track_u8(U, S, strand, nc[k]) + ((kPadPos + x0 - 1) >> 1));
         u32x4 v[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q)
-            if (64 * q + lane < N * 4) v[q] = t[64 * q + lane];
+            if (64 * q + lane < N * 2) v[q] = t[64 * q + lane];
         __builtin_amdgcn_wave_barrier();  // earlier readers of the stage are done
 #pragma unroll
         for (int q = 0; q < NV; ++q)
-            if (64 * q + lane < N * 4) *(u32x4 *)(stage + 16 * (64 * q + lane)) = v[q];
+            if (64 * q + lane < N * 2) *(u32x4 *)(stage + 16 * (64 * q + lane)) = v[q];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t sh = 4 * (uint32_t)(lane & 1);
 #pragma unroll
-        for (int w = 0; w < N; ++w) c[w] = stage[64 * w + lane];
+        for (int w = 0; w < N; ++w) c[w] = ((uint32_t)stage[32 * w + (lane >> 1)] >> sh) & 15u;
 #pragma unroll
         for (int w = 0; w < N; ++w)
             if (c[w] == kEsc)
@@ -288,8 +317,8 @@ struct WordLoop<K1, K1> {
     __device__ __forceinline__ static void run(F &&) {}
 };
 
-__device__ __forceinline__ uint32_t find_unit(const UnitDesc *units, uint32_t nunits,
-                                              uint32_t strip) {
+template <typename UP>
+__device__ __forceinline__ uint32_t find_unit(UP units, uint32_t nunits, uint32_t strip) {
     uint32_t lo = 0, hi = nunits;  // last unit with strip0 <= strip
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -413,7 +442,13 @@ __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], 
 // ballots and scattered into FP64 accumulators, so every position's sum
 // keeps the reference's order; flags give run boundaries.
 // ------------------------------------------------------------------------
-constexpr int kScrWords = 8 + kBlocks * kWave + 8;  // chunk sums of one strip + halos
+// chunk sums of one strip + halos, one pad word after every 16: chunk index
+// i lives at word i + i/16, so the reads below (lane l takes indices 16l ..
+// 16l + 31, the same offset on every lane) hit 64 different banks; unpadded,
+// that 16-word lane stride made every read a 16-way bank conflict
+constexpr int kScrIdx = 8 + kBlocks * kWave + 8;
+constexpr int kScrWords = kScrIdx + kScrIdx / 16 + 2;  // even: 8-byte aligned per wave
+__device__ __forceinline__ int scr_at(int i) { return i + (i >> 4); }
 constexpr size_t kScreenLds = kKTab * sizeof(double) + 4 * kScrWords * sizeof(uint32_t);
 constexpr size_t kScanLds = kScreenLds + 4 * kStepWords * kWave * sizeof(double);
 #ifndef UPK_XFRONT
@@ -422,30 +457,36 @@ constexpr size_t kScanLds = kScreenLds + 4 * kStepWords * kWave * sizeof(double)
 constexpr int kXFront = UPK_XFRONT;  // K1b work items with >= this many exact blocks go first
 constexpr size_t kExactLds = kKTab * sizeof(double) + 4 * kStepWords * kWave * sizeof(double);
 
-// chunk i (0..15) of this lane: window a[8+i-R .. 8+i+R] > wskip
+// chunks 16l .. 16l+15 of lane l whose window of +-R chunks sums to more
+// than wskip.  rd = this lane's row of the padded chunk-sum area (index
+// 16l + j, j = 0..31, holds chunk 16l + j - 8).  Most lanes hold a handful of
+// background tags: when no lane's whole span [16l - R, 16l + 15 + R] exceeds
+// wskip, no window can, and the sliding sums are skipped (wave-uniform).
 template <int R>
-__device__ __forceinline__ uint32_t screen_bits(const uint32_t (&a)[32], uint32_t wskip) {
+__device__ __forceinline__ uint32_t screen_bits(const uint32_t *rd, uint32_t wskip) {
+    uint32_t a[16 + 2 * R];  // chunks 16l - R .. 16l + 15 + R
+    uint32_t tot = 0;
+#pragma unroll
+    for (int j = 0; j < 16 + 2 * R; ++j) {
+        const int i = 8 - R + j;
+        a[j] = rd[i + (i >> 4)];
+    }
+#pragma unroll
+    for (int j = 0; j < 16 + 2 * R; ++j) tot += a[j];
+    if (__ballot(tot > wskip) == 0) return 0u;
+#ifdef UPK_EXP_NOFINE  // timing experiment (wrong results): no sliding window
+    if (tot != 0xDEADBEEFu) return 0u;
+#endif
     uint32_t W = 0;
 #pragma unroll
-    for (int j = 8 - R; j <= 8 + R; ++j) W += a[j];
+    for (int j = 0; j <= 2 * R; ++j) W += a[j];
     uint32_t m = W > wskip ? 1u : 0u;
 #pragma unroll
     for (int i = 1; i < 16; ++i) {
-        W += a[8 + i + R] - a[8 + i - 1 - R];
+        W += a[i + 2 * R] - a[i - 1];
         m |= (W > wskip ? 1u : 0u) << i;
     }
     return m;
-}
-
-__device__ __forceinline__ uint32_t sad4(u32x4 v, uint32_t acc) {
-    acc = __builtin_amdgcn_sad_u8(v.x, 0u, acc);
-    acc = __builtin_amdgcn_sad_u8(v.y, 0u, acc);
-    acc = __builtin_amdgcn_sad_u8(v.z, 0u, acc);
-    return __builtin_amdgcn_sad_u8(v.w, 0u, acc);
-}
-
-__device__ __forceinline__ bool has_big(u32x4 v) {
-    return ((v.x | v.y | v.z | v.w) & 0x80808080u) != 0u;
 }
 
 // MODE kModeScreen (K1a): stream + screen every strip; strips without exact
@@ -475,8 +516,14 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     constexpr int SW = kStepWords;
     constexpr int NWIN = SW + 2 * NH;
     using T = WinT<POOL>;
+    const auto *units = cptr(P.units);
+    const auto *ncs = cptr(P.nc);
     const int lane = threadIdx.x & 63;
-    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // wave-uniform by construction; readfirstlane tells the compiler, so the
+    // strip / unit / work-list indices derived from it live in SGPRs and the
+    // unit table is read with scalar loads (vector loads of it cost a
+    // dependent round trip behind the streaming loads on every strip)
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
     const int R = (bw + kChunk - 1) / kChunk;
     const int S = P.S;
@@ -490,11 +537,13 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 
     uint32_t cur = 0;
     bool have = false;
-    // K1b: multi-block entries were listed from the front, single-block ones
-    // from the back, so the first resident waves take the long items
+    constexpr int kLoads = kStripBytes / (kWave * 16);  // K1a wave loads per strip and track
+    // K1b: multi-block entries are listed first, single-block ones after
+    // them, so the first resident waves take the long items
     const uint32_t nfront = MODE == kModeExact ? P.xcount[0] : 0u;
     const uint32_t nback = MODE == kModeExact ? P.xcount[1] : 0u;
     uint32_t it_end = MODE == kModeExact ? nfront + nback : strip_end;
+    uint32_t xnf = 0, xnb = 0;  // K1a: entries this wave stashed (front / back)
     uint32_t it0 = (MODE == kModeExact ? 0u : strip_begin) + wave, istep = nwaves;
 #ifdef UPK_EXP_CONTIG
     if constexpr (MODE == kModeExact) {  // contiguous item ranges per wave (locality experiment)
@@ -512,72 +561,105 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         uint32_t mchunk = 0xFFFFu;
         uint32_t exact_blocks = 0xFFFFu;
         if constexpr (MODE == kModeExact) {
-            const uint32_t ei = it < nfront ? it : P.nstrips - nback + (it - nfront);
+            const uint32_t ei = cptr(P.xref)[it];
             const uint32_t *e = P.xlist + (uint64_t)ei * kXEntry;
-            strip = e[0];
-            exact_blocks = e[1] & 0xFFFFu;
+            const auto *es = cptr(e);  // the uniform words through scalar loads
+            strip = es[0];
+            const uint32_t e1 = es[1];
+            exact_blocks = e1 & 0xFFFFu;
             mchunk = (e[2 + (lane >> 1)] >> (16 * (lane & 1))) & 0xFFFFu;
             // K1a stored the unit with the entry (no dependent binary search)
-            cur = e[1] >> 16;
-            if (cur == 0xFFFFu) cur = find_unit(P.units, P.nunits, strip);
+            cur = e1 >> 16;
+            if (cur == 0xFFFFu) cur = find_unit(units, P.nunits, strip);
         } else {
-            if (!have) { cur = find_unit(P.units, P.nunits, strip); have = true; }
-            while (strip >= P.units[cur].strip0 + P.units[cur].nstrips) ++cur;
+            if (!have) { cur = find_unit(units, P.nunits, strip); have = true; }
+            while (strip >= units[cur].strip0 + units[cur].nstrips) ++cur;
         }
-        const UnitDesc U = P.units[cur];
+        const UnitDesc U = units[cur];
         const uint32_t local = strip - U.strip0;
         const int64_t p0 = 1 + (int64_t)local * kStrip;  // first position of the strip
 
         // ---- screen: which blocks can hold a flagged position ----
         if constexpr (!PROF && MODE != kModeExact) {
-            uint32_t cs[kBlocks];
-            uint32_t big = 0, hs = 0;
-            bool hbig = false;
+            // lane l of wave load q holds positions 2048q + 32l .. +31, i.e.
+            // chunks 128q + 2l (dwords x, y) and 128q + 2l + 1 (dwords z, w)
+            uint32_t cs[2 * kLoads];
+            uint32_t big = 0, hs0 = 0, hs1 = 0, hbig = 0;
+            // An escape nibble (15) stands for a count the screen does not
+            // know.  When wskip < 15 its chunk fails the screen anyway (sum
+            // >= 15 > wskip, every sample weight >= 1), so only higher
+            // thresholds need the explicit check (any nibble >= 8 -> exact).
+            const bool big_check = P.wskip >= kEsc;
 #pragma unroll
-            for (int k = 0; k < kBlocks; ++k) cs[k] = 0;
+            for (int k = 0; k < 2 * kLoads; ++k) cs[k] = 0;
             for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
                 for (int k = 0; k < P.nnc; ++k) {
-                    gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, P.nc[k]) + kPad + p0 - 1);
-                    u32x4 v[kBlocks];
+                    gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, ncs[k]) + ((kPadPos + p0 - 1) >> 1));
+                    u32x4 v[kLoads];
 #pragma unroll
-                    for (int bk = 0; bk < kBlocks; ++bk) v[bk] = __builtin_nontemporal_load(t + 64 * bk + lane);
+                    for (int q = 0; q < kLoads; ++q) v[q] = __builtin_nontemporal_load(t + 64 * q + lane);
+                    // halos: 8 chunks (64 bytes) on each side, two per lane
                     u32x4 hv = {0u, 0u, 0u, 0u};
-                    if (lane < 16) hv = t[lane < 8 ? lane - 8 : kBlocks * kWave + lane - 8];
-                    const uint32_t w = POOL == 2 ? P.wscreen[k] : 1u;
+                    if (lane < 8) hv = t[lane < 4 ? lane - 4 : kLoads * kWave + lane - 4];
+                    const uint32_t w = POOL == 2 ? cptr(P.wscreen)[k] : 1u;
 #pragma unroll
-                    for (int bk = 0; bk < kBlocks; ++bk) {
-                        const uint32_t x = sad4(v[bk], 0u);
-                        cs[bk] += POOL == 2 ? x * w : x;
-                        big |= has_big(v[bk]) ? (1u << bk) : 0u;
+                    for (int q = 0; q < kLoads; ++q) {
+                        const uint32_t a = nsum8(v[q].y, nsum8(v[q].x, 0u));
+                        const uint32_t b = nsum8(v[q].w, nsum8(v[q].z, 0u));
+                        cs[2 * q] += POOL == 2 ? a * w : a;
+                        cs[2 * q + 1] += POOL == 2 ? b * w : b;
+                        if (big_check) {
+                            big |= (((v[q].x | v[q].y) & 0x88888888u) ? 1u : 0u) << (2 * q);
+                            big |= (((v[q].z | v[q].w) & 0x88888888u) ? 1u : 0u) << (2 * q + 1);
+                        }
                     }
-                    const uint32_t hx = sad4(hv, 0u);
-                    hs += POOL == 2 ? hx * w : hx;
-                    hbig = hbig || has_big(hv);
+                    const uint32_t ha = nsum8(hv.y, nsum8(hv.x, 0u)), hb = nsum8(hv.w, nsum8(hv.z, 0u));
+                    hs0 += POOL == 2 ? ha * w : ha;
+                    hs1 += POOL == 2 ? hb * w : hb;
+                    if (big_check) {
+                        hbig |= ((hv.x | hv.y) & 0x88888888u) ? 1u : 0u;
+                        hbig |= ((hv.z | hv.w) & 0x88888888u) ? 2u : 0u;
+                    }
                 }
             }
+            // a chunk holding a count >= 8 (incl. the escape) goes exact
+#ifdef UPK_EXP_K1A_LOADONLY  // timing experiment: stream + chunk sums only
+            if constexpr (MODE == kModeScreen) {
+                uint32_t t = big;
 #pragma unroll
-            for (int bk = 0; bk < kBlocks; ++bk) scr[8 + kWave * bk + lane] = ((big >> bk) & 1u) ? kBig : cs[bk];
-            if (lane < 8) scr[lane] = hbig ? kBig : hs;
-            else if (lane < 16) scr[8 + kBlocks * kWave + lane - 8] = hbig ? kBig : hs;
+                for (int q = 0; q < 2 * kLoads; ++q) t += cs[q];
+                const uint64_t info = ((uint64_t)(local == 0) << 34) | ((uint64_t)(local + 1 == U.nstrips) << 35) |
+                                      ((uint64_t)(__ballot(t == 0xDEADBEEFu) != 0) << 40);
+                if (lane == 0) P.strip_info[strip] = info;
+                continue;
+            }
+#endif
+            // (an even index and the next one share a 16-word group: adjacent words)
+#pragma unroll
+            for (int q = 0; q < kLoads; ++q) {
+                uint32_t *d = scr + scr_at(8 + 128 * q + 2 * lane);
+                d[0] = ((big >> (2 * q)) & 1u) ? kBig : cs[2 * q];
+                d[1] = ((big >> (2 * q + 1)) & 1u) ? kBig : cs[2 * q + 1];
+            }
+            if (lane < 8) {
+                uint32_t *d = scr + scr_at(lane < 4 ? 2 * lane : 8 + kBlocks * kWave + 2 * (lane - 4));
+                d[0] = (hbig & 1u) ? kBig : hs0;
+                d[1] = (hbig & 2u) ? kBig : hs1;
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint32_t a[32];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint4 q = *(const uint4 *)(scr + 16 * lane + 4 * j);
-                a[4 * j] = q.x; a[4 * j + 1] = q.y; a[4 * j + 2] = q.z; a[4 * j + 3] = q.w;
-            }
+            const uint32_t *rd = scr + 17 * lane;  // index 16l + j = word 17l + j + j/16
             uint32_t m = 0;
             switch (R) {
-            case 1: m = screen_bits<1>(a, P.wskip); break;
-            case 2: m = screen_bits<2>(a, P.wskip); break;
-            case 3: m = screen_bits<3>(a, P.wskip); break;
-            case 4: m = screen_bits<4>(a, P.wskip); break;
-            case 5: m = screen_bits<5>(a, P.wskip); break;
-            case 6: m = screen_bits<6>(a, P.wskip); break;
-            case 7: m = screen_bits<7>(a, P.wskip); break;
-            default: m = screen_bits<8>(a, P.wskip); break;
+            case 1: m = screen_bits<1>(rd, P.wskip); break;
+            case 2: m = screen_bits<2>(rd, P.wskip); break;
+            case 3: m = screen_bits<3>(rd, P.wskip); break;
+            case 4: m = screen_bits<4>(rd, P.wskip); break;
+            case 5: m = screen_bits<5>(rd, P.wskip); break;
+            case 6: m = screen_bits<6>(rd, P.wskip); break;
+            case 7: m = screen_bits<7>(rd, P.wskip); break;
+            default: m = screen_bits<8>(rd, P.wskip); break;
             }
             const uint64_t lanes = __ballot(m != 0u);  // lane l covers chunks 16l..16l+15
             mchunk = m;
@@ -587,16 +669,20 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 exact_blocks |= ((lanes >> (4 * bk)) & 0xFull) ? (1u << bk) : 0u;
             // the next strip reuses scr only after every lane has read it
             __builtin_amdgcn_wave_barrier();
+#ifdef UPK_EXP_K1A_NOLIST  // timing experiment: no work-list entries (wrong results)
+            if (exact_blocks == 0xFFFFu && lane == 63) P.strip_info[strip] = mchunk;
+            exact_blocks = 0;
+#endif
         }
         if constexpr (MODE == kModeScreen) {
             if (exact_blocks == 0) {  // no run can touch this strip
                 const uint64_t info = ((uint64_t)(local == 0) << 34) | ((uint64_t)(local + 1 == U.nstrips) << 35);
                 if (lane == 0) P.strip_info[strip] = info;
             } else {
-                uint32_t slot = 0;
+                // into this wave's stash: multi-block strips from its front,
+                // single-block ones from its back (xref_kernel lists them)
                 const bool front = __builtin_popcount(exact_blocks) >= kXFront;
-                if (lane == 0) slot = front ? atomicAdd(P.xcount, 1u) : P.nstrips - 1u - atomicAdd(P.xcount + 1, 1u);
-                slot = rl_u(slot, 0);
+                const uint32_t slot = wave * P.xcap + (front ? xnf++ : P.xcap - 1u - xnb++);
                 uint32_t *e = P.xlist + (uint64_t)slot * kXEntry;
                 const uint32_t hi = (uint32_t)__shfl_down((int)mchunk, 1);
                 if ((lane & 1) == 0) e[2 + (lane >> 1)] = mchunk | (hi << 16);
@@ -820,6 +906,46 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                               ((uint64_t)(R_.slot != kInline) << 36);
         if (lane == 0) P.strip_info[strip] = info;
     }
+    if constexpr (MODE == kModeScreen) {
+        if (lane == 0) {
+            P.xwcount[2 * wave] = xnf;
+            P.xwcount[2 * wave + 1] = xnb;
+        }
+    }
+}
+
+// K1x: the K1a waves' stash counts -> xref (stash indices of the listed
+// entries, every front entry first) and the totals in xcount.  One block:
+// thread t owns K1a waves [t*per, (t+1)*per).
+__global__ void __launch_bounds__(1024) xref_kernel(const uint32_t *__restrict__ xwcount, uint32_t nw,
+                                                    uint32_t xcap, uint32_t *__restrict__ xref,
+                                                    uint32_t *__restrict__ xcount) {
+    __shared__ uint64_t sc[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nw + 1023) / 1024;
+    const uint32_t w0 = t * per, w1 = w0 + per < nw ? w0 + per : nw;
+    uint64_t mine = 0;  // front count | back count << 32 (totals < 2^32)
+    for (uint32_t w = w0; w < w1; ++w) mine += (uint64_t)xwcount[2 * w] | ((uint64_t)xwcount[2 * w + 1] << 32);
+    sc[t] = mine;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan
+        const uint64_t v = t >= o ? sc[t - o] : 0;
+        __syncthreads();
+        sc[t] += v;
+        __syncthreads();
+    }
+    const uint64_t tot = sc[1023];
+    const uint32_t nf = (uint32_t)tot;
+    uint32_t of = (uint32_t)(sc[t] - mine), ob = nf + (uint32_t)((sc[t] - mine) >> 32);
+    for (uint32_t w = w0; w < w1; ++w) {
+        const uint32_t a = xwcount[2 * w], b = xwcount[2 * w + 1];
+        for (uint32_t k = 0; k < a; ++k) xref[of++] = w * xcap + k;
+        for (uint32_t k = 0; k < b; ++k) xref[ob++] = w * xcap + xcap - 1 - k;
+    }
+    if (t == 0) {
+        xcount[0] = nf;
+        xcount[1] = (uint32_t)(tot >> 32);
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -943,15 +1069,19 @@ __global__ void __launch_bounds__(kSegBlock) seg_compact_kernel(
 // per-unit last add (the last position whose pooled count is nonzero): one
 // wave per strip finds its highest nonzero byte over the pooled tracks and
 // folds it into the unit's slot with atomicMax (out zeroed by the caller)
-__device__ __forceinline__ uint32_t top_byte(uint32_t x) {  // index of highest nonzero byte
-    return (uint32_t)(31 - __builtin_clz(x)) >> 3;
+__device__ __forceinline__ uint32_t top_nib(uint32_t x) {  // index of highest nonzero nibble
+    return (uint32_t)(31 - __builtin_clz(x)) >> 2;
 }
 
 __global__ void __launch_bounds__(256) unit_last_kernel(const UnitDesc *units, uint32_t nunits,
                                                         uint32_t nstrips, int S, int nnc,
                                                         const int32_t *nc, uint32_t *out) {
     const int lane = threadIdx.x & 63;
-    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // wave-uniform by construction; readfirstlane tells the compiler, so the
+    // strip / unit / work-list indices derived from it live in SGPRs and the
+    // unit table is read with scalar loads (vector loads of it cost a
+    // dependent round trip behind the streaming loads on every strip)
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t strip = wave; strip < nstrips; strip += nwaves) {
         const uint32_t u = find_unit(units, nunits, strip);
@@ -960,16 +1090,16 @@ __global__ void __launch_bounds__(256) unit_last_kernel(const UnitDesc *units, u
         uint32_t best = 0;
         for (int st = 0; st < U.nstrands; ++st)
             for (int k = 0; k < nnc; ++k) {
-                gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, nc[k]) + kPad + p0 - 1);
+                gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, nc[k]) + ((kPadPos + p0 - 1) >> 1));
 #pragma unroll 4
-                for (int bk = 0; bk < kBlocks; ++bk) {
+                for (int bk = 0; bk < kStripBytes / (kWave * 16); ++bk) {
                     const u32x4 v = __builtin_nontemporal_load(t + 64 * bk + lane);
-                    const int64_t q = p0 + kWave * kChunk * bk + kChunk * lane;
+                    const int64_t q = p0 + 2048 * bk + 32 * lane;  // position of the lane's first nibble
                     uint32_t hi = 0;
-                    if (v.x) hi = (uint32_t)q + top_byte(v.x);
-                    if (v.y) hi = (uint32_t)q + 4 + top_byte(v.y);
-                    if (v.z) hi = (uint32_t)q + 8 + top_byte(v.z);
-                    if (v.w) hi = (uint32_t)q + 12 + top_byte(v.w);
+                    if (v.x) hi = (uint32_t)q + top_nib(v.x);
+                    if (v.y) hi = (uint32_t)q + 8 + top_nib(v.y);
+                    if (v.z) hi = (uint32_t)q + 16 + top_nib(v.z);
+                    if (v.w) hi = (uint32_t)q + 24 + top_nib(v.w);
                     best = hi > best ? hi : best;
                 }
             }
@@ -1008,7 +1138,11 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
     const double *ktab = load_ktab(lds_, P.kern, bw);
     constexpr int NWT = 2 * NH + 1;
     const int lane = threadIdx.x & 63;
-    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // wave-uniform by construction; readfirstlane tells the compiler, so the
+    // strip / unit / work-list indices derived from it live in SGPRs and the
+    // unit table is read with scalar loads (vector loads of it cost a
+    // dependent round trip behind the streaming loads on every strip)
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
     const uint64_t nreg = *P.nreg < P.cap ? *P.nreg : P.cap;
     uint64_t wm[2 * NH + 1];
@@ -1035,9 +1169,11 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
         // the current one is scored (escapes resolved at use)
         uint32_t nf[NWT], nr[NONDIR ? NWT : 1];
         auto fetch_raw = [&](uint32_t (&dst)[NWT], int strand, int64_t x0) {
-            gu8 *t = track_u8(U, S, strand, P.nc[0]) + kPad + (x0 - 64 * NH) - 1 + lane;
+            const int64_t n0 = kPadPos + (x0 - 64 * NH) - 1 + lane;
+            gu8 *t = track_u8(U, S, strand, P.nc[0]) + (n0 >> 1);
+            const uint32_t sh = 4 * (uint32_t)(n0 & 1);
 #pragma unroll
-            for (int w = 0; w < NWT; ++w) dst[w] = t[64 * w];
+            for (int w = 0; w < NWT; ++w) dst[w] = ((uint32_t)t[32 * w] >> sh) & 15u;
         };
         // K1 saw the whole run: its peak is known and, unless the strand
         // correlation is wanted, no score is needed here -- only the counts
@@ -1080,14 +1216,21 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             if (known && S == 1 && nw <= kStatCache) {
                 best = kval;
                 best_x = kpos;
-                gu8 *t0 = track_u8(U, S, 0, P.nc[0]) + kPad + (int64_t)left - 1 + lane;
+                const int64_t n0 = kPadPos + (int64_t)left - 1 + lane;
+                const uint32_t sh = 4 * (uint32_t)(n0 & 1);
+                gu8 *t0 = track_u8(U, S, 0, P.nc[0]) + (n0 >> 1);
                 uint32_t r0[kStatCache], r1[NONDIR ? kStatCache : 1];
 #pragma unroll
-                for (int w = 0; w < kStatCache; ++w) r0[w] = w < nw ? t0[64 * w] : 0u;
+                for (int w = 0; w < kStatCache; ++w) r0[w] = w < nw ? t0[32 * w] : 0u;
                 if constexpr (NONDIR) {
-                    gu8 *t1 = track_u8(U, S, 1, P.nc[0]) + kPad + (int64_t)left - 1 + lane;
+                    gu8 *t1 = track_u8(U, S, 1, P.nc[0]) + (n0 >> 1);
 #pragma unroll
-                    for (int w = 0; w < kStatCache; ++w) r1[w] = w < nw ? t1[64 * w] : 0u;
+                    for (int w = 0; w < kStatCache; ++w) r1[w] = w < nw ? t1[32 * w] : 0u;
+                }
+#pragma unroll
+                for (int w = 0; w < kStatCache; ++w) {
+                    r0[w] = (r0[w] >> sh) & 15u;
+                    if constexpr (NONDIR) r1[w] = (r1[w] >> sh) & 15u;
                 }
 #pragma unroll
                 for (int w = 0; w < kStatCache; ++w) {
@@ -1450,38 +1593,43 @@ __global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t 
 // ------------------------------------------------------------------------
 // aux kernels
 // ------------------------------------------------------------------------
-// host pairs -> one uint8 track (counts >= 255 become the escape byte; the
-// host keeps their values in the unit's overflow table)
+// host pairs -> one 4-bit track (counts >= 15 become the escape nibble; the
+// host keeps their values in the unit's overflow table).  Two positions share
+// a byte, so each pair clears and sets its own nibble of the dword with
+// atomics on disjoint bits (positions within one call are unique).
 __global__ void scatter_kernel(uint8_t *track, const uint32_t *__restrict__ pos,
                                const uint32_t *__restrict__ cnt, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) track[kPad + pos[i] - 1] = (uint8_t)(cnt[i] >= kEsc ? kEsc : cnt[i]);
+    if (i >= n) return;
+    const uint64_t nb = kPadPos + (uint64_t)pos[i] - 1;        // nibble index
+    uint32_t *word = (uint32_t *)(track + ((nb >> 1) & ~3ull));  // its aligned dword
+    const uint32_t sh = 4 * (uint32_t)(nb & 7);
+    const uint32_t c = cnt[i] >= kEsc ? kEsc : cnt[i];
+    atomicAnd(word, ~(15u << sh));
+    if (c) atomicOr(word, c << sh);
 }
 
-// dense device uint32 counts (position p at src[p-1]) -> uint8 track;
-// counts >= 255 are appended to an overflow list (pos << 32 | count)
+// dense device uint32 counts (position p at src[p-1]) -> 4-bit track;
+// counts >= 15 are appended to an overflow list (pos << 32 | count)
 __global__ void pack_kernel(uint8_t *track, const uint32_t *__restrict__ src, uint64_t len,
                             unsigned long long *ovf, uint32_t *novf, uint32_t cap) {
-    const uint64_t i4 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    if (i4 >= len) return;
+    const uint64_t i8 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (i8 >= len) return;
     uint32_t out = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint64_t i = i4 + k;
+    for (int k = 0; k < 8; ++k) {
+        const uint64_t i = i8 + k;
         uint32_t c = i < len ? src[i] : 0u;
         if (c >= kEsc) {
             const uint32_t slot = atomicAdd(novf, 1u);
             if (slot < cap) ovf[slot] = ((unsigned long long)(i + 1) << 32) | c;
             c = kEsc;
         }
-        out |= c << (8 * k);
+        out |= c << (4 * k);
     }
-    // kPad and p-1 = i4 are multiples of 4: one aligned dword store
-    if (i4 + 4 <= len) {
-        *(uint32_t *)(track + kPad + i4) = out;
-    } else {
-        for (int k = 0; i4 + k < len; ++k) track[kPad + i4 + k] = (uint8_t)(out >> (8 * k));
-    }
+    // kPadPos and p-1 = i8 are multiples of 8: one aligned dword store (the
+    // nibbles past len are zero, and the track extends past len + kMaxBw)
+    *(uint32_t *)(track + ((kPadPos + i8) >> 1)) = out;
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -1508,7 +1656,7 @@ __global__ void synth_bg_kernel(uint32_t *stage, uint64_t tkey, int64_t lo, int6
     stage[x - 1] = c;
 }
 
-// sum of a uint8 track's bytes, escapes excluded (their counts are added on
+// sum of a 4-bit track's counts, escapes excluded (their counts are added on
 // the host from the overflow table)
 __global__ void track_sum_kernel(const uint8_t *__restrict__ t, uint64_t n, unsigned long long *out) {
     uint64_t acc = 0;
@@ -1519,12 +1667,9 @@ __global__ void track_sum_kernel(const uint8_t *__restrict__ t, uint64_t n, unsi
         const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            uint32_t y = w[k];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const uint32_t c = (y >> (8 * b)) & 0xFFu;
-                acc += c == kEsc ? 0u : c;
-            }
+            const uint32_t y = w[k];
+            const uint32_t esc = y & (y >> 1) & (y >> 2) & (y >> 3) & 0x11111111u;  // nibbles == 15
+            acc += nsum8(y, 0u) - kEsc * (uint32_t)__builtin_popcount(esc);
         }
     }
     __shared__ unsigned long long red[256];
