@@ -194,12 +194,15 @@ def main():
     n0 = g.run()
     cap = int((comm.max_over_ranks(n0) if comm else n0) * 1.25) + 64
     # shm delivery: passes are pipelined -- step i launches pass i and then
-    # completes pass i-1 (up_run_async / up_run_wait), so the GPU never waits
-    # for the host between passes; four rotating record slots per rank
+    # completes pass i-DEPTH+1 (up_run_async / up_run_wait), so the GPU never
+    # waits for the host between passes and consecutive passes overlap on the
+    # device (a pass's streaming K1a beside the previous passes' exact and
+    # statistics kernels); NSLOT rotating record slots per rank
+    DEPTH, NSLOT = 3, 6
     pipelined = comm is None or gather_mode == "shm"
     if pipelined:
         tag = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}_{os.environ.get('MASTER_PORT', '0')}"
-        nr = shard.NodeRecords(comm, cap, S, capi.REGION_DTYPE.itemsize, tag, nslots=4)
+        nr = shard.NodeRecords(comm, cap, S, capi.REGION_DTYPE.itemsize, tag, nslots=NSLOT)
         g.host_register(*nr.my_range())
         if rank == 0:
             from concurrent.futures import ThreadPoolExecutor
@@ -254,9 +257,9 @@ def main():
             phase["launch"] += t2 - t1
             phase["gather_merge"] += t3 - t2
             return
-        # slot i % 4 held step i-4: its read must be over before any rank
-        # passes this step's collective and launches into it
-        while reads and reads[0][0] <= i - 4:
+        # slot i % NSLOT held step i-NSLOT: its read must be over before any
+        # rank passes this step's collective and launches into it
+        while reads and reads[0][0] <= i - NSLOT:
             reads.pop(0)[1].result()
         if comm is not None:
             # this step's all-reduce was started one step ahead (RCCL gets the
@@ -267,17 +270,17 @@ def main():
             tags = local_tags
         set_background(tags)
         t1 = time.perf_counter()
-        # every rank has completed pass i-2 (it waited for it before entering
-        # this collective): rank 0 reads it while passes i-1 and i run
-        if rank == 0 and i >= 2:
-            reads.append((i - 2, read_step(i - 2)))
+        # every rank has completed pass i-DEPTH (it waited for it before
+        # entering this collective): rank 0 reads it while later passes run
+        if rank == 0 and i >= DEPTH:
+            reads.append((i - DEPTH, read_step(i - DEPTH)))
         g.set_record_target(nr.my_slot_address(i), cap)
         if timed[0]:  # K1a events on every K1A_EVERY-th timed pass only (an event pair idles the GPU)
             g.set_timing(1 if i % K1A_EVERY == 0 else 0)
         g.run_async()
         it[0] += 1
         t2 = time.perf_counter()
-        if i >= 1:
+        if i >= DEPTH - 1:
             g.run_wait()
             done_times.append(g.timings())
         t3 = time.perf_counter()
@@ -305,9 +308,7 @@ def main():
             reads.clear()
             for f in pend:
                 res = f.result()
-            for j in range(max(0, last - 1), last + 1):
-                if j <= last - 2:
-                    continue
+            for j in range(max(0, last - DEPTH + 1), last + 1):  # steps not read during the loop
                 res = consume(nr.read(capi.REGION_DTYPE, j))
         return res
 

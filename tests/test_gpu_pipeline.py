@@ -1,6 +1,8 @@
 """Pipelined passes (up_run_async / up_run_wait, include/unipeak_hip.h):
-two passes in flight, each delivering into the record target that was set
-when it was launched, give exactly the records of the blocking up_run; state
+two or three passes in flight (each on its own stream and buffers, a pass's
+K1a overlapping the previous passes' K1b/K2/K3), each delivering into the
+record target that was set when it was launched, give exactly the records of
+the blocking up_run; a fourth launch is refused; state
 cannot change under a pass in flight; the K2 segmentation (two launches,
 re-armed counters) stays exact across many passes and across units whose
 strip counts span several K2 blocks."""
@@ -39,8 +41,8 @@ def _parse(buf, off, cap, S, dtype):
     return recs, cnt
 
 
-@pytest.mark.parametrize("seed", [0, 1])
-def test_async_matches_blocking(gpu_lib, seed):
+@pytest.mark.parametrize("seed,depth", [(0, 2), (1, 2), (2, 3), (3, 3)])
+def test_async_matches_blocking(gpu_lib, seed, depth):
     capi = gpu_lib
     rng = np.random.default_rng(seed)
     bw = 50
@@ -52,28 +54,29 @@ def test_async_matches_blocking(gpu_lib, seed):
         ref, rcnt = g.regions(n)
         assert n > 0
         cap = n + 16
-        bufs = [_target(cap, 1, capi.REGION_DTYPE.itemsize) for _ in range(2)]
+        bufs = [_target(cap, 1, capi.REGION_DTYPE.itemsize) for _ in range(depth)]
         for b, off in bufs:
             g.host_register(b[off:].ctypes.data, len(b) - off)
         for timing in (0, 1, 2):
             g.set_timing(timing)
             got = []
-            npass = 6
+            npass = 7
             for i in range(npass):
-                b, off = bufs[i & 1]
+                b, off = bufs[i % depth]
                 g.set_record_target(b[off:].ctypes.data, cap)
                 g.run_async()
-                if i >= 1:
+                if i >= depth - 1:
                     m = g.run_wait()
-                    pb, poff = bufs[(i - 1) & 1]
+                    pb, poff = bufs[(i - depth + 1) % depth]
                     got.append((m,) + _parse(pb, poff, cap, 1, capi.REGION_DTYPE))
                 # state is frozen while passes are in flight
                 with pytest.raises(capi.UpError) as e:
                     g.set_params(bw, 1, 0.003)
                 assert e.value.code == UP_E_STATE
-            m = g.run_wait()
-            b, off = bufs[(npass - 1) & 1]
-            got.append((m,) + _parse(b, off, cap, 1, capi.REGION_DTYPE))
+            for j in range(npass - depth + 1, npass):
+                m = g.run_wait()
+                b, off = bufs[j % depth]
+                got.append((m,) + _parse(b, off, cap, 1, capi.REGION_DTYPE))
             with pytest.raises(capi.UpError):
                 g.run_wait()  # nothing in flight
             assert len(got) == npass
@@ -87,8 +90,8 @@ def test_async_matches_blocking(gpu_lib, seed):
 
 
 def test_async_host_delivery_and_growth(gpu_lib):
-    """host delivery (no target), first pass grows the record areas while a
-    second pass is in flight"""
+    """host delivery (no target), first pass grows the record areas while
+    later passes are in flight; a fourth pass in flight is refused"""
     capi = gpu_lib
     rng = np.random.default_rng(5)
     bw = 5  # narrow windows: most tags are regions of their own
@@ -100,15 +103,21 @@ def test_async_host_delivery_and_growth(gpu_lib):
             g.scatter(u, 0, 0, pos, cnt[:, 0])
         g.run_async()
         g.run_async()
+        g.run_async()
+        with pytest.raises(capi.UpError) as e:
+            g.run_async()
+        assert e.value.code == UP_E_STATE
         n1 = g.run_wait()
         r1, c1 = g.regions(n1)
         n2 = g.run_wait()
         r2, c2 = g.regions(n2)
+        n4 = g.run_wait()
+        r4, c4 = g.regions(n4)
         n3 = g.run()
         r3, c3 = g.regions(n3)
-    assert n1 == n2 == n3 and n1 > (1 << 16)  # beyond the initial record capacity
-    assert r1.tobytes() == r2.tobytes() == r3.tobytes()
-    assert np.array_equal(c1, c3) and np.array_equal(c2, c3)
+    assert n1 == n2 == n3 == n4 and n1 > (1 << 16)  # beyond the initial record capacity
+    assert r1.tobytes() == r2.tobytes() == r3.tobytes() == r4.tobytes()
+    assert np.array_equal(c1, c3) and np.array_equal(c2, c3) and np.array_equal(c4, c3)
 
 
 def test_many_units_many_blocks(gpu_lib, oracle):

@@ -89,11 +89,14 @@ struct HostBuf {
     }
 };
 
+constexpr int kSlots = 3;  // passes in flight at most (up_run_async)
+
 }  // namespace
 
 struct up_ctx {
     int dev = 0;
     int ncu = 0;                     // compute units of the device
+    int k1a_per_cu = 2;              // K1a workgroups per CU (UNIPEAK_K1A_PER_CU; 0 = resident max)
     hipStream_t stream = nullptr;
     bool have_params = false;
     up_params p{};
@@ -105,6 +108,8 @@ struct up_ctx {
     DevBuf<uint8_t> d_ctl;
     DevBuf<uint32_t> d_wscreen;
     uint32_t wskip = 0;
+    float fw[9] = {};                // fine screen weights per chunk distance
+    float fthr = 0.f;
     DevBuf<uint32_t> d_stage;          // dense uint32 staging for synth / pack
     DevBuf<unsigned long long> d_pack_ovf;
     DevBuf<uint32_t> d_pack_n;
@@ -114,13 +119,8 @@ struct up_ctx {
     DevBuf<UnitDesc> d_units;
     uint32_t nstrips = 0;
     int bw_layout = -1;  // bw the strip layout was computed for
-    DevBuf<uint64_t> d_info;
-    DevBuf<uint32_t> d_rec, d_lastnz, d_ovf_count, d_ovf_rec, d_unit_last;
-    DevBuf<uint64_t> d_cnt, d_nreg;
-    DevBuf<uint32_t> d_starts, d_ends, d_runit, d_peak_pos, d_xlist, d_xcount, d_xwcount, d_xref;
+    DevBuf<uint32_t> d_unit_last;
     uint32_t k1a_waves = 0, k1a_xcap = 0;  // grid and per-wave stash size of the last K1a launch
-    DevBuf<double> d_peak_val;
-    DevBuf<uint64_t> d_spk;          // K1 per-strip partial peaks (ScanParams::spk)
     uint32_t ovf_cap = 256;
     uint64_t nreg = 0;
     bool ran = false;
@@ -128,9 +128,27 @@ struct up_ctx {
     hipEvent_t ev[8] = {};
     double times[5] = {0, 0, 0, 0, 0};
     int timing = 2;                  // up_set_timing: 0 wall only, 1 + K1a, 2 every phase
-    bool counters_armed = false;     // xcount / ovf_count are zero (re-armed by K2b)
-    // passes in flight (up_run_async); slot = sequence & 1
+    // passes in flight (up_run_async); slot = sequence % kSlots.  Each slot
+    // owns its device buffers and its stream, so a pass's streaming K1a can
+    // run while earlier passes' latency-bound K1b/K2/K3 finish (a pass's K1a
+    // starts once the previous pass's K1a has ended, k1a_end); three slots let
+    // the host enqueue a pass before the one two back has completed
     struct Pass {
+        hipStream_t stream = nullptr;
+        hipEvent_t k1a_end = nullptr;   // this pass's K1a finished
+        bool counters_armed = false;    // xcount / ovf_count are zero (re-armed by K2b)
+        DevBuf<uint64_t> d_info;
+        DevBuf<uint32_t> d_rec, d_ovf_count, d_ovf_rec, d_head;
+        DevBuf<uint64_t> d_cnt, d_nreg, d_bsum;
+        DevBuf<uint32_t> d_starts, d_ends, d_runit, d_peak_pos, d_xlist, d_xcount, d_xwcount, d_xref;
+        DevBuf<double> d_peak_val;
+        DevBuf<uint64_t> d_spk;          // K1 per-strip partial peaks (ScanParams::spk)
+        void release() {
+            d_info.release(); d_rec.release(); d_ovf_count.release(); d_ovf_rec.release(); d_head.release();
+            d_cnt.release(); d_nreg.release(); d_bsum.release(); d_starts.release(); d_ends.release();
+            d_runit.release(); d_peak_pos.release(); d_xlist.release(); d_xcount.release();
+            d_xwcount.release(); d_xref.release(); d_peak_val.release(); d_spk.release();
+        }
         uint8_t *target = nullptr;   // record target of this pass (device address) or null
         void *target_hostp = nullptr;// host address of a host target
         uint64_t target_cap = 0;
@@ -140,11 +158,12 @@ struct up_ctx {
         std::chrono::steady_clock::time_point t0;
         hipEvent_t ev[5] = {};       // K1a begin, K1a end, K1b end, K2 end, K3 end
         hipEvent_t done = nullptr;
-    } pass[2];
+    } pass[kSlots];
     uint64_t seq_launched = 0, seq_done = 0;
     int cur_slot = 0;                // slot of the last completed pass (host records)
     // head-hit (quirk Q1) replay
-    DevBuf<uint32_t> d_head, d_resync, d_emu_n, d_emu_err, d_emu_counts, d_ring_hits, d_reg_hit, d_reg_hits;
+    hipEvent_t host_work = nullptr;  // marks work on `stream` that a pass must follow
+    DevBuf<uint32_t> d_resync, d_emu_n, d_emu_err, d_emu_counts, d_ring_hits, d_reg_hit, d_reg_hits;
     DevBuf<int32_t> d_unit_buffer;
     DevBuf<double> d_reg_f, d_reg_r;
     DevBuf<up_region> d_emu_out;
@@ -162,11 +181,10 @@ struct up_ctx {
     std::vector<uint32_t> h_counts;
     std::vector<uint8_t> h_emulated;
     // per pass slot: head-hit flags (seg_count_head_kernel), host records, status
-    HostBuf<uint32_t> hp_head[2];
-    HostBuf<up_region> hp_regions[2];
-    HostBuf<uint32_t> hp_counts[2];
-    HostBuf<unsigned long long> hp_status[2];
-    DevBuf<uint64_t> d_bsum;
+    HostBuf<uint32_t> hp_head[kSlots];
+    HostBuf<up_region> hp_regions[kSlots];
+    HostBuf<uint32_t> hp_counts[kSlots];
+    HostBuf<unsigned long long> hp_status[kSlots];
     void *target_hostp = nullptr;    // host address of the current host target
     // up_unit_scatter staging: two mapped host buffers the scatter kernel
     // reads directly, reused once the event of their previous use fired
@@ -182,6 +200,12 @@ struct up_ctx {
 };
 
 static bool busy(const up_ctx *c) { return c && c->seq_launched != c->seq_done; }
+
+// the context stream and both pass streams idle
+static void sync_all(up_ctx *c) {
+    (void)hipStreamSynchronize(c->stream);
+    for (auto &ps : c->pass) (void)hipStreamSynchronize(ps.stream);
+}
 
 #define HIPCHK(x)                                                                   \
     do {                                                                            \
@@ -245,12 +269,16 @@ int up_open(int hip_device, up_ctx **out) {
     c->dev = hip_device;
     HIPCHK(hipSetDevice(hip_device));
     HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
+    if (const char *e = getenv("UNIPEAK_K1A_PER_CU")) c->k1a_per_cu = atoi(e);
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     for (auto &ps : c->pass) {
         for (auto &e : ps.ev) HIPCHK(hipEventCreate(&e));
         HIPCHK(hipEventCreateWithFlags(&ps.done, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ps.k1a_end, hipEventDisableTiming));
+        HIPCHK(hipStreamCreateWithFlags(&ps.stream, hipStreamNonBlocking));
     }
+    HIPCHK(hipEventCreateWithFlags(&c->host_work, hipEventDisableTiming));
     for (auto &e : c->scat_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     *out = c;
     return UP_OK;
@@ -273,28 +301,26 @@ void up_close(up_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->stream);
+    for (auto &ps : c->pass) (void)hipStreamSynchronize(ps.stream);
     free_units(c);
     drop_target(c);
     for (void *h : c->host_regs) (void)hipHostUnregister(h);
     c->d_kern.release(); c->d_coef.release(); c->d_nc.release(); c->d_ctl.release();
-    c->d_units.release(); c->d_info.release(); c->d_rec.release(); c->d_lastnz.release();
-    c->d_ovf_count.release(); c->d_ovf_rec.release(); c->d_unit_last.release();
-    c->d_cnt.release(); c->d_nreg.release();
-    c->d_starts.release(); c->d_ends.release(); c->d_runit.release();
-    c->d_peak_pos.release(); c->d_peak_val.release(); c->d_xlist.release(); c->d_xcount.release();
-    c->d_xwcount.release(); c->d_xref.release();
-    c->d_spk.release();
-    c->d_head.release(); c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
+    c->d_units.release(); c->d_unit_last.release();
+    c->d_resync.release(); c->d_emu_n.release(); c->d_emu_err.release();
     c->d_emu_counts.release(); c->d_ring_hits.release(); c->d_reg_hit.release(); c->d_reg_hits.release();
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
     c->d_ring_f.release(); c->d_ring_r.release(); c->d_ring_has.release();
     c->d_emu_scores.release(); c->d_emu_score_off.release(); c->d_emu_nscores.release();
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kSlots; ++k) {
         c->hp_regions[k].release(); c->hp_counts[k].release(); c->hp_status[k].release(); c->hp_head[k].release();
         for (auto &e : c->pass[k].ev) (void)hipEventDestroy(e);
         (void)hipEventDestroy(c->pass[k].done);
+        (void)hipEventDestroy(c->pass[k].k1a_end);
+        c->pass[k].release();
+        (void)hipStreamDestroy(c->pass[k].stream);
     }
-    c->d_bsum.release();
+    (void)hipEventDestroy(c->host_work);
     for (auto &e : c->scat_ev) (void)hipEventSynchronize(e);
     c->hp_scat[0].release(); c->hp_scat[1].release();
     for (auto &e : c->scat_ev) (void)hipEventDestroy(e);
@@ -368,6 +394,20 @@ int up_set_params(up_ctx *c, const up_params *p) {
         else if (wf >= (double)(kBig - 1)) ws = kBig - 1;
         else ws = (uint32_t)std::ceil(wf) - 1u;
         c->wskip = ws;
+        // fine screen: fw[d] bounds the kernel weight between any two
+        // positions of chunks d apart (smallest distance 0, 1, 17, 33, ...),
+        // inflated by 1e-4; a chunk can hold a flag only if its bound > fthr
+        const int bwi = p->bw;
+        for (int d = 0; d < 9; ++d) {
+            const int u0 = d == 0 ? 0 : 16 * (d - 1) + 1;
+            double kd = 0.0;
+            for (int u = u0; u <= bwi; ++u) kd = std::max(kd, std::fabs(c->kern[bwi + u]));
+            float f = (float)(kd * (1.0 + 1e-4));
+            if ((double)f < kd * (1.0 + 1e-4)) f = std::nextafter(f, HUGE_VALF);
+            c->fw[d] = f;
+        }
+        // screen off (huge coefficients): every tag within reach goes exact
+        c->fthr = (huge || !(wf > 0.0)) ? 0.f : (float)(p->region_thr * (1.0 - 1e-6));
     }
     c->have_params = true;
     if (old_bw != p->bw) c->units_dirty = true;
@@ -693,7 +733,7 @@ static int pool_mode(const up_ctx *c) {
     return c->nc.size() == 1 ? 0 : 1;
 }
 
-static ScanParams scan_params(up_ctx *c) {
+static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps) {
     ScanParams P{};
     P.units = c->d_units.p;
     P.nunits = (uint32_t)c->units.size();
@@ -705,18 +745,20 @@ static ScanParams scan_params(up_ctx *c) {
     P.kern = c->d_kern.p;
     P.wscreen = c->d_wscreen.p;
     P.wskip = c->wskip;
+    for (int d = 0; d < 9; ++d) P.fw[d] = c->fw[d];
+    P.fthr = c->fthr;
     P.bw = c->p.bw;
     P.thr = c->p.region_thr;
-    P.strip_info = c->d_info.p;
-    P.rec = c->d_rec.p;
-    P.ovf_count = c->d_ovf_count.p;
-    P.ovf_rec = c->d_ovf_rec.p;
+    P.strip_info = ps.d_info.p;
+    P.rec = ps.d_rec.p;
+    P.ovf_count = ps.d_ovf_count.p;
+    P.ovf_rec = ps.d_ovf_rec.p;
     P.ovf_cap = c->ovf_cap;
-    P.xlist = c->d_xlist.p;
-    P.xwcount = c->d_xwcount.p;
-    P.xref = c->d_xref.p;
-    P.xcount = c->d_xcount.p;
-    P.spk = c->d_spk.p;
+    P.xlist = ps.d_xlist.p;
+    P.xwcount = ps.d_xwcount.p;
+    P.xref = ps.d_xref.p;
+    P.xcount = ps.d_xcount.p;
+    P.spk = ps.d_spk.p;
     return P;
 }
 
@@ -743,7 +785,7 @@ static uint32_t resident_blocks(const up_ctx *c, const void *kernel, size_t lds)
 }
 
 template <int NH, int POOL, bool ND, bool PROF, int MODE>
-static void launch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e) {
+static void launch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32_t b, uint32_t e) {
     const size_t lds = MODE == kModeScreen ? kScreenLds : MODE == kModeExact ? kExactLds : kScanLds;
     const void *k = (const void *)scan_kernel<NH, POOL, ND, PROF, MODE>;
     uint32_t blocks = resident_blocks(c, k, lds);
@@ -754,6 +796,12 @@ static void launch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e) 
         // start at later (cheaper, single-block) items
         blocks *= 2;
     } else {
+        if (MODE == kModeScreen) {
+            // K1a leaves room on every CU for the previous pass's K1b/K3
+            // (they overlap it, launch_pass): k1a_per_cu workgroups per CU
+            const uint32_t cap = (uint32_t)c->k1a_per_cu * (uint32_t)(c->ncu > 0 ? c->ncu : 256);
+            if (c->k1a_per_cu > 0 && cap < blocks) blocks = cap;
+        }
         const uint32_t need = (e - b + 3) / 4;  // one wave per strip at most
         if (need < blocks) blocks = need;
         if (blocks > kMaxK1aWaves / 4) blocks = kMaxK1aWaves / 4;
@@ -763,19 +811,19 @@ static void launch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e) 
         ScanParams Q = P;
         c->k1a_waves = 4 * blocks;
         c->k1a_xcap = Q.xcap = (e - b + c->k1a_waves - 1) / c->k1a_waves;
-        hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF, MODE>), dim3(blocks), dim3(256), lds, c->stream, Q, b, e);
+        hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF, MODE>), dim3(blocks), dim3(256), lds, st, Q, b, e);
         return;
     }
-    hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF, MODE>), dim3(blocks), dim3(256), lds, c->stream, P, b, e);
+    hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF, MODE>), dim3(blocks), dim3(256), lds, st, P, b, e);
 }
 
 template <bool PROF, int MODE>
-static void dispatch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e) {
+static void dispatch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32_t b, uint32_t e) {
     const int nh = P.bw <= 63 ? 1 : 2;
     const int pool = pool_mode(c);
     const bool nd = c->p.nondir != 0;
 #define UPK_SCAN(NH, PL, ND) \
-    if (nh == NH && pool == PL && nd == ND) return launch_scan<NH, PL, ND, PROF, MODE>(c, P, b, e);
+    if (nh == NH && pool == PL && nd == ND) return launch_scan<NH, PL, ND, PROF, MODE>(c, st, P, b, e);
     UPK_SCAN(1, 0, false) UPK_SCAN(1, 1, false) UPK_SCAN(1, 2, false)
     UPK_SCAN(1, 0, true) UPK_SCAN(1, 1, true) UPK_SCAN(1, 2, true)
     UPK_SCAN(2, 0, false) UPK_SCAN(2, 1, false) UPK_SCAN(2, 2, false)
@@ -783,7 +831,7 @@ static void dispatch_scan(up_ctx *c, const ScanParams &P, uint32_t b, uint32_t e
 #undef UPK_SCAN
 }
 
-static StatParams stat_params(up_ctx *c) {
+static StatParams stat_params(up_ctx *c, up_ctx::Pass &ps) {
     StatParams P{};
     P.units = c->d_units.p;
     P.S = c->p.n_samples;
@@ -799,19 +847,19 @@ static StatParams stat_params(up_ctx *c) {
     P.kurt_thr = c->p.kurt_thr;
     P.corr_thr = c->p.corr_thr;
     P.hit_thr = c->p.hit_thr;
-    P.starts = c->d_starts.p;
-    P.ends = c->d_ends.p;
-    P.reg_unit = c->d_runit.p;
+    P.starts = ps.d_starts.p;
+    P.ends = ps.d_ends.p;
+    P.reg_unit = ps.d_runit.p;
     P.peak_pos = nullptr;  // set by up_run (known peaks from K1)
     P.peak_val = nullptr;
-    P.nreg = c->d_nreg.p;
+    P.nreg = ps.d_nreg.p;
     P.out = nullptr;  // set by up_run (mapped host records)
     P.out_counts = nullptr;
     P.cap = 0;
     return P;
 }
 
-static void dispatch_stats(up_ctx *c, const StatParams &P, uint64_t nreg) {
+static void dispatch_stats(up_ctx *c, hipStream_t st, const StatParams &P, uint64_t nreg) {
     const int nh = P.bw <= 63 ? 1 : 2;
     const int pool = pool_mode(c);
     const bool nd = c->p.nondir != 0;
@@ -822,7 +870,7 @@ static void dispatch_stats(up_ctx *c, const StatParams &P, uint64_t nreg) {
                                              resident_blocks(c, (const void *)stats_kernel<NH, PL, ND>, lds)); \
         if (blocks == 0) return;                                                                 \
         hipLaunchKernelGGL((stats_kernel<NH, PL, ND>), dim3((unsigned)blocks), dim3(256), lds,     \
-                           c->stream, P);                                                         \
+                           st, P);                                                                \
         return;                                                                                  \
     }
     UPK_ST(1, 0, false) UPK_ST(1, 1, false) UPK_ST(1, 2, false)
@@ -858,21 +906,22 @@ static int check_runnable(up_ctx *c) {  // the parallel scan
 // K2a (segment counts of every strip) + quirk-Q1 head detection (units with
 // pooled tags at positions <= bw, misc/peakcall.cpp:177-183) in one launch
 static int launch_seg_count_head(up_ctx *c, int slot) {
+    up_ctx::Pass &ps = c->pass[slot];
     const uint32_t nu = (uint32_t)c->units.size();
     const uint32_t ns = c->nstrips;
     const uint32_t nsb = (ns + kSegBlock - 1) / kSegBlock;
-    HIPCHK(c->d_head.ensure(nu));
+    HIPCHK(ps.d_head.ensure(nu));
     HIPCHK(c->hp_head[slot].ensure(nu));
     if (c->p.bw > kSegBlock) return UP_E_INTERNAL;  // one thread per head position
     if (pool_mode(c) == 2)
-        hipLaunchKernelGGL(seg_count_head_kernel<2>, dim3(nsb + nu), dim3(kSegBlock), 0, c->stream, c->d_info.p,
-                           c->d_cnt.p, c->d_bsum.p, ns, nsb, c->d_units.p, (int)c->p.n_samples,
-                           (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw, c->d_head.p,
+        hipLaunchKernelGGL(seg_count_head_kernel<2>, dim3(nsb + nu), dim3(kSegBlock), 0, ps.stream, ps.d_info.p,
+                           ps.d_cnt.p, ps.d_bsum.p, ns, nsb, c->d_units.p, (int)c->p.n_samples,
+                           (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw, ps.d_head.p,
                            c->hp_head[slot].dev);
     else
-        hipLaunchKernelGGL(seg_count_head_kernel<1>, dim3(nsb + nu), dim3(kSegBlock), 0, c->stream, c->d_info.p,
-                           c->d_cnt.p, c->d_bsum.p, ns, nsb, c->d_units.p, (int)c->p.n_samples,
-                           (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw, c->d_head.p,
+        hipLaunchKernelGGL(seg_count_head_kernel<1>, dim3(nsb + nu), dim3(kSegBlock), 0, ps.stream, ps.d_info.p,
+                           ps.d_cnt.p, ps.d_bsum.p, ns, nsb, c->d_units.p, (int)c->p.n_samples,
+                           (int)c->nc.size(), c->d_nc.p, c->d_coef.p, (int)c->p.bw, ps.d_head.p,
                            c->hp_head[slot].dev);
     HIPCHK(hipGetLastError());
     return UP_OK;
@@ -882,7 +931,8 @@ static int launch_seg_count_head(up_ctx *c, int slot) {
 // d_head (replay_all: over every unit, never resynced) -> its regions, their
 // exptSums and the per-unit resync positions.  Capacity of the region
 // record area and of one open region grow until the replay fits.
-static int emulate_units(up_ctx *c, bool replay_all, std::vector<up_region> &emu, std::vector<uint32_t> &ecnt,
+static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std::vector<up_region> &emu,
+                         std::vector<uint32_t> &ecnt,
                          std::vector<uint32_t> &resync, std::vector<uint64_t> &soff) {
     const uint32_t nu = (uint32_t)c->units.size();
     const int S = c->p.n_samples;
@@ -928,7 +978,7 @@ static int emulate_units(up_ctx *c, bool replay_all, std::vector<up_region> &emu
         E.units = c->d_units.p;
         E.nunits = nu;
         E.unit_buffer = c->d_unit_buffer.p;
-        E.unit_head = c->d_head.p;
+        E.unit_head = d_head;
         E.S = S;
         E.nnc = (int32_t)c->nc.size();
         E.nc = c->d_nc.p;
@@ -1042,7 +1092,7 @@ static int replay_head_hits(up_ctx *c, int slot) {
     std::vector<up_region> emu;
     std::vector<uint32_t> ecnt, resync;
     std::vector<uint64_t> soff;
-    int rc = emulate_units(c, false, emu, ecnt, resync, soff);
+    int rc = emulate_units(c, c->pass[slot].d_head.p, false, emu, ecnt, resync, soff);
     if (rc) return rc;
     const uint32_t nemu = (uint32_t)emu.size();
     // the parallel path's records of this pass, wherever K3 wrote them
@@ -1111,26 +1161,26 @@ static int launch_pass(up_ctx *c, int slot) {
     const int S = c->p.n_samples;
     up_ctx::Pass &ps = c->pass[slot];
     const uint32_t nsb = (ns + kSegBlock - 1) / kSegBlock;
-    HIPCHK(c->d_info.ensure(ns));
-    HIPCHK(c->d_rec.ensure((size_t)ns * kRecStride));
-    HIPCHK(c->d_xlist.ensure(((size_t)ns + kMaxK1aWaves) * kXEntry));  // K1a stash regions
-    HIPCHK(c->d_xwcount.ensure(2 * kMaxK1aWaves));
-    HIPCHK(c->d_xref.ensure(ns));
-    HIPCHK(c->d_spk.ensure((size_t)ns * 4));
-    HIPCHK(c->d_cnt.ensure(ns));
-    HIPCHK(c->d_bsum.ensure(nsb));
-    HIPCHK(c->d_nreg.ensure(1));
+    HIPCHK(ps.d_info.ensure(ns));
+    HIPCHK(ps.d_rec.ensure((size_t)ns * kRecStride));
+    HIPCHK(ps.d_xlist.ensure(((size_t)ns + kMaxK1aWaves) * kXEntry));  // K1a stash regions
+    HIPCHK(ps.d_xwcount.ensure(2 * kMaxK1aWaves));
+    HIPCHK(ps.d_xref.ensure(ns));
+    HIPCHK(ps.d_spk.ensure((size_t)ns * 4));
+    HIPCHK(ps.d_cnt.ensure(ns));
+    HIPCHK(ps.d_bsum.ensure(nsb));
+    HIPCHK(ps.d_nreg.ensure(1));
     HIPCHK(c->hp_status[slot].ensure(4));
-    if (!c->d_xcount.p || !c->d_ovf_count.p) c->counters_armed = false;
-    HIPCHK(c->d_xcount.ensure(2));  // front / back ends of the work list
-    HIPCHK(c->d_ovf_count.ensure(1));
+    if (!ps.d_xcount.p || !ps.d_ovf_count.p) ps.counters_armed = false;
+    HIPCHK(ps.d_xcount.ensure(2));  // front / back ends of the work list
+    HIPCHK(ps.d_ovf_count.ensure(1));
     const uint64_t cap = c->reg_cap;
-    HIPCHK(c->d_ovf_rec.ensure((size_t)c->ovf_cap * kOvfStride));
-    HIPCHK(c->d_peak_pos.ensure(cap + 1));
-    HIPCHK(c->d_peak_val.ensure(cap + 1));
-    HIPCHK(c->d_starts.ensure(cap + 1));
-    HIPCHK(c->d_ends.ensure(cap + 1));
-    HIPCHK(c->d_runit.ensure(cap + 1));
+    HIPCHK(ps.d_ovf_rec.ensure((size_t)c->ovf_cap * kOvfStride));
+    HIPCHK(ps.d_peak_pos.ensure(cap + 1));
+    HIPCHK(ps.d_peak_val.ensure(cap + 1));
+    HIPCHK(ps.d_starts.ensure(cap + 1));
+    HIPCHK(ps.d_ends.ensure(cap + 1));
+    HIPCHK(ps.d_runit.ensure(cap + 1));
     if (!c->target) {
         HIPCHK(c->hp_regions[slot].ensure(cap + 1));
         HIPCHK(c->hp_counts[slot].ensure((cap + 1) * S));
@@ -1140,53 +1190,61 @@ static int launch_pass(up_ctx *c, int slot) {
     ps.target_cap = c->target_cap;
     ps.cap = cap;
     ps.ovf_cap = c->ovf_cap;
-    if (!c->counters_armed) {  // K2b re-arms them at the end of every pass
-        HIPCHK(hipMemsetAsync(c->d_ovf_count.p, 0, sizeof(uint32_t), c->stream));
-        HIPCHK(hipMemsetAsync(c->d_xcount.p, 0, 2 * sizeof(uint32_t), c->stream));
+    if (!ps.counters_armed) {  // K2b re-arms them at the end of every pass
+        HIPCHK(hipMemsetAsync(ps.d_ovf_count.p, 0, sizeof(uint32_t), ps.stream));
+        HIPCHK(hipMemsetAsync(ps.d_xcount.p, 0, 2 * sizeof(uint32_t), ps.stream));
     }
-    c->counters_armed = false;  // until K2b is enqueued
-    ScanParams SP = scan_params(c);
+    ps.counters_armed = false;  // until K2b is enqueued
+    ScanParams SP = scan_params(c, ps);
 #ifdef UPK_DEBUG_COUNTS
     static const bool dbg = getenv("UNIPEAK_DEBUG_COUNTS") != nullptr;
     if (dbg) {
         HIPCHK(c->d_dbg.ensure(8));
-        HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 8 * sizeof(unsigned long long), c->stream));
+        HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 8 * sizeof(unsigned long long), ps.stream));
         SP.dbg = c->d_dbg.p;
     }
 #endif
     const int tl = c->timing;
     ps.tl = tl;
-    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[0], c->stream));
+    // the pass follows everything enqueued on the context stream (track
+    // writes), and its K1a follows the K1a of the pass in flight in the other
+    // slot: one streaming K1a at a time, the other pass's K1b/K2/K3 beside it
+    HIPCHK(hipEventRecord(c->host_work, c->stream));
+    HIPCHK(hipStreamWaitEvent(ps.stream, c->host_work, 0));
+    if (c->seq_launched > c->seq_done)  // the previous pass is in flight
+        HIPCHK(hipStreamWaitEvent(ps.stream, c->pass[(slot + kSlots - 1) % kSlots].k1a_end, 0));
+    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[0], ps.stream));
     c->k1a_waves = 0;
-    dispatch_scan<false, kModeScreen>(c, SP, 0, ns);   // K1a: stream + screen
+    dispatch_scan<false, kModeScreen>(c, ps.stream, SP, 0, ns);   // K1a: stream + screen
     HIPCHK(hipGetLastError());
-    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[1], c->stream));
+    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[1], ps.stream));
+    HIPCHK(hipEventRecord(ps.k1a_end, ps.stream));
     if (c->k1a_waves) {  // K1x: list the stashed work-list entries for K1b
-        hipLaunchKernelGGL(xref_kernel, dim3(1), dim3(1024), 0, c->stream, c->d_xwcount.p, c->k1a_waves,
-                           c->k1a_xcap, c->d_xref.p, c->d_xcount.p);
+        hipLaunchKernelGGL(xref_kernel, dim3(1), dim3(1024), 0, ps.stream, ps.d_xwcount.p, c->k1a_waves,
+                           c->k1a_xcap, ps.d_xref.p, ps.d_xcount.p);
         HIPCHK(hipGetLastError());
     }
-    dispatch_scan<false, kModeExact>(c, SP, 0, ns);    // K1b: exact blocks
+    dispatch_scan<false, kModeExact>(c, ps.stream, SP, 0, ns);    // K1b: exact blocks
     HIPCHK(hipGetLastError());
 #ifdef UPK_EXP_K1B_TWICE  // experiment: a second (idempotent) K1b over warm caches/TLBs
-    dispatch_scan<false, kModeExact>(c, SP, 0, ns);
+    dispatch_scan<false, kModeExact>(c, ps.stream, SP, 0, ns);
 #endif
-    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[2], c->stream));
+    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[2], ps.stream));
     unsigned long long *thdr = (unsigned long long *)ps.target;
     if (int r = launch_seg_count_head(c, slot)) return r;
-    hipLaunchKernelGGL(seg_compact_kernel, dim3(nsb), dim3(kSegBlock), 0, c->stream, c->d_units.p,
-                       (uint32_t)c->units.size(), c->d_info.p, c->d_cnt.p, c->d_bsum.p, c->d_rec.p,
-                       c->d_ovf_rec.p, c->ovf_cap, c->d_starts.p, c->d_ends.p, c->d_runit.p, c->d_peak_pos.p,
-                       c->d_peak_val.p, ns, (uint64_t)cap, c->d_ovf_count.p, c->d_xcount.p, c->d_nreg.p,
+    hipLaunchKernelGGL(seg_compact_kernel, dim3(nsb), dim3(kSegBlock), 0, ps.stream, c->d_units.p,
+                       (uint32_t)c->units.size(), ps.d_info.p, ps.d_cnt.p, ps.d_bsum.p, ps.d_rec.p,
+                       ps.d_ovf_rec.p, c->ovf_cap, ps.d_starts.p, ps.d_ends.p, ps.d_runit.p, ps.d_peak_pos.p,
+                       ps.d_peak_val.p, ns, (uint64_t)cap, ps.d_ovf_count.p, ps.d_xcount.p, ps.d_nreg.p,
                        c->hp_status[slot].dev, thdr);
     HIPCHK(hipGetLastError());
-    c->counters_armed = true;
-    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[3], c->stream));
-    StatParams P = stat_params(c);
+    ps.counters_armed = true;
+    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[3], ps.stream));
+    StatParams P = stat_params(c, ps);
     P.cap = cap;
-    P.peak_pos = c->d_peak_pos.p;
-    P.peak_val = c->d_peak_val.p;
-    P.spk = c->d_spk.p;
+    P.peak_pos = ps.d_peak_pos.p;
+    P.peak_val = ps.d_peak_val.p;
+    P.spk = ps.d_spk.p;
     // K3 writes the records straight into mapped pinned host memory (or the
     // caller's record target).  Staging them in device memory and delivering
     // them with a DMA copy on a second stream measured within run-to-run
@@ -1199,10 +1257,10 @@ static int launch_pass(up_ctx *c, int slot) {
         P.out = c->hp_regions[slot].dev;
         P.out_counts = c->hp_counts[slot].dev;
     }
-    dispatch_stats(c, P, std::max<uint64_t>(c->last_nreg, 1024));
+    dispatch_stats(c, ps.stream, P, std::max<uint64_t>(c->last_nreg, 1024));
     HIPCHK(hipGetLastError());
-    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[4], c->stream));
-    HIPCHK(hipEventRecord(ps.done, c->stream));
+    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[4], ps.stream));
+    HIPCHK(hipEventRecord(ps.done, ps.stream));
     return UP_OK;
 }
 
@@ -1215,17 +1273,17 @@ static int prepare_run(up_ctx *c) {
 
 int up_run_async(up_ctx *c) {
     if (!c) return UP_E_ARG;
-    if (c->seq_launched - c->seq_done >= 2) return UP_E_STATE;  // at most two passes in flight
+    if (c->seq_launched - c->seq_done >= kSlots) return UP_E_STATE;  // at most kSlots passes in flight
     int r = prepare_run(c);
     if (r) return r;
-    const int slot = (int)(c->seq_launched & 1);
+    const int slot = (int)(c->seq_launched % kSlots);
     c->pass[slot].t0 = std::chrono::steady_clock::now();
     if (c->units.empty()) {
         ++c->seq_launched;
         return UP_OK;
     }
     if ((r = launch_pass(c, slot))) {
-        (void)hipStreamSynchronize(c->stream);
+        sync_all(c);
         c->seq_done = c->seq_launched;  // drop whatever was in flight
         return r;
     }
@@ -1238,7 +1296,7 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
     if (!c) return UP_E_ARG;
     if (!busy(c)) return UP_E_STATE;
     HIPCHK(hipSetDevice(c->dev));
-    const int slot = (int)(c->seq_done & 1);
+    const int slot = (int)(c->seq_done % kSlots);
     up_ctx::Pass &ps = c->pass[slot];
     c->ran = false;
     c->nreg = 0;
@@ -1251,7 +1309,7 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
         return UP_OK;
     }
     auto fail = [&](int rc) {
-        (void)hipStreamSynchronize(c->stream);
+        sync_all(c);
         c->seq_done = c->seq_launched;
         return rc;
     };
@@ -1278,7 +1336,7 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
         if (!again) break;
         // rerun this pass alone with grown areas (a later pass in flight
         // finishes first; its own status tells whether it needs the same)
-        if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(UP_E_HIP);
+        if (hipDeviceSynchronize() != hipSuccess) return fail(UP_E_HIP);
         void *keep_t = c->target, *keep_h = c->target_hostp;
         const uint64_t keep_cap = c->target_cap;
         c->target = ps.target;
@@ -1333,12 +1391,13 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
     ps.target_hostp = c->target_hostp;
     ps.target_cap = c->target_cap;
     if (nu) {
-        HIPCHK(c->d_head.ensure(nu));
-        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)c->d_head.p, 1, nu, c->stream));
+        up_ctx::Pass &p0 = c->pass[0];  // no pass in flight (replay configurations)
+        HIPCHK(p0.d_head.ensure(nu));
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)p0.d_head.p, 1, nu, c->stream));
         std::vector<up_region> emu;
         std::vector<uint32_t> ecnt, resync;
         std::vector<uint64_t> soff;
-        if ((r = emulate_units(c, true, emu, ecnt, resync, soff))) return r;
+        if ((r = emulate_units(c, p0.d_head.p, true, emu, ecnt, resync, soff))) return r;
         const int S = c->p.n_samples;
         std::vector<uint32_t> order(emu.size());
         for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
@@ -1390,7 +1449,7 @@ int up_get_regions(up_ctx *c, up_region *out, uint32_t *counts, size_t cap) {
 
 static void drop_target(up_ctx *c) {
     if (c->target_host && busy(c))  // a pass in flight may still write it
-        (void)hipStreamSynchronize(c->stream);
+        sync_all(c);
     if (c->target_host) (void)hipHostUnregister(c->target_host);
     c->target_host = nullptr;
     c->target = nullptr;
@@ -1456,6 +1515,7 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
     if (!c->p.nondir) return UP_E_UNSUPPORTED;
     if (n == 0) return UP_OK;
     HIPCHK(hipSetDevice(c->dev));
+    up_ctx::Pass &ps = c->pass[c->cur_slot];  // the last completed pass's region lists
     std::vector<uint32_t> st(c->nreg), en(c->nreg);
     if (c->host_regions) {
         // replayed (Q1) regions carry state-machine scores the dense KDE
@@ -1468,15 +1528,15 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
         }
         // replayed regions (Q1 heads, whole-buffer replay) correlate the
         // scores the state machine stored (Region::scores), copied below
-        HIPCHK(c->d_starts.ensure(c->nreg + 1));
-        HIPCHK(c->d_ends.ensure(c->nreg + 1));
-        HIPCHK(c->d_runit.ensure(c->nreg + 1));
-        HIPCHK(hipMemcpy(c->d_starts.p, st.data(), c->nreg * 4, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(c->d_ends.p, en.data(), c->nreg * 4, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(c->d_runit.p, un.data(), c->nreg * 4, hipMemcpyHostToDevice));
+        HIPCHK(ps.d_starts.ensure(c->nreg + 1));
+        HIPCHK(ps.d_ends.ensure(c->nreg + 1));
+        HIPCHK(ps.d_runit.ensure(c->nreg + 1));
+        HIPCHK(hipMemcpy(ps.d_starts.p, st.data(), c->nreg * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(ps.d_ends.p, en.data(), c->nreg * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(ps.d_runit.p, un.data(), c->nreg * 4, hipMemcpyHostToDevice));
     } else {
-        HIPCHK(hipMemcpy(st.data(), c->d_starts.p, c->nreg * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(en.data(), c->d_ends.p, c->nreg * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(st.data(), ps.d_starts.p, c->nreg * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(en.data(), ps.d_ends.p, c->nreg * 4, hipMemcpyDeviceToHost));
     }
     std::vector<uint64_t> off(n);
     uint64_t tot = 0;
@@ -1509,7 +1569,7 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
         HIPCHK(hipMemcpyAsync(d_pref, pref.data(), n + 1, hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
     }
-    StatParams P = stat_params(c);
+    StatParams P = stat_params(c, ps);
     const int nh = P.bw <= 63 ? 1 : 2;
     const int pool = pool_mode(c);
     const size_t lds = kKTab * sizeof(double);
@@ -1551,7 +1611,7 @@ int up_unit_profile_range(up_ctx *c, uint32_t unit, uint64_t first, uint32_t cou
     double *d = nullptr;
     HIPCHK(hipMalloc(&d, 2 * (size_t)count * sizeof(double) + 16));
     HIPCHK(hipMemsetAsync(d, 0, 2 * (size_t)count * sizeof(double), c->stream));
-    ScanParams P = scan_params(c);
+    ScanParams P = scan_params(c, c->pass[0]);  // no pass in flight; records unused
     P.prof_f = d;
     P.prof_r = d + count;
     P.prof_first = (int64_t)first;
@@ -1559,7 +1619,7 @@ int up_unit_profile_range(up_ctx *c, uint32_t unit, uint64_t first, uint32_t cou
     P.prof_unit = unit;
     const uint32_t s0 = u.strip0 + (uint32_t)((first - 1) / kStrip);
     const uint32_t s1 = u.strip0 + (uint32_t)((first + count - 2) / kStrip) + 1;
-    dispatch_scan<true, kModeFused>(c, P, s0, s1);
+    dispatch_scan<true, kModeFused>(c, c->stream, P, s0, s1);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(out_f, d, (size_t)count * sizeof(double), hipMemcpyDeviceToHost));

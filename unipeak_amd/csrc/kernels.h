@@ -70,6 +70,8 @@ struct ScanParams {
     const double *kern; // 2*bw+1 weights
     const uint32_t *wscreen;  // per non-control sample: integer weight >= |pooled share|
     uint32_t wskip;     // a window whose weighted tag sum is <= wskip cannot reach thr
+    float fw[9];        // fine screen: weight bound per chunk distance 0..8 (K1 screen_bits)
+    float fthr;         // a chunk whose weighted bound is <= fthr cannot reach thr
     int32_t bw;
     double thr;
     uint64_t *strip_info;

@@ -413,18 +413,46 @@ __device__ __forceinline__ double wave_max_d(double v) {
 template <int NH, int SW, int W, typename A>
 __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], const double (&c)[kHB],
                                              int lane, int bw, const double *ktab, uint32_t live) {
+#ifdef UPK_EXP_SCATTER_PERWORD
     WordLoop<W - NH, W + NH + 1>::run([&](auto tc) {
         constexpr int t = decltype(tc)::value;
         if constexpr (t >= NH && t < NH + SW) {
             if (!((live >> (t - NH)) & 1u)) return;  // uniform: word holds no flag
-            // output word t-NH, lane position 64(t-NH)+lane; hit at 64(W-NH)+b
             double kv[kHB];
 #pragma unroll
-            for (int h = 0; h < kHB; ++h) kv[h] = ktab[lane + bw - b[h] + 64 * (t - W)];  // 0 outside
+            for (int h = 0; h < kHB; ++h) kv[h] = ktab[lane + bw - b[h] + 64 * (t - W)];
 #pragma unroll
             for (int h = 0; h < kHB; ++h) acc[t - NH] = acc[t - NH] + kv[h] * c[h];
         }
     });
+#else
+    // Every weight read of the batch -- all output words in reach, live or
+    // not (the padded table keeps every index valid) -- is issued before the
+    // first multiply, so one LDS latency is paid per batch instead of one per
+    // output word; the volatile view keeps the compiler from sinking a read
+    // into its word's live branch.
+    constexpr int T0 = W - NH < NH ? NH : W - NH;           // first output window word in reach
+    constexpr int T1 = W + NH > NH + SW - 1 ? NH + SW - 1 : W + NH;
+    constexpr int NT = T1 - T0 + 1;
+    typedef const volatile __attribute__((address_space(3))) double lds_vd;
+    lds_vd *vk = (lds_vd *)ktab;
+    double kv[NT > 0 ? NT : 1][kHB];
+    int base[kHB];
+#pragma unroll
+    for (int h = 0; h < kHB; ++h) base[h] = lane + bw - b[h];
+#pragma unroll
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int h = 0; h < kHB; ++h) kv[q][h] = vk[base[h] + 64 * (T0 + q - W)];  // 0 outside
+    WordLoop<0, (NT > 0 ? NT : 0)>::run([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int t = T0 + q;
+        if (!((live >> (t - NH)) & 1u)) return;  // uniform: word holds no flag
+        // output word t-NH, lane position 64(t-NH)+lane; hit at 64(W-NH)+b
+#pragma unroll
+        for (int h = 0; h < kHB; ++h) acc[t - NH] = acc[t - NH] + kv[q][h] * c[h];
+    });
+#endif
 }
 
 // ------------------------------------------------------------------------
@@ -457,13 +485,20 @@ constexpr size_t kScanLds = kScreenLds + 4 * kStepWords * kWave * sizeof(double)
 constexpr int kXFront = UPK_XFRONT;  // K1b work items with >= this many exact blocks go first
 constexpr size_t kExactLds = kKTab * sizeof(double) + 4 * kStepWords * kWave * sizeof(double);
 
-// chunks 16l .. 16l+15 of lane l whose window of +-R chunks sums to more
-// than wskip.  rd = this lane's row of the padded chunk-sum area (index
-// 16l + j, j = 0..31, holds chunk 16l + j - 8).  Most lanes hold a handful of
-// background tags: when no lane's whole span [16l - R, 16l + 15 + R] exceeds
-// wskip, no window can, and the sliding sums are skipped (wave-uniform).
+// chunks 16l .. 16l+15 of lane l that can hold a position with score >= thr.
+// rd = this lane's row of the padded chunk-sum area (index 16l + j, j =
+// 0..31, holds chunk 16l + j - 8).  Two bounds, both upper bounds of every
+// score in the chunk:
+//  * coarse (integer): kmax * (tags of the lane's span [16l - R, 16l+15+R]);
+//    most lanes hold a handful of background tags, and when no lane's span
+//    exceeds wskip the wave is done (wave-uniform);
+//  * fine (FP32, distance-aware): sum over d of fw[|d|] * (tags of chunk
+//    c + d), fw[d] = the largest kernel weight at the smallest distance
+//    between positions of chunks d apart, inflated by 1e-4 (far above the
+//    FP32 rounding of <= 9 positive terms).  Tags two or more chunks away
+//    weigh less than kmax, so peak flanks stop failing the screen.
 template <int R>
-__device__ __forceinline__ uint32_t screen_bits(const uint32_t *rd, uint32_t wskip) {
+__device__ __forceinline__ uint32_t screen_bits(const uint32_t *rd, uint32_t wskip, const float *fw, float fthr) {
     uint32_t a[16 + 2 * R];  // chunks 16l - R .. 16l + 15 + R
     uint32_t tot = 0;
 #pragma unroll
@@ -474,17 +509,33 @@ __device__ __forceinline__ uint32_t screen_bits(const uint32_t *rd, uint32_t wsk
 #pragma unroll
     for (int j = 0; j < 16 + 2 * R; ++j) tot += a[j];
     if (__ballot(tot > wskip) == 0) return 0u;
-#ifdef UPK_EXP_NOFINE  // timing experiment (wrong results): no sliding window
+#ifdef UPK_EXP_NOFINE  // timing experiment (wrong results): no fine screen
     if (tot != 0xDEADBEEFu) return 0u;
 #endif
-    uint32_t W = 0;
+#ifdef UPK_EXP_INTSCREEN  // A/B: the integer kmax * window-sum bound only
+    {
+        uint32_t W = 0;
 #pragma unroll
-    for (int j = 0; j <= 2 * R; ++j) W += a[j];
-    uint32_t m = W > wskip ? 1u : 0u;
+        for (int j = 0; j <= 2 * R; ++j) W += a[j];
+        uint32_t m = W > wskip ? 1u : 0u;
 #pragma unroll
-    for (int i = 1; i < 16; ++i) {
-        W += a[i + 2 * R] - a[i - 1];
-        m |= (W > wskip ? 1u : 0u) << i;
+        for (int i = 1; i < 16; ++i) {
+            W += a[i + 2 * R] - a[i - 1];
+            m |= (W > wskip ? 1u : 0u) << i;
+        }
+        return m;
+    }
+#endif
+    float f[16 + 2 * R];
+#pragma unroll
+    for (int j = 0; j < 16 + 2 * R; ++j) f[j] = (float)a[j];  // exact: sums < 2^24
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        float b = fw[0] * f[i + R];
+#pragma unroll
+        for (int d = 1; d <= R; ++d) b = __builtin_fmaf(fw[d], f[i + R - d] + f[i + R + d], b);
+        m |= (b > fthr ? 1u : 0u) << i;
     }
     return m;
 }
@@ -498,8 +549,15 @@ __device__ __forceinline__ uint32_t screen_bits(const uint32_t *rd, uint32_t wsk
 // the 2-3 its register count allows: 128 VGPRs with a few spilled registers
 // beat the lower occupancy (hg19 0.35 -> 0.29 ms; nondirectional 0.42 ->
 // 0.30 ms; 8 samples 4.1 -> 2.7 ms).  K1a keeps the compiler's choice.
+#ifndef UPK_K1A_WPE
+#define UPK_K1A_WPE 1
+#endif
+#ifndef UPK_K1B_WPE
+#define UPK_K1B_WPE 4
+#endif
 #ifndef UPK_SCAN_ATTR
-#define UPK_SCAN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == kModeExact ? 4 : 1)))
+#define UPK_SCAN_ATTR \
+    __attribute__((amdgpu_waves_per_eu(MODE == kModeExact ? UPK_K1B_WPE : MODE == kModeScreen ? UPK_K1A_WPE : 1)))
 #endif
 template <int NH, int POOL, bool NONDIR, bool PROF, int MODE>
 __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, uint32_t strip_begin,
@@ -584,12 +642,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             // lane l of wave load q holds positions 2048q + 32l .. +31, i.e.
             // chunks 128q + 2l (dwords x, y) and 128q + 2l + 1 (dwords z, w)
             uint32_t cs[2 * kLoads];
-            uint32_t big = 0, hs0 = 0, hs1 = 0, hbig = 0;
-            // An escape nibble (15) stands for a count the screen does not
-            // know.  When wskip < 15 its chunk fails the screen anyway (sum
-            // >= 15 > wskip, every sample weight >= 1), so only higher
-            // thresholds need the explicit check (any nibble >= 8 -> exact).
-            const bool big_check = P.wskip >= kEsc;
+            uint32_t big = 0, hs0 = 0, hs1 = 0, hbig = 0, anybig = 0;
 #pragma unroll
             for (int k = 0; k < 2 * kLoads; ++k) cs[k] = 0;
             for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
@@ -608,17 +661,33 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                         const uint32_t b = nsum8(v[q].w, nsum8(v[q].z, 0u));
                         cs[2 * q] += POOL == 2 ? a * w : a;
                         cs[2 * q + 1] += POOL == 2 ? b * w : b;
-                        if (big_check) {
-                            big |= (((v[q].x | v[q].y) & 0x88888888u) ? 1u : 0u) << (2 * q);
-                            big |= (((v[q].z | v[q].w) & 0x88888888u) ? 1u : 0u) << (2 * q + 1);
-                        }
+                        anybig |= v[q].x | v[q].y | v[q].z | v[q].w;
                     }
                     const uint32_t ha = nsum8(hv.y, nsum8(hv.x, 0u)), hb = nsum8(hv.w, nsum8(hv.z, 0u));
                     hs0 += POOL == 2 ? ha * w : ha;
                     hs1 += POOL == 2 ? hb * w : hb;
-                    if (big_check) {
-                        hbig |= ((hv.x | hv.y) & 0x88888888u) ? 1u : 0u;
-                        hbig |= ((hv.z | hv.w) & 0x88888888u) ? 2u : 0u;
+                    anybig |= hv.x | hv.y | hv.z | hv.w;
+                }
+            }
+            // A count >= 8 -- the escape nibble 15 among them, whose true count
+            // the screen does not know -- makes its chunk exact (kBig).  Rare:
+            // the strip is re-read (L2) for the per-chunk bits only when some
+            // lane saw such a nibble.
+            if (__ballot((anybig & 0x88888888u) != 0u) != 0) {
+                for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
+                    for (int k = 0; k < P.nnc; ++k) {
+                        gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, ncs[k]) + ((kPadPos + p0 - 1) >> 1));
+#pragma unroll 2
+                        for (int q = 0; q < kLoads; ++q) {
+                            const u32x4 x = t[64 * q + lane];
+                            big |= (((x.x | x.y) & 0x88888888u) ? 1u : 0u) << (2 * q);
+                            big |= (((x.z | x.w) & 0x88888888u) ? 1u : 0u) << (2 * q + 1);
+                        }
+                        if (lane < 8) {
+                            const u32x4 x = t[lane < 4 ? lane - 4 : kLoads * kWave + lane - 4];
+                            hbig |= ((x.x | x.y) & 0x88888888u) ? 1u : 0u;
+                            hbig |= ((x.z | x.w) & 0x88888888u) ? 2u : 0u;
+                        }
                     }
                 }
             }
@@ -652,14 +721,14 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             const uint32_t *rd = scr + 17 * lane;  // index 16l + j = word 17l + j + j/16
             uint32_t m = 0;
             switch (R) {
-            case 1: m = screen_bits<1>(rd, P.wskip); break;
-            case 2: m = screen_bits<2>(rd, P.wskip); break;
-            case 3: m = screen_bits<3>(rd, P.wskip); break;
-            case 4: m = screen_bits<4>(rd, P.wskip); break;
-            case 5: m = screen_bits<5>(rd, P.wskip); break;
-            case 6: m = screen_bits<6>(rd, P.wskip); break;
-            case 7: m = screen_bits<7>(rd, P.wskip); break;
-            default: m = screen_bits<8>(rd, P.wskip); break;
+            case 1: m = screen_bits<1>(rd, P.wskip, P.fw, P.fthr); break;
+            case 2: m = screen_bits<2>(rd, P.wskip, P.fw, P.fthr); break;
+            case 3: m = screen_bits<3>(rd, P.wskip, P.fw, P.fthr); break;
+            case 4: m = screen_bits<4>(rd, P.wskip, P.fw, P.fthr); break;
+            case 5: m = screen_bits<5>(rd, P.wskip, P.fw, P.fthr); break;
+            case 6: m = screen_bits<6>(rd, P.wskip, P.fw, P.fthr); break;
+            case 7: m = screen_bits<7>(rd, P.wskip, P.fw, P.fthr); break;
+            default: m = screen_bits<8>(rd, P.wskip, P.fw, P.fthr); break;
             }
             const uint64_t lanes = __ballot(m != 0u);  // lane l covers chunks 16l..16l+15
             mchunk = m;
@@ -769,6 +838,9 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             }
             WordLoop<0, NWIN>::run([&](auto wc) {
                 constexpr int W = decltype(wc)::value;
+#ifdef UPK_EXP_K1B_NOSCATTER  // timing experiment (wrong results)
+                if (hf[W] != 0x5A5A5A5A5A5Aull) return;
+#endif
                 // output words a hit of window word W reaches: W-2NH .. W
                 constexpr int OLO = W - 2 * NH < 0 ? 0 : W - 2 * NH;
                 constexpr int OHI = W > SW - 1 ? SW - 1 : W;
@@ -819,7 +891,12 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 }
             } else {
                 // ---- flags and run boundaries (only blocks touching a run) ----
+#ifdef UPK_EXP_K1B_NOFLAGS  // timing experiment (wrong results)
+                const uint64_t anyflag = 0;
+                prevF = __ballot(mx == 1.2345) & 1;
+#else
                 const uint64_t anyflag = __ballot(mx >= P.thr);
+#endif
                 if (anyflag | prevF) {
                     // scores through LDS so the word loop below stays a loop
                     // (unrolled, its run bookkeeping overflows the I-cache)
