@@ -213,7 +213,11 @@ def main():
         g.set_record_target(rbuf.data_ptr(), cap)
     it = [0]           # steps launched
     timed = [False]    # inside the timed region
-    K1A_EVERY = 4      # timed passes with HIP events around K1a (roofline sample)
+    # timed passes with HIP events around K1a (the roofline sample): every
+    # pass -- consecutive passes overlap and alternate between a K1a that runs
+    # beside one earlier pass's kernels and one beside two, so a sparser
+    # sample would see one phase only
+    K1A_EVERY = int(os.environ.get("UNIPEAK_K1A_EVERY", "1"))
     ar = [None]        # the next step's background all-reduce, in flight
     reads = []         # rank 0: (step, future) of record reads in flight
     done_times = []    # per completed pass: library timings
@@ -325,7 +329,7 @@ def main():
         tt = done_times[-1]
         print(f"[bench] warmup: K1 {tt[0]:.3f} ms (exact part {tt[4]:.3f}), K2 {tt[1]:.3f} ms, "
               f"K3 {tt[2]:.3f} ms, pass wall {tt[3]:.3f} ms", file=sys.stderr, flush=True)
-    g.set_timing(1)  # timed passes: HIP events around K1a only (each pair idles the GPU a few us)
+    g.set_timing(1)  # timed passes: HIP events around K1a only
     timed[0] = True
     for k in phase:
         phase[k] = 0.0
@@ -343,6 +347,16 @@ def main():
         comm.torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     last = (None, final if final is not None else (n0, 0), None)
+    # after the timed region: blocking passes (nothing overlapping) for the
+    # per-kernel breakdown of one pass on an otherwise idle GPU
+    iso = []
+    if pipelined:
+        g.set_record_target(nr.my_slot_address(it[0]), cap)
+    g.set_timing(2)
+    for _ in range(3):
+        g.run()
+        iso.append(g.timings())
+    iso = [float(np.median([t[k] for t in iso])) for k in range(5)]
     # K1a = K1 minus its exact part (timing level 1: K1b = 0); level-0 passes carry no events
     k1a = [t[0] - t[4] for t in done_times if t[0] > 0] or [t[0] for t in done_times]
     k1 = k1a
@@ -399,11 +413,13 @@ def main():
                          "kernel_ms": round(k1a_ms, 4), "kernel_ms_max_rank": round(k1a_max, 4),
                          "bytes_per_launch": int(alg_bytes),
                          "bytes_rule": "0.5 B (4-bit count) per bp per strand per non-control sample",
-                         "k1_total_ms": round(k1a_ms + warm[4], 4),
-                         "k1b_exact_ms": round(warm[4], 4),
-                         "k2_ms": round(warm[1], 4), "k3_ms": round(warm[2], 4),
-                         "phase_ms_note": "K1b/K2/K3 from the last warm-up pass (timing level 2); "
-                                          "timed passes carry HIP events around K1a only",
+                         "kernel_note": "mean K1a duration over the timed passes (HIP events on the pass "
+                                        "stream); passes overlap, so K1a shares the GPU with earlier "
+                                        "passes' K1b/K2/K3",
+                         "isolated_ms": {"k1a": round(iso[0] - iso[4], 4), "k1b_k1x": round(iso[4], 4),
+                                         "k2": round(iso[1], 4), "k3": round(iso[2], 4),
+                                         "pass_wall": round(iso[3], 4)},
+                         "frac_isolated": round(alg_bytes / ((iso[0] - iso[4]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "hbm_copy_GBps": round(copy_gbps, 1),
                          "frac_of_copy_rate": round(achieved / copy_gbps, 4)},
             "setup_s": round(gen_s, 2),

@@ -97,6 +97,7 @@ struct up_ctx {
     int dev = 0;
     int ncu = 0;                     // compute units of the device
     int k1a_per_cu = 2;              // K1a workgroups per CU (UNIPEAK_K1A_PER_CU; 0 = resident max)
+    bool use_graphs = true;          // passes as hipGraphs (UNIPEAK_GRAPHS=0: plain launches)
     hipStream_t stream = nullptr;
     bool have_params = false;
     up_params p{};
@@ -136,6 +137,9 @@ struct up_ctx {
     struct Pass {
         hipStream_t stream = nullptr;
         hipEvent_t k1a_end = nullptr;   // this pass's K1a finished
+        // K1x..K3 of the pass as hipGraphs, one per launch-argument set
+        // (record targets rotate), most recent first
+        std::vector<std::pair<std::vector<uint8_t>, hipGraphExec_t>> graphs;
         bool counters_armed = false;    // xcount / ovf_count are zero (re-armed by K2b)
         DevBuf<uint64_t> d_info;
         DevBuf<uint32_t> d_rec, d_ovf_count, d_ovf_rec, d_head;
@@ -270,6 +274,7 @@ int up_open(int hip_device, up_ctx **out) {
     HIPCHK(hipSetDevice(hip_device));
     HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     if (const char *e = getenv("UNIPEAK_K1A_PER_CU")) c->k1a_per_cu = atoi(e);
+    if (const char *e = getenv("UNIPEAK_GRAPHS")) c->use_graphs = e[0] != '0';
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     for (auto &ps : c->pass) {
@@ -317,6 +322,7 @@ void up_close(up_ctx *c) {
         for (auto &e : c->pass[k].ev) (void)hipEventDestroy(e);
         (void)hipEventDestroy(c->pass[k].done);
         (void)hipEventDestroy(c->pass[k].k1a_end);
+        for (auto &g : c->pass[k].graphs) (void)hipGraphExecDestroy(g.second);
         c->pass[k].release();
         (void)hipStreamDestroy(c->pass[k].stream);
     }
@@ -1150,12 +1156,49 @@ static int replay_head_hits(up_ctx *c, int slot) {
     return publish_host_regions(c, ps);
 }
 
-// Enqueue one pass K1a -> K1b -> K2a -> K2b -> K3 -> head detect into `slot`
-// with no host round trip: the region count stays on the device, the record
-// areas are pre-sized (reg_cap, ovf_cap) and K3 writes the records straight
-// into mapped pinned host memory (or the caller's record target).  An
-// undersized area is detected when the pass is finished; it is grown and
-// the pass rerun (first passes only).
+template <typename T>
+static void key_add(std::vector<uint8_t> &k, const T &v) {
+    const uint8_t *b = (const uint8_t *)&v;
+    k.insert(k.end(), b, b + sizeof(T));
+}
+
+// K1x -> K1b -> K2a -> K2b -> K3 of a pass on ps.stream (the timing events
+// between them only at timing level 2, never while capturing)
+static int enqueue_rest(up_ctx *c, int slot, const ScanParams &SP, const StatParams &P, uint64_t cap,
+                        uint32_t k1a_waves, uint32_t k1a_xcap, bool events) {
+    up_ctx::Pass &ps = c->pass[slot];
+    const uint32_t ns = c->nstrips;
+    const uint32_t nsb = (ns + kSegBlock - 1) / kSegBlock;
+    if (k1a_waves) {  // K1x: list the stashed work-list entries for K1b
+        hipLaunchKernelGGL(xref_kernel, dim3(1), dim3(1024), 0, ps.stream, ps.d_xwcount.p, k1a_waves,
+                           k1a_xcap, ps.d_xref.p, ps.d_xcount.p);
+        HIPCHK(hipGetLastError());
+    }
+    dispatch_scan<false, kModeExact>(c, ps.stream, SP, 0, ns);    // K1b: exact blocks
+    HIPCHK(hipGetLastError());
+    if (events) HIPCHK(hipEventRecord(ps.ev[2], ps.stream));
+    unsigned long long *thdr = (unsigned long long *)ps.target;
+    if (int r = launch_seg_count_head(c, slot)) return r;
+    hipLaunchKernelGGL(seg_compact_kernel, dim3(nsb), dim3(kSegBlock), 0, ps.stream, c->d_units.p,
+                       (uint32_t)c->units.size(), ps.d_info.p, ps.d_cnt.p, ps.d_bsum.p, ps.d_rec.p,
+                       ps.d_ovf_rec.p, c->ovf_cap, ps.d_starts.p, ps.d_ends.p, ps.d_runit.p, ps.d_peak_pos.p,
+                       ps.d_peak_val.p, ns, (uint64_t)cap, ps.d_ovf_count.p, ps.d_xcount.p, ps.d_nreg.p,
+                       c->hp_status[slot].dev, thdr);
+    HIPCHK(hipGetLastError());
+    if (events) HIPCHK(hipEventRecord(ps.ev[3], ps.stream));
+    dispatch_stats(c, ps.stream, P, std::max<uint64_t>(c->last_nreg, 1024));
+    HIPCHK(hipGetLastError());
+    if (events) HIPCHK(hipEventRecord(ps.ev[4], ps.stream));
+    return UP_OK;
+}
+
+// Enqueue one pass K1a -> K1x -> K1b -> K2a -> K2b -> K3 into `slot` with no
+// host round trip: the region count stays on the device, the record areas
+// are pre-sized (reg_cap, ovf_cap) and K3 writes the records straight into
+// mapped pinned host memory (or the caller's record target).  An undersized
+// area is detected when the pass is finished; it is grown and the pass rerun
+// (first passes only).  K1a is launched directly (between its timing
+// events); K1x..K3 go out as one cached hipGraph of the slot.
 static int launch_pass(up_ctx *c, int slot) {
     const uint32_t ns = c->nstrips;
     const int S = c->p.n_samples;
@@ -1181,6 +1224,8 @@ static int launch_pass(up_ctx *c, int slot) {
     HIPCHK(ps.d_starts.ensure(cap + 1));
     HIPCHK(ps.d_ends.ensure(cap + 1));
     HIPCHK(ps.d_runit.ensure(cap + 1));
+    HIPCHK(ps.d_head.ensure(c->units.size()));
+    HIPCHK(c->hp_head[slot].ensure(c->units.size()));
     if (!c->target) {
         HIPCHK(c->hp_regions[slot].ensure(cap + 1));
         HIPCHK(c->hp_counts[slot].ensure((cap + 1) * S));
@@ -1190,56 +1235,30 @@ static int launch_pass(up_ctx *c, int slot) {
     ps.target_cap = c->target_cap;
     ps.cap = cap;
     ps.ovf_cap = c->ovf_cap;
+    // the pass follows everything enqueued on the context stream (track
+    // writes), and its K1a follows the K1a of the previous pass if that one
+    // is in flight: one streaming K1a at a time, earlier passes' K1b/K2/K3
+    // beside it
+    HIPCHK(hipEventRecord(c->host_work, c->stream));
+    HIPCHK(hipStreamWaitEvent(ps.stream, c->host_work, 0));
+    if (c->seq_launched > c->seq_done)
+        HIPCHK(hipStreamWaitEvent(ps.stream, c->pass[(slot + kSlots - 1) % kSlots].k1a_end, 0));
     if (!ps.counters_armed) {  // K2b re-arms them at the end of every pass
         HIPCHK(hipMemsetAsync(ps.d_ovf_count.p, 0, sizeof(uint32_t), ps.stream));
         HIPCHK(hipMemsetAsync(ps.d_xcount.p, 0, 2 * sizeof(uint32_t), ps.stream));
     }
-    ps.counters_armed = false;  // until K2b is enqueued
     ScanParams SP = scan_params(c, ps);
+    bool graph = c->use_graphs;
 #ifdef UPK_DEBUG_COUNTS
     static const bool dbg = getenv("UNIPEAK_DEBUG_COUNTS") != nullptr;
     if (dbg) {
-        HIPCHK(c->d_dbg.ensure(8));
-        HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 8 * sizeof(unsigned long long), ps.stream));
+        HIPCHK(c->d_dbg.ensure(32));
+        HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 32 * sizeof(unsigned long long), ps.stream));
         SP.dbg = c->d_dbg.p;
+        graph = false;
     }
 #endif
-    const int tl = c->timing;
-    ps.tl = tl;
-    // the pass follows everything enqueued on the context stream (track
-    // writes), and its K1a follows the K1a of the pass in flight in the other
-    // slot: one streaming K1a at a time, the other pass's K1b/K2/K3 beside it
-    HIPCHK(hipEventRecord(c->host_work, c->stream));
-    HIPCHK(hipStreamWaitEvent(ps.stream, c->host_work, 0));
-    if (c->seq_launched > c->seq_done)  // the previous pass is in flight
-        HIPCHK(hipStreamWaitEvent(ps.stream, c->pass[(slot + kSlots - 1) % kSlots].k1a_end, 0));
-    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[0], ps.stream));
-    c->k1a_waves = 0;
-    dispatch_scan<false, kModeScreen>(c, ps.stream, SP, 0, ns);   // K1a: stream + screen
-    HIPCHK(hipGetLastError());
-    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[1], ps.stream));
-    HIPCHK(hipEventRecord(ps.k1a_end, ps.stream));
-    if (c->k1a_waves) {  // K1x: list the stashed work-list entries for K1b
-        hipLaunchKernelGGL(xref_kernel, dim3(1), dim3(1024), 0, ps.stream, ps.d_xwcount.p, c->k1a_waves,
-                           c->k1a_xcap, ps.d_xref.p, ps.d_xcount.p);
-        HIPCHK(hipGetLastError());
-    }
-    dispatch_scan<false, kModeExact>(c, ps.stream, SP, 0, ns);    // K1b: exact blocks
-    HIPCHK(hipGetLastError());
-#ifdef UPK_EXP_K1B_TWICE  // experiment: a second (idempotent) K1b over warm caches/TLBs
-    dispatch_scan<false, kModeExact>(c, ps.stream, SP, 0, ns);
-#endif
-    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[2], ps.stream));
-    unsigned long long *thdr = (unsigned long long *)ps.target;
-    if (int r = launch_seg_count_head(c, slot)) return r;
-    hipLaunchKernelGGL(seg_compact_kernel, dim3(nsb), dim3(kSegBlock), 0, ps.stream, c->d_units.p,
-                       (uint32_t)c->units.size(), ps.d_info.p, ps.d_cnt.p, ps.d_bsum.p, ps.d_rec.p,
-                       ps.d_ovf_rec.p, c->ovf_cap, ps.d_starts.p, ps.d_ends.p, ps.d_runit.p, ps.d_peak_pos.p,
-                       ps.d_peak_val.p, ns, (uint64_t)cap, ps.d_ovf_count.p, ps.d_xcount.p, ps.d_nreg.p,
-                       c->hp_status[slot].dev, thdr);
-    HIPCHK(hipGetLastError());
-    ps.counters_armed = true;
-    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[3], ps.stream));
+    ps.tl = c->timing;
     StatParams P = stat_params(c, ps);
     P.cap = cap;
     P.peak_pos = ps.d_peak_pos.p;
@@ -1257,9 +1276,63 @@ static int launch_pass(up_ctx *c, int slot) {
         P.out = c->hp_regions[slot].dev;
         P.out_counts = c->hp_counts[slot].dev;
     }
-    dispatch_stats(c, ps.stream, P, std::max<uint64_t>(c->last_nreg, 1024));
+    ps.counters_armed = true;  // K2b re-arms them
+    const int tl = ps.tl;
+    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[0], ps.stream));
+    c->k1a_waves = 0;
+    dispatch_scan<false, kModeScreen>(c, ps.stream, SP, 0, ns);   // K1a: stream + screen
     HIPCHK(hipGetLastError());
-    if (tl >= 2) HIPCHK(hipEventRecord(ps.ev[4], ps.stream));
+    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[1], ps.stream));
+    HIPCHK(hipEventRecord(ps.k1a_end, ps.stream));
+    const uint32_t kw = c->k1a_waves, kx = c->k1a_xcap;
+    if (!graph || tl >= 2) {
+        if (int r = enqueue_rest(c, slot, SP, P, cap, kw, kx, tl >= 2)) return r;
+        HIPCHK(hipEventRecord(ps.done, ps.stream));
+        return UP_OK;
+    }
+    // every launch argument of K1x..K3: parameter blocks and grid inputs
+    std::vector<uint8_t> key;
+    key_add(key, SP);
+    key_add(key, P);
+    key_add(key, kw);
+    key_add(key, kx);
+    key_add(key, std::max<uint64_t>(c->last_nreg, 1024));
+    key_add(key, (uint32_t)c->units.size());
+    key_add(key, c->ovf_cap);
+    key_add(key, pool_mode(c));
+    key_add(key, c->p.nondir);
+    key_add(key, c->nc.size());
+    key_add(key, c->hp_head[slot].dev);
+    key_add(key, c->hp_status[slot].dev);
+    key_add(key, ps.d_head.p);
+    key_add(key, c->d_coef.p);
+    key_add(key, ps.target);
+    key_add(key, ps.d_cnt.p);
+    key_add(key, ps.d_bsum.p);
+    size_t gi = 0;
+    while (gi < ps.graphs.size() && ps.graphs[gi].first != key) ++gi;
+    if (gi == ps.graphs.size()) {
+        HIPCHK(hipStreamBeginCapture(ps.stream, hipStreamCaptureModeThreadLocal));
+        const int r = enqueue_rest(c, slot, SP, P, cap, kw, kx, false);
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(ps.stream, &g);
+        if (r) {
+            if (g) (void)hipGraphDestroy(g);
+            return r;
+        }
+        HIPCHK(e);
+        hipGraphExec_t x = nullptr;
+        const hipError_t ei = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        HIPCHK(ei);
+        if (ps.graphs.size() >= 8) {  // keep the most recent ones
+            (void)hipGraphExecDestroy(ps.graphs.back().second);
+            ps.graphs.pop_back();
+        }
+        ps.graphs.insert(ps.graphs.begin(), {key, x});
+        gi = 0;
+    }
+    HIPCHK(hipGraphLaunch(ps.graphs[gi].second, ps.stream));
     HIPCHK(hipEventRecord(ps.done, ps.stream));
     return UP_OK;
 }
@@ -1327,10 +1400,13 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
         if (ps.target && nreg > ps.target_cap) return fail(UP_E_NOMEM);  // caller's buffer too small
 #ifdef UPK_DEBUG_COUNTS
         if (getenv("UNIPEAK_DEBUG_COUNTS")) {
-            unsigned long long h[8];
+            unsigned long long h[32];
             HIPCHK(hipMemcpy(h, c->d_dbg.p, sizeof h, hipMemcpyDeviceToHost));
             fprintf(stderr, "unipeak_hip: K1 strips %u exact blocks %llu live words %llu hits %llu "
                             "cycles load %llu scatter %llu\n", c->nstrips, h[0], h[1], h[2], h[3], h[4]);
+            fprintf(stderr, "unipeak_hip: K1b items by exact blocks:");
+            for (int k = 1; k <= 16; ++k) fprintf(stderr, " %d:%llu", k, h[8 + k]);
+            fprintf(stderr, "\n");
         }
 #endif
         if (!again) break;

@@ -628,6 +628,9 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             mchunk = (e[2 + (lane >> 1)] >> (16 * (lane & 1))) & 0xFFFFu;
             // K1a stored the unit with the entry (no dependent binary search)
             cur = e1 >> 16;
+#ifdef UPK_DEBUG_COUNTS
+            if (lane == 0) atomicAdd(&P.dbg[8 + __builtin_popcount(exact_blocks)], 1ull);  // blocks per item
+#endif
             if (cur == 0xFFFFu) cur = find_unit(units, P.nunits, strip);
         } else {
             if (!have) { cur = find_unit(units, P.nunits, strip); have = true; }
