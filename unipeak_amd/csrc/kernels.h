@@ -120,6 +120,8 @@ struct StatParams {
     uint64_t cap;         // records the output areas hold
     void *out;            // up_region records (mapped host memory in up_run)
     uint32_t *out_counts; // [n][S]
+    double *corr_scratch; // -D -y: per K3 wave corr_cap (f, r) pairs, or null
+    uint32_t corr_cap;
 };
 
 }  // namespace upk

@@ -1212,7 +1212,10 @@ __device__ __forceinline__ void region_words(WinT<POOL> (&cs)[2 * NH + 1], uint6
 }
 
 template <int NH, int POOL, bool NONDIR>
-__global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
+#ifndef UPK_K3_WPE
+#define UPK_K3_WPE 1
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3_WPE))) stats_kernel(StatParams P) {
     extern __shared__ double lds_[];
     const int bw = P.bw;
     const double *ktab = load_ktab(lds_, P.kern, bw);
@@ -1233,6 +1236,9 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
     // per-wave cache of the pass-1 hit totals pc (pass 2 reads them back)
     uint32_t *pcache = (uint32_t *)(lds_ + kKTab) + (threadIdx.x >> 6) * (kStatCache * 64);
     double2 *terms = (double2 *)((uint32_t *)(lds_ + kKTab) + 4 * kStatCache * 64) + (threadIdx.x >> 6) * 64;
+    // this wave's slab of (f, r) per region position for the correlation
+    double2 *cslab = (NONDIR && P.want_corr && P.corr_scratch)
+                         ? (double2 *)P.corr_scratch + (uint64_t)wave * P.corr_cap : nullptr;
 
     for (uint64_t ri = wave; ri < nreg; ri += nwaves) {
         const uint32_t left = P.starts[ri], right = P.ends[ri], u = P.reg_unit[ri];
@@ -1415,10 +1421,24 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
             const double score = NONDIR ? f + r : f;
             if (valid && (best_x < 0 || score > best)) { best = score; best_x = x; }
             if (NONDIR && P.want_corr) {
+                // pass 3 reads f, r back from this wave's slab instead of
+                // recomputing the KDE
+                const int64_t off = x0 - (int64_t)left;
+                if (cslab && off + 64 <= (int64_t)P.corr_cap) cslab[off + lane] = make_double2(f, r);
+                // the two sums stay sequential in position order
+                // (data.cpp:22-30): each position's (f, r) is read back as a
+                // wave-uniform LDS broadcast (one ds_read_b128 per position
+                // instead of four readlanes)
+                terms[lane] = make_double2(f, r);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 for (int l = 0; l < nvalid; ++l) {
-                    sf = sf + rl_d(f, l);
-                    sr = sr + rl_d(r, l);
+                    const double2 v = terms[l];
+                    sf = sf + v.x;
+                    sr = sr + v.y;
                 }
+                __builtin_amdgcn_wave_barrier();  // terms reused by the next word
             }
             // stored hit vectors (peakcall.cpp:210-219; quirk Q7)
             const bool sf_hit = (hf[NH] >> lane) & 1, sr_hit = (hr_c >> lane) & 1;
@@ -1558,21 +1578,36 @@ __global__ void __launch_bounds__(256) stats_kernel(StatParams P) {
         if (NONDIR && P.want_corr && n > 3) {
             const double m1 = sf / (double)n, m2 = sr / (double)n;
             double ss1 = 0.0, ss2 = 0.0, ssr = 0.0;
+            const bool cached = cslab && (uint64_t)n + 63 <= P.corr_cap;
+            double *prod = (double *)pcache;  // 64 x (p1, p2, p3); pass 2 is done with pcache
             for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
                 const int nvalid = (int)(((int64_t)right - x0 + 1) < 64 ? ((int64_t)right - x0 + 1) : 64);
-                WinT<POOL> cf[NWT], cr[NWT];
-                uint64_t hf[NWT], hr[NWT];
-                region_words<NH, POOL>(cf, hf, U, 0, x0, lane, P);
-                region_words<NH, POOL>(cr, hr, U, 1, x0, lane, P);
-                const double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
-                const double r = kde_word<NWT, NH, NH>(cr, hr, wm, lane, bw, ktab);
-                const double d1 = f - m1, d2 = r - m2;
-                const double p1 = d1 * d1, p2 = d2 * d2, p3 = d1 * d2;
-                for (int l = 0; l < nvalid; ++l) {
-                    ss1 = ss1 + rl_d(p1, l);
-                    ss2 = ss2 + rl_d(p2, l);
-                    ssr = ssr + rl_d(p3, l);
+                double f, r;
+                if (cached) {
+                    const double2 v = cslab[x0 - (int64_t)left + lane];
+                    f = v.x;
+                    r = v.y;
+                } else {
+                    WinT<POOL> cf[NWT], cr[NWT];
+                    uint64_t hf[NWT], hr[NWT];
+                    region_words<NH, POOL>(cf, hf, U, 0, x0, lane, P);
+                    region_words<NH, POOL>(cr, hr, U, 1, x0, lane, P);
+                    f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
+                    r = kde_word<NWT, NH, NH>(cr, hr, wm, lane, bw, ktab);
                 }
+                const double d1 = f - m1, d2 = r - m2;
+                prod[3 * lane] = d1 * d1;
+                prod[3 * lane + 1] = d2 * d2;
+                prod[3 * lane + 2] = d1 * d2;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int l = 0; l < nvalid; ++l) {  // sequential sums, broadcast reads
+                    ss1 = ss1 + prod[3 * l];
+                    ss2 = ss2 + prod[3 * l + 1];
+                    ssr = ssr + prod[3 * l + 2];
+                }
+                __builtin_amdgcn_wave_barrier();
             }
             const double sd1 = sqrt(ss1 / ((double)n - 1));
             const double sd2 = sqrt(ss2 / ((double)n - 1));

@@ -58,22 +58,54 @@ def plan(contig_lens, nondir, world, n_samples=1):
     return units, owner, mine
 
 
+class BlockOrder:
+    """Zero-copy global-unit order of per-rank, unit-major record blocks for
+    a fixed plan: the (rank, local unit) order by global unit id is computed
+    once; per step only each rank's unit boundaries are searched (one
+    vectorised searchsorted per rank), so rank 0's merge costs tens of
+    microseconds for ~40 k records instead of a Python pass per record block."""
+
+    def __init__(self, mine_all):
+        self.mine = [np.asarray(m, np.int64) for m in mine_all]
+        pairs = sorted((int(g), r, li) for r, m in enumerate(self.mine) for li, g in enumerate(m))
+        self.order = [(g, r, li) for g, r, li in pairs]
+        self.probe = [np.arange(len(m) + 1, dtype=np.uint32) for m in self.mine]
+
+    def spans(self, parts):
+        """parts: [(records, counts or None)] per rank -> ([(global unit,
+        rank, first, end)] in global unit order for the units with records,
+        total records).  Record i of the merged order is parts[rank][0][first
+        + k]: a zero-copy index, not a copy."""
+        bounds, n = [], 0
+        for r, (recs, _) in enumerate(parts):
+            if len(recs):
+                b = np.searchsorted(recs["unit"], self.probe[r]).tolist()
+                bounds.append(b)
+                n += len(recs)
+            else:
+                bounds.append(None)
+        out = []
+        for g, r, li in self.order:
+            b = bounds[r]
+            if b is not None and b[li + 1] > b[li]:
+                out.append((g, r, b[li], b[li + 1]))
+        return out, n
+
+    def blocks(self, parts):
+        """spans() materialised as (global unit, records view, counts view)
+        blocks, plus the total and the accepted count"""
+        spans, n = self.spans(parts)
+        acc = sum(int(np.count_nonzero(recs["accepted"])) for recs, _ in parts if len(recs))
+        out = [(g, parts[r][0][a:e], None if parts[r][1] is None else parts[r][1][a:e])
+               for g, r, a, e in spans]
+        return out, n, acc
+
+
 def order_blocks(parts):
     """Zero-copy form of merge(): [(global unit, records view, counts view)]
     in global unit order, one block per (rank, unit) with records."""
-    blocks = []
-    for recs, gids, cnt in parts:
-        if len(recs) == 0:
-            continue
-        gids = np.asarray(gids, np.int64)
-        loc = recs["unit"].astype(np.int64)
-        bounds = np.searchsorted(loc, np.arange(len(gids) + 1), side="left")
-        for li, g in enumerate(gids):
-            a, b = int(bounds[li]), int(bounds[li + 1])
-            if b > a:
-                blocks.append((int(g), recs[a:b], None if cnt is None else cnt[a:b]))
-    blocks.sort(key=lambda t: t[0])
-    return blocks
+    bo = BlockOrder([gids for _, gids, _ in parts])
+    return bo.blocks([(recs, cnt) for recs, _, cnt in parts])[0]
 
 
 def merge(parts, n_units, dtype):
@@ -139,27 +171,44 @@ class Comm:
         return v
 
     def global_tags_start(self, local_tags: int):
-        """Start the same all-reduce without waiting for it (one step ahead):
-        its RCCL kernel runs whenever the device has room -- a pass holds
-        every CU while it streams -- and global_tags_finish() collects it."""
+        """Start the same all-reduce without waiting for it (steps ahead):
+        its RCCL kernel runs whenever the device has room, on a high-priority
+        side stream, and global_tags_finish() collects it."""
         torch = self.torch
         if self.device == "cpu":
             t = torch.tensor([int(local_tags)], dtype=torch.int64)
             return (self.dist.all_reduce(t, async_op=True), t)
-        if getattr(self, "_side", None) is None:
-            self._tags = torch.zeros(1, dtype=torch.int64, device=self.device)
-            self._side = torch.cuda.Stream(device=self.device)
+        if getattr(self, "_ring", None) is None:
+            # high priority: its kernels go ahead of queued pass kernels
+            self._side = torch.cuda.Stream(device=self.device, priority=-1)
+            self._ring = [(torch.zeros(1, dtype=torch.int64, pin_memory=True),
+                           torch.zeros(1, dtype=torch.int64, device=self.device),
+                           torch.zeros(1, dtype=torch.int64, pin_memory=True),
+                           torch.cuda.Event()) for _ in range(8)]
+            self._ri = 0
+        h_in, d, h_out, ev = self._ring[self._ri]
+        self._ri = (self._ri + 1) % len(self._ring)
+        h_in[0] = int(local_tags)
         with torch.cuda.stream(self._side):
-            t = torch.full((1,), int(local_tags), dtype=torch.int64, device=self.device)
-            return (self.dist.all_reduce(t, async_op=True), t)
+            d.copy_(h_in, non_blocking=True)
+            self.dist.all_reduce(d, async_op=True).wait()  # the side stream waits, the host does not
+            # the sum lands in pinned host memory by an async copy; finish
+            # waits for its event only (.item() on the busy device waited
+            # ~0.35 ms per step behind queued pass kernels)
+            h_out.copy_(d, non_blocking=True)
+            ev.record(self._side)
+        return ("gpu", ev, h_out)
 
     def global_tags_finish(self, handle) -> int:
+        """The all-reduced tag total of a global_tags_start() handle (the
+        ring holds 8 handles: at most 8 may be in flight)."""
+        if handle[0] == "gpu":
+            _, ev, h = handle
+            ev.synchronize()
+            return int(h[0])
         work, t = handle
         work.wait()
-        if self.device == "cpu":
-            return int(t.item())
-        with self.torch.cuda.stream(self._side):
-            return int(t.item())
+        return int(t.item())
 
     def max_over_ranks(self, x: float) -> float:
         t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=self.device)
