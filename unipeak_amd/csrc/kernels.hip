@@ -545,15 +545,17 @@ __device__ __forceinline__ uint32_t screen_bits(const uint32_t *rd, uint32_t wsk
 // MODE kModeExact (K1b): run the exact blocks of the listed strips, so the
 // latency-bound KDE never stalls the streaming waves.  kModeFused: both in
 // one pass (the PROF profile variant, every block exact).
-// K1b runs 4 waves per SIMD (the LDS limit of its 38 KiB blocks) instead of
-// the 2-3 its register count allows: 128 VGPRs with a few spilled registers
-// beat the lower occupancy (hg19 0.35 -> 0.29 ms; nondirectional 0.42 ->
-// 0.30 ms; 8 samples 4.1 -> 2.7 ms).  K1a keeps the compiler's choice.
+// K1b runs 3 waves per SIMD (168 VGPRs, a few spilled).  Alone, 4 waves
+// (128 VGPRs) finish it sooner (hg19 0.28 vs 0.31 ms), but K1b runs beside
+// the next passes' K1a, and fewer latency-bound K1b waves leave K1a more of
+// the CU: overlapped K1a 0.72 -> 0.67 ms, bench 4,010 -> 4,160 Gbp/s;
+// nondirectional 2,710 -> 2,880; 8 samples 523 -> 528 (tools/ab_libs2.sh).
+// K1a keeps the compiler's choice.
 #ifndef UPK_K1A_WPE
 #define UPK_K1A_WPE 1
 #endif
 #ifndef UPK_K1B_WPE
-#define UPK_K1B_WPE 4
+#define UPK_K1B_WPE 3
 #endif
 #ifndef UPK_SCAN_ATTR
 #define UPK_SCAN_ATTR \
