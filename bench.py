@@ -198,7 +198,10 @@ def main():
     # waits for the host between passes and consecutive passes overlap on the
     # device (a pass's streaming K1a beside the previous passes' exact and
     # statistics kernels); NSLOT rotating record slots per rank
-    DEPTH, NSLOT = 3, 6
+    # (NSLOT a multiple of the library's pass slots: each pass slot then cycles
+    # through two record targets, i.e. two cached graphs)
+    DEPTH = int(os.environ.get("UNIPEAK_BENCH_DEPTH", str(capi.MAX_IN_FLIGHT)))
+    NSLOT = 2 * capi.MAX_IN_FLIGHT
     pipelined = comm is None or gather_mode == "shm"
     if pipelined:
         tag = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}_{os.environ.get('MASTER_PORT', '0')}"

@@ -147,14 +147,15 @@ int up_reset_units(up_ctx *ctx);
  * scores (Region::scores), as strandCorr does. */
 int up_run(up_ctx *ctx, uint64_t *n_regions);
 /* Pipelined form of up_run: up_run_async enqueues one pass and returns
- * (at most three passes in flight); up_run_wait completes the OLDEST pass in
+ * (at most UP_MAX_IN_FLIGHT passes in flight); up_run_wait completes the OLDEST pass in
  * flight and makes its records current (as up_run would).  Passes in flight
  * overlap on the device: a pass's streaming K1a starts when the previous
  * pass's K1a has ended, beside that pass's exact/segmentation/statistics
  * kernels.  Each pass delivers into the record target that was set when it
  * was launched, so a caller rotates targets; with host delivery the view of
- * a pass stays valid until the third following launch.  Units and
+ * a pass stays valid until the UP_MAX_IN_FLIGHT-th following launch.  Units and
  * parameters cannot change while a pass is in flight (UP_E_STATE). */
+#define UP_MAX_IN_FLIGHT 5
 int up_run_async(up_ctx *ctx);
 int up_run_wait(up_ctx *ctx, uint64_t *n_regions);
 /* device timing of passes launched from now on (passes in flight keep

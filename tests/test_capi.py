@@ -19,6 +19,13 @@ def declared_symbols():
     return sorted(set(re.findall(r"\b(up_[a-z_]+)\s*\(", src)))
 
 
+def test_header_constants_match_capi():
+    """the Python mirror's copies of header constants"""
+    src = open(os.path.join(ROOT, "include", "unipeak_hip.h")).read()
+    m = re.search(r"#define\s+UP_MAX_IN_FLIGHT\s+(\d+)", src)
+    assert m and int(m.group(1)) == capi.MAX_IN_FLIGHT
+
+
 def test_library_exports_header():
     L = capi.load_library()
     syms = declared_symbols()

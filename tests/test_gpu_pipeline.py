@@ -1,8 +1,8 @@
 """Pipelined passes (up_run_async / up_run_wait, include/unipeak_hip.h):
-two or three passes in flight (each on its own stream and buffers, a pass's
+two, three or UP_MAX_IN_FLIGHT passes in flight (each on its own stream and buffers, a pass's
 K1a overlapping the previous passes' K1b/K2/K3), each delivering into the
 record target that was set when it was launched, give exactly the records of
-the blocking up_run; a fourth launch is refused; state
+the blocking up_run; one launch more than UP_MAX_IN_FLIGHT is refused; state
 cannot change under a pass in flight; the K2 segmentation (two launches,
 re-armed counters) stays exact across many passes and across units whose
 strip counts span several K2 blocks."""
@@ -41,7 +41,7 @@ def _parse(buf, off, cap, S, dtype):
     return recs, cnt
 
 
-@pytest.mark.parametrize("seed,depth", [(0, 2), (1, 2), (2, 3), (3, 3)])
+@pytest.mark.parametrize("seed,depth", [(0, 2), (1, 2), (2, 3), (3, 3), (4, 5)])
 def test_async_matches_blocking(gpu_lib, seed, depth):
     capi = gpu_lib
     rng = np.random.default_rng(seed)
@@ -91,7 +91,7 @@ def test_async_matches_blocking(gpu_lib, seed, depth):
 
 def test_async_host_delivery_and_growth(gpu_lib):
     """host delivery (no target), first pass grows the record areas while
-    later passes are in flight; a fourth pass in flight is refused"""
+    later passes are in flight; one pass more than UP_MAX_IN_FLIGHT is refused"""
     capi = gpu_lib
     rng = np.random.default_rng(5)
     bw = 5  # narrow windows: most tags are regions of their own
@@ -101,9 +101,8 @@ def test_async_host_delivery_and_growth(gpu_lib):
             u = g.add_unit(L)
             pos, cnt = random_unit(rng, L, bw, n_bg=L // 25)
             g.scatter(u, 0, 0, pos, cnt[:, 0])
-        g.run_async()
-        g.run_async()
-        g.run_async()
+        for _ in range(capi.MAX_IN_FLIGHT):
+            g.run_async()
         with pytest.raises(capi.UpError) as e:
             g.run_async()
         assert e.value.code == UP_E_STATE
@@ -111,6 +110,8 @@ def test_async_host_delivery_and_growth(gpu_lib):
         r1, c1 = g.regions(n1)
         n2 = g.run_wait()
         r2, c2 = g.regions(n2)
+        for _ in range(capi.MAX_IN_FLIGHT - 3):
+            g.run_wait()
         n4 = g.run_wait()
         r4, c4 = g.regions(n4)
         n3 = g.run()

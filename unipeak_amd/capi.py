@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("UNIPEAK_LIB") or os.path.join(_HERE, "lib", "libunipeak_hip.so")
 
 UP_OK = 0
+MAX_IN_FLIGHT = 5  # UP_MAX_IN_FLIGHT (include/unipeak_hip.h)
 
 
 class UpError(RuntimeError):
@@ -231,7 +232,7 @@ class Lib:
         return n.value
 
     def run_async(self):
-        """enqueue one pass (at most two in flight); see up_run_async"""
+        """enqueue one pass (at most MAX_IN_FLIGHT in flight); see up_run_async"""
         _ck(self.L.up_run_async(self.ctx))
 
     def run_wait(self):

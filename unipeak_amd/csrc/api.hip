@@ -89,7 +89,7 @@ struct HostBuf {
     }
 };
 
-constexpr int kSlots = 3;  // passes in flight at most (up_run_async)
+constexpr int kSlots = UP_MAX_IN_FLIGHT;  // passes in flight at most (up_run_async)
 
 }  // namespace
 
@@ -97,7 +97,16 @@ struct up_ctx {
     int dev = 0;
     int ncu = 0;                     // compute units of the device
     int k1a_per_cu = 2;              // K1a workgroups per CU (UNIPEAK_K1A_PER_CU; 0 = resident max)
+    int k1b_per_cu = 0;              // K1b workgroups per CU (UNIPEAK_K1B_PER_CU; 0 = twice resident)
     bool use_graphs = true;          // passes as hipGraphs (UNIPEAK_GRAPHS=0: plain launches)
+    // streams of the passes (with the context stream: four, HIP's default
+    // hardware queues per process, so no two share a queue): every K1a on one
+    // high-priority stream (stream order serialises them; as resources free
+    // up the dispatcher serves it first), the rest of a pass on one of two
+    // chain streams, alternating, so two passes' K1x..K3 may overlap
+    hipStream_t k1a_stream = nullptr;
+    hipStream_t chain[2] = {};
+    uint64_t nlaunch = 0;
     hipStream_t stream = nullptr;
     bool have_params = false;
     up_params p{};
@@ -132,8 +141,8 @@ struct up_ctx {
     // passes in flight (up_run_async); slot = sequence % kSlots.  Each slot
     // owns its device buffers and its stream, so a pass's streaming K1a can
     // run while earlier passes' latency-bound K1b/K2/K3 finish (a pass's K1a
-    // starts once the previous pass's K1a has ended, k1a_end); three slots let
-    // the host enqueue a pass before the one two back has completed
+    // starts once the previous pass's K1a has ended, k1a_end); several slots
+    // let the host enqueue passes while earlier ones are still completing
     struct Pass {
         hipStream_t stream = nullptr;
         hipEvent_t k1a_end = nullptr;   // this pass's K1a finished
@@ -206,10 +215,11 @@ struct up_ctx {
 
 static bool busy(const up_ctx *c) { return c && c->seq_launched != c->seq_done; }
 
-// the context stream and both pass streams idle
+// the context, K1a and chain streams idle
 static void sync_all(up_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
-    for (auto &ps : c->pass) (void)hipStreamSynchronize(ps.stream);
+    (void)hipStreamSynchronize(c->k1a_stream);
+    for (auto st : c->chain) (void)hipStreamSynchronize(st);
 }
 
 #define HIPCHK(x)                                                                   \
@@ -276,13 +286,21 @@ int up_open(int hip_device, up_ctx **out) {
     HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     if (const char *e = getenv("UNIPEAK_K1A_PER_CU")) c->k1a_per_cu = atoi(e);
     if (const char *e = getenv("UNIPEAK_GRAPHS")) c->use_graphs = e[0] != '0';
+    if (const char *e = getenv("UNIPEAK_K1B_PER_CU")) c->k1b_per_cu = atoi(e);
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    {
+        int least = 0, greatest = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        const char *e = getenv("UNIPEAK_K1A_PRIO");  // A/B: 0 = normal priority
+        HIPCHK(hipStreamCreateWithPriority(&c->k1a_stream, hipStreamNonBlocking,
+                                           (e && e[0] == '0') ? least : greatest));
+        for (auto &st : c->chain) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    }
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     for (auto &ps : c->pass) {
         for (auto &e : ps.ev) HIPCHK(hipEventCreate(&e));
         HIPCHK(hipEventCreateWithFlags(&ps.done, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ps.k1a_end, hipEventDisableTiming));
-        HIPCHK(hipStreamCreateWithFlags(&ps.stream, hipStreamNonBlocking));
     }
     HIPCHK(hipEventCreateWithFlags(&c->host_work, hipEventDisableTiming));
     for (auto &e : c->scat_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -307,7 +325,7 @@ void up_close(up_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->stream);
-    for (auto &ps : c->pass) (void)hipStreamSynchronize(ps.stream);
+    sync_all(c);
     free_units(c);
     drop_target(c);
     for (void *h : c->host_regs) (void)hipHostUnregister(h);
@@ -325,8 +343,9 @@ void up_close(up_ctx *c) {
         (void)hipEventDestroy(c->pass[k].k1a_end);
         for (auto &g : c->pass[k].graphs) (void)hipGraphExecDestroy(g.second);
         c->pass[k].release();
-        (void)hipStreamDestroy(c->pass[k].stream);
     }
+    (void)hipStreamDestroy(c->k1a_stream);
+    for (auto st : c->chain) (void)hipStreamDestroy(st);
     (void)hipEventDestroy(c->host_work);
     for (auto &e : c->scat_ev) (void)hipEventSynchronize(e);
     c->hp_scat[0].release(); c->hp_scat[1].release();
@@ -709,13 +728,20 @@ static int sync_units(up_ctx *c) {
             if (u.d_ovf_off) (void)hipFree(u.d_ovf_off);
             u.d_ovf = nullptr;
             u.d_ovf_off = nullptr;
+            // entries sorted by (track, position), indexed per kOvfBlk positions
             std::vector<uint64_t> e;
-            std::vector<uint32_t> off(u.ovf.size() + 1, 0);
+            const uint32_t nb = ovf_nblk(u.len);
+            std::vector<uint32_t> off(u.ovf.size() * (size_t)(nb + 1), 0);
             for (size_t t = 0; t < u.ovf.size(); ++t) {
-                off[t] = (uint32_t)e.size();
-                for (const auto &kv : u.ovf[t]) e.push_back(((uint64_t)kv.first << 32) | kv.second);
+                uint32_t *o = off.data() + t * (size_t)(nb + 1);
+                uint32_t b = 0;
+                for (const auto &kv : u.ovf[t]) {
+                    const uint32_t kb = (uint32_t)((kv.first - 1) >> kOvfBlkShift);  // positions are 1-based
+                    while (b <= kb) o[b++] = (uint32_t)e.size();
+                    e.push_back(((uint64_t)kv.first << 32) | kv.second);
+                }
+                while (b <= nb) o[b++] = (uint32_t)e.size();
             }
-            off[u.ovf.size()] = (uint32_t)e.size();
             if (!e.empty()) {
                 HIPCHK(hipMalloc(&u.d_ovf, e.size() * sizeof(uint64_t)));
                 HIPCHK(hipMalloc(&u.d_ovf_off, off.size() * sizeof(uint32_t)));
@@ -802,6 +828,7 @@ static void launch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32_t
         // a workgroup that retires early hands its slot to one whose waves
         // start at later (cheaper, single-block) items
         blocks *= 2;
+        if (c->k1b_per_cu > 0) blocks = (uint32_t)c->k1b_per_cu * (uint32_t)(c->ncu > 0 ? c->ncu : 256);
     } else {
         if (MODE == kModeScreen) {
             // K1a leaves room on every CU for the previous pass's K1b/K3
@@ -1245,21 +1272,23 @@ static int launch_pass(up_ctx *c, int slot) {
     // writes), and its K1a follows the K1a of the previous pass if that one
     // is in flight: one streaming K1a at a time, earlier passes' K1b/K2/K3
     // beside it
+    // (stream order serialises the K1a's; a slot is reused only after the
+    // host saw its previous pass done)
+    hipStream_t s1 = c->k1a_stream;
+    ps.stream = c->chain[c->nlaunch++ & 1];
     HIPCHK(hipEventRecord(c->host_work, c->stream));
-    HIPCHK(hipStreamWaitEvent(ps.stream, c->host_work, 0));
-    if (c->seq_launched > c->seq_done)
-        HIPCHK(hipStreamWaitEvent(ps.stream, c->pass[(slot + kSlots - 1) % kSlots].k1a_end, 0));
+    HIPCHK(hipStreamWaitEvent(s1, c->host_work, 0));
     if (!ps.counters_armed) {  // K2b re-arms them at the end of every pass
-        HIPCHK(hipMemsetAsync(ps.d_ovf_count.p, 0, sizeof(uint32_t), ps.stream));
-        HIPCHK(hipMemsetAsync(ps.d_xcount.p, 0, 2 * sizeof(uint32_t), ps.stream));
+        HIPCHK(hipMemsetAsync(ps.d_ovf_count.p, 0, sizeof(uint32_t), s1));
+        HIPCHK(hipMemsetAsync(ps.d_xcount.p, 0, 2 * sizeof(uint32_t), s1));
     }
     ScanParams SP = scan_params(c, ps);
     bool graph = c->use_graphs;
-#ifdef UPK_DEBUG_COUNTS
+#if defined(UPK_DEBUG_COUNTS) || defined(UPK_DEBUG_TIMES)
     static const bool dbg = getenv("UNIPEAK_DEBUG_COUNTS") != nullptr;
     if (dbg) {
         HIPCHK(c->d_dbg.ensure(32));
-        HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 32 * sizeof(unsigned long long), ps.stream));
+        HIPCHK(hipMemsetAsync(c->d_dbg.p, 0, 32 * sizeof(unsigned long long), s1));
         SP.dbg = c->d_dbg.p;
         graph = false;
     }
@@ -1286,12 +1315,13 @@ static int launch_pass(up_ctx *c, int slot) {
     }
     ps.counters_armed = true;  // K2b re-arms them
     const int tl = ps.tl;
-    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[0], ps.stream));
+    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[0], s1));
     c->k1a_waves = 0;
-    dispatch_scan<false, kModeScreen>(c, ps.stream, SP, 0, ns);   // K1a: stream + screen
+    dispatch_scan<false, kModeScreen>(c, s1, SP, 0, ns);   // K1a: stream + screen
     HIPCHK(hipGetLastError());
-    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[1], ps.stream));
-    HIPCHK(hipEventRecord(ps.k1a_end, ps.stream));
+    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[1], s1));
+    HIPCHK(hipEventRecord(ps.k1a_end, s1));
+    HIPCHK(hipStreamWaitEvent(ps.stream, ps.k1a_end, 0));
     const uint32_t kw = c->k1a_waves, kx = c->k1a_xcap;
     if (!graph || tl >= 2) {
         if (int r = enqueue_rest(c, slot, SP, P, cap, kw, kx, tl >= 2)) return r;
@@ -1406,12 +1436,16 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
         if (ovf > ps.ovf_cap) { c->ovf_cap = std::max<uint32_t>(c->ovf_cap, (uint32_t)(ovf + ovf / 2 + 64)); again = true; }
         if (nreg > ps.cap) { c->reg_cap = std::max<uint64_t>(c->reg_cap, nreg + nreg / 4 + 1024); again = true; }
         if (ps.target && nreg > ps.target_cap) return fail(UP_E_NOMEM);  // caller's buffer too small
-#ifdef UPK_DEBUG_COUNTS
+#if defined(UPK_DEBUG_COUNTS) || defined(UPK_DEBUG_TIMES)
         if (getenv("UNIPEAK_DEBUG_COUNTS")) {
             unsigned long long h[32];
             HIPCHK(hipMemcpy(h, c->d_dbg.p, sizeof h, hipMemcpyDeviceToHost));
             fprintf(stderr, "unipeak_hip: K1 strips %u exact blocks %llu live words %llu hits %llu "
-                            "cycles load %llu scatter %llu\n", c->nstrips, h[0], h[1], h[2], h[3], h[4]);
+                            "cycles load %llu scatter %llu; words with a flag %llu, flagged positions %llu, "
+                            "words reaching thr/2 %llu\n",
+                    c->nstrips, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+            fprintf(stderr, "unipeak_hip: K1b clocks: item %llu load %llu scatter %llu flags %llu items %llu "
+                            "max wave %llu waves %llu\n", h[16], h[17], h[18], h[19], h[20], h[21], h[22]);
             fprintf(stderr, "unipeak_hip: K1b items by exact blocks:");
             for (int k = 1; k <= 16; ++k) fprintf(stderr, " %d:%llu", k, h[8 + k]);
             fprintf(stderr, "\n");

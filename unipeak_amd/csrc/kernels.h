@@ -39,6 +39,11 @@ constexpr int kMaxK1aWaves = 16384;     // K1a grid cap (stash regions)
 constexpr int kModeFused = 0, kModeScreen = 1, kModeExact = 2;  // K1 variants
 constexpr uint32_t kBig = 1u << 22; // screen value of a chunk holding a nibble >= 8
 
+// overflow entries are indexed per block of kOvfBlk positions, so a lookup
+// searches one block's entries instead of the whole track's
+constexpr uint32_t kOvfBlkShift = 10, kOvfBlk = 1u << kOvfBlkShift;
+__host__ __device__ inline uint32_t ovf_nblk(uint32_t len) { return (len + kOvfBlk - 1) >> kOvfBlkShift; }
+
 struct UnitDesc {
     uint64_t base;      // device address of track (0, 0)
     uint64_t stride;    // bytes per track (multiple of 256)
@@ -47,7 +52,9 @@ struct UnitDesc {
     uint32_t nstrips;   // strips covering [1, len + bw]
     int32_t nstrands;   // 1 or 2
     uint64_t ovf;       // overflow entries (uint64 pos << 32 | count) or 0
-    uint64_t ovf_off;   // uint32[ntracks + 1] offsets into ovf, or 0
+    uint64_t ovf_off;   // uint32[ntracks][nblk + 1], nblk = ceil(len / kOvfBlk): index of
+                        // the track's first entry at or after block b's first position
+                        // (b = nblk: the track's end), or 0
 };
 
 // packed per-strip summary written by the scan kernel (uint64):
@@ -93,7 +100,7 @@ struct ScanParams {
                             // inside the strip) and of the run open at its last position
                             // ([2..3], from its start or the strip's first position)
     uint32_t ovf_cap;
-#ifdef UPK_DEBUG_COUNTS
+#if defined(UPK_DEBUG_COUNTS) || defined(UPK_DEBUG_TIMES)
     unsigned long long *dbg;  // counters: exact blocks, live words
 #endif
     double *prof_f, *prof_r;  // optional dense profile of one unit's positions

@@ -94,18 +94,40 @@ __device__ __forceinline__ uint32_t nsum8(uint32_t x, uint32_t acc) {
     return __builtin_amdgcn_udot8(x, 0x11111111u, acc, false);
 }
 
-// count >= 255: binary search of the track's overflow entries
-__device__ __noinline__ uint32_t ovf_lookup(const UnitDesc &U, uint32_t track, uint32_t pos) {
-    if (!U.ovf) return kEsc;
-    const uint32_t *off = (const uint32_t *)U.ovf_off;
+// escaped count (>= 15): binary search of the entries of the position's
+// block (UnitDesc::ovf_off indexes them per kOvfBlk positions)
+// (inline: a call needs a stack frame, i.e. scratch, in every kernel using it)
+__device__ __forceinline__ uint32_t ovf_lookup(const UnitDesc &U, uint32_t track, uint32_t pos) {
+    if (!U.ovf || pos - 1u >= U.len) return kEsc;
+    const uint32_t *off = (const uint32_t *)U.ovf_off + (size_t)track * (ovf_nblk(U.len) + 1) +
+                          ((pos - 1u) >> kOvfBlkShift);
     const uint64_t *e = (const uint64_t *)U.ovf;
-    uint32_t lo = off[track], hi = off[track + 1];
+    uint32_t lo = off[0], hi = off[1];
+    const uint32_t end = hi;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         const uint32_t p = (uint32_t)(e[mid] >> 32);
         if (p < pos) lo = mid + 1; else hi = mid;
     }
-    return (lo < off[track + 1] && (uint32_t)(e[lo] >> 32) == pos) ? (uint32_t)e[lo] : kEsc;
+    return (lo < end && (uint32_t)(e[lo] >> 32) == pos) ? (uint32_t)e[lo] : kEsc;
+}
+
+// escapes of N words (lane's position x0 + 64w + lane in word w): each lane
+// resolves its own escaped words, one lookup per round, so the rounds are the
+// most escapes any lane holds rather than the words with an escape anywhere
+template <int N>
+__device__ __forceinline__ void resolve_escapes(uint32_t (&c)[N], const UnitDesc &U, uint32_t track, int64_t x0,
+                                                int lane) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int w = 0; w < N; ++w) m |= (c[w] == kEsc ? 1u : 0u) << w;
+    while (m) {
+        const int w = __builtin_ctz(m);
+        m &= m - 1;
+        const uint32_t v = ovf_lookup(U, track, (uint32_t)(x0 + 64 * w + lane));
+#pragma unroll
+        for (int q = 0; q < N; ++q) c[q] = q == w ? v : c[q];
+    }
 }
 
 // exact count of (strand, sample) at position p (1-based)
@@ -133,10 +155,7 @@ __device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], const UnitDesc &
         for (int w = 0; w < N; ++w) c[w] = t[32 * w];
 #pragma unroll
         for (int w = 0; w < N; ++w) c[w] = (c[w] >> sh) & 15u;
-#pragma unroll
-        for (int w = 0; w < N; ++w)
-            if (c[w] == kEsc)
-                c[w] = ovf_lookup(U, (uint32_t)(strand * S + nc[k]), (uint32_t)(x0 + 64 * w + lane));
+        resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[k]), x0, lane);
     };
     if constexpr (POOL == 0) {
         fetch(0);
@@ -238,10 +257,7 @@ __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const Uni
         const uint32_t sh = 4 * (uint32_t)(lane & 1);
 #pragma unroll
         for (int w = 0; w < N; ++w) c[w] = ((uint32_t)stage[32 * w + (lane >> 1)] >> sh) & 15u;
-#pragma unroll
-        for (int w = 0; w < N; ++w)
-            if (c[w] == kEsc)
-                c[w] = ovf_lookup(U, (uint32_t)(strand * S + nc[k]), (uint32_t)(x0 + 64 * w + lane));
+        resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[k]), x0, lane);
     };
     if constexpr (POOL == 0) {
         fetch(0);
@@ -441,9 +457,13 @@ __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], 
 #pragma unroll
     for (int h = 0; h < kHB; ++h) base[h] = lane + bw - b[h];
 #pragma unroll
-    for (int q = 0; q < NT; ++q)
+    for (int q = 0; q < NT; ++q) {
+#ifdef UPK_EXP_LIVEREADS
+        if (!((live >> (T0 + q - NH)) & 1u)) continue;  // uniform: no reads for a dead word
+#endif
 #pragma unroll
         for (int h = 0; h < kHB; ++h) kv[q][h] = vk[base[h] + 64 * (T0 + q - W)];  // 0 outside
+    }
     WordLoop<0, (NT > 0 ? NT : 0)>::run([&](auto qc) {
         constexpr int q = decltype(qc)::value;
         constexpr int t = T0 + q;
@@ -613,7 +633,15 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         istep = 1;
     }
 #endif
+#ifdef UPK_DEBUG_TIMES
+    // K1b phase clocks of this wave (s_memtime), added up once at the end
+    uint64_t dt_item = 0, dt_load = 0, dt_scat = 0, dt_flag = 0, n_items = 0;
+#endif
     for (uint32_t it = it0; it < it_end; it += istep) {
+#ifdef UPK_DEBUG_TIMES
+        const uint64_t t_it0 = __builtin_amdgcn_s_memtime();
+        ++n_items;
+#endif
         uint32_t strip = it;
         // this lane's failing-chunk bits (chunks 16l..16l+15 = words 4l..4l+3
         // of the strip); the live words of an exact block are gathered from
@@ -812,8 +840,8 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             }
 #endif
             const int64_t x0 = p0 + 64 * (j * SW - NH);  // position of window word 0, lane 0
-#ifdef UPK_DEBUG_COUNTS
-            const uint64_t tq0 = __builtin_readcyclecounter();
+#if defined(UPK_DEBUG_COUNTS) || defined(UPK_DEBUG_TIMES)
+            const uint64_t tq0 = __builtin_amdgcn_s_memtime();
 #endif
             T wf[NWIN], wr[NONDIR ? NWIN : 1];
             uint64_t hf[NWIN], hr[NONDIR ? NWIN : 1];
@@ -825,8 +853,12 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 hf[w] = __ballot(nz(wf[w]));
                 if constexpr (NONDIR) hr[w] = __ballot(nz(wr[w]));
             }
+#ifdef UPK_DEBUG_TIMES
+            const uint64_t tq1 = __builtin_amdgcn_s_memtime();
+            dt_load += tq1 - tq0;
+#endif
 #ifdef UPK_DEBUG_COUNTS
-            const uint64_t tq1 = __builtin_readcyclecounter();
+            const uint64_t tq1 = __builtin_amdgcn_s_memtime();
             if (lane == 0) {
                 uint32_t nh = 0;
                 for (int w = 0; w < NWIN; ++w) nh += __builtin_popcountll(hf[w]);
@@ -873,8 +905,12 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 }
             });
 #ifdef UPK_DEBUG_COUNTS
-            const uint64_t tq2 = __builtin_readcyclecounter();
+            const uint64_t tq2 = __builtin_amdgcn_s_memtime();
             if (lane == 0) atomicAdd(&P.dbg[4], (unsigned long long)(tq2 - tq1));
+#endif
+#ifdef UPK_DEBUG_TIMES
+            const uint64_t tq2 = __builtin_amdgcn_s_memtime();
+            dt_scat += tq2 - tq1;
 #endif
             double sc[SW];
             double mx = -__builtin_inf();
@@ -896,6 +932,22 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 }
             } else {
                 // ---- flags and run boundaries (only blocks touching a run) ----
+#ifdef UPK_DEBUG_COUNTS
+                {
+                    uint32_t fw = 0, fp = 0, hw = 0;
+                    for (int k = 0; k < SW; ++k) {
+                        const uint64_t Fk = __ballot(sc[k] >= P.thr);
+                        fw += Fk != 0;
+                        fp += __builtin_popcountll(Fk);
+                        hw += __ballot(sc[k] >= 0.5 * P.thr) != 0;
+                    }
+                    if (lane == 0) {
+                        atomicAdd(&P.dbg[5], (unsigned long long)fw);
+                        atomicAdd(&P.dbg[6], (unsigned long long)fp);
+                        atomicAdd(&P.dbg[7], (unsigned long long)hw);
+                    }
+                }
+#endif
 #ifdef UPK_EXP_K1B_NOFLAGS  // timing experiment (wrong results)
                 const uint64_t anyflag = 0;
                 prevF = __ballot(mx == 1.2345) & 1;
@@ -971,6 +1023,9 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     __builtin_amdgcn_wave_barrier();  // scs reused by the next block
                 }
             }
+#ifdef UPK_DEBUG_TIMES
+            dt_flag += __builtin_amdgcn_s_memtime() - tq2;
+#endif
         }
         if constexpr (PROF) continue;
         if (prevF >> 63) {  // the run open at the strip's last position: its part here
@@ -987,7 +1042,21 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                               ((uint64_t)(local + 1 == U.nstrips) << 35) |
                               ((uint64_t)(R_.slot != kInline) << 36);
         if (lane == 0) P.strip_info[strip] = info;
+#ifdef UPK_DEBUG_TIMES
+        dt_item += __builtin_amdgcn_s_memtime() - t_it0;
+#endif
     }
+#ifdef UPK_DEBUG_TIMES
+    if (MODE == kModeExact && lane == 0 && P.dbg) {
+        atomicAdd(&P.dbg[16], (unsigned long long)dt_item);
+        atomicAdd(&P.dbg[17], (unsigned long long)dt_load);
+        atomicAdd(&P.dbg[18], (unsigned long long)dt_scat);
+        atomicAdd(&P.dbg[19], (unsigned long long)dt_flag);
+        atomicAdd(&P.dbg[20], (unsigned long long)n_items);
+        atomicMax(&P.dbg[21], (unsigned long long)dt_item);
+        atomicAdd(&P.dbg[22], 1ull);
+    }
+#endif
     if constexpr (MODE == kModeScreen) {
         if (lane == 0) {
             P.xwcount[2 * wave] = xnf;
@@ -1320,19 +1389,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                     r0[w] = (r0[w] >> sh) & 15u;
                     if constexpr (NONDIR) r1[w] = (r1[w] >> sh) & 15u;
                 }
+                resolve_escapes<kStatCache>(r0, U, (uint32_t)P.nc[0], (int64_t)left, lane);
+                if constexpr (NONDIR) resolve_escapes<kStatCache>(r1, U, (uint32_t)(S + P.nc[0]), (int64_t)left, lane);
 #pragma unroll
                 for (int w = 0; w < kStatCache; ++w) {
                     if (w >= nw) break;
                     const int64_t x = (int64_t)left + 64 * w + lane;
                     const bool valid = x <= (int64_t)right;
-                    uint32_t c0 = r0[w];
-                    if (c0 == kEsc) c0 = ovf_lookup(U, (uint32_t)P.nc[0], (uint32_t)x);
-                    uint32_t pc = valid ? c0 : 0u;
-                    if constexpr (NONDIR) {
-                        uint32_t c1 = r1[w];
-                        if (c1 == kEsc) c1 = ovf_lookup(U, (uint32_t)(S + P.nc[0]), (uint32_t)x);
-                        pc += valid ? c1 : 0u;
-                    }
+                    uint32_t pc = valid ? r0[w] : 0u;
+                    if constexpr (NONDIR) pc += valid ? r1[w] : 0u;
                     esum1 += pc;
                     pcache[64 * w + lane] = pc;
                     cnt_acc += pc;
