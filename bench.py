@@ -14,10 +14,11 @@ resident in HBM before timing.  Other BASELINE configs are available with
   hg19mm9-32s  configs[4]  hg19+mm9, 32 samples, -D -k 50 -u 0.3 -y (8 GPUs)
 
 One step = the whole hot path over the genome: RCCL all-reduce of the tag
-totals -> background -> up_run (K1a stream+screen -> K1b exact blocks -> K2
-segmentation -> K3 region statistics + filters, one stream, records written
-straight into pinned host memory) -> (N>1) RCCL gather of the records to
-rank 0 -> records in global unit order.
+totals -> background -> up_run_async (K1a stream+screen on a high-priority
+stream -> K1b exact blocks -> K2 segmentation -> K3 region statistics +
+filters on a chain stream, records written straight into pinned host memory;
+up to five passes in flight) -> rank 0 reads every rank's records from the
+node's shared memory in global unit order.
 
 Multi-GPU: one process per GPU (torchrun); units are LPT-assigned to ranks by
 unipeak_amd/shard.py (strong scaling: the genome is fixed), so there is no
@@ -38,6 +39,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# the library's four streams (context, K1a, two chains) plus torch's and
+# RCCL's: more hardware queues than HIP's default 4, so no stream of a pass
+# shares an in-order queue with a collective (read at HIP initialisation)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 from unipeak_amd import capi, shard  # noqa: E402
 
