@@ -212,25 +212,23 @@ def main():
         tag = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}_{os.environ.get('MASTER_PORT', '0')}"
         nr = shard.NodeRecords(comm, cap, S, capi.REGION_DTYPE.itemsize, tag, nslots=NSLOT)
         g.host_register(*nr.my_range())
+        board = shard.StepBoard(comm, tag) if comm is not None else None
         if rank == 0:
             from concurrent.futures import ThreadPoolExecutor
             pool = ThreadPoolExecutor(1)
     else:
+        board = None
         rbuf = comm.target_buffer(cap, S, capi.REGION_DTYPE.itemsize)
         comm.torch.cuda.synchronize()
         g.set_record_target(rbuf.data_ptr(), cap)
     it = [0]           # steps launched
+    bbase = [0]        # board index of this phase's step 0 (the board never rewinds)
     timed = [False]    # inside the timed region
     # timed passes with HIP events around K1a (the roofline sample): every
     # pass -- consecutive passes overlap and alternate between a K1a that runs
     # beside one earlier pass's kernels and one beside two, so a sparser
     # sample would see one phase only
     K1A_EVERY = int(os.environ.get("UNIPEAK_K1A_EVERY", "1"))
-    # background all-reduces in flight, started AR_AHEAD steps ahead: with
-    # DEPTH passes queued on the device an all-reduce started one step ahead
-    # still waited behind them (0.37 ms of host wait per step at world 1)
-    AR_AHEAD = DEPTH + 1
-    ar = []
     reads = []         # rank 0: (step, future) of record reads in flight
     done_times = []    # per completed pass: library timings
 
@@ -245,10 +243,14 @@ def main():
     read_s = [0.0, 0]  # host time of the rank-0 record reads (helper thread)
 
     def timed_read(j):
+        if board is not None:  # every rank has completed pass j
+            board.wait_done(bbase[0] + j)
         t = time.perf_counter()
         r = consume(nr.read(capi.REGION_DTYPE, j))
         read_s[0] += time.perf_counter() - t
         read_s[1] += 1
+        if board is not None:
+            board.post_read(bbase[0] + j)
         return r
 
     def read_step(j):
@@ -261,6 +263,8 @@ def main():
             while it[0] > len(done_times):  # parameters change only between passes
                 g.run_wait()
                 done_times.append(g.timings())
+                if board is not None:
+                    board.post_done(bbase[0] + len(done_times) - 1)
             g.set_params(args.bw, S, background, region_thr=25.0, kurt_thr=W["kurt"],
                          corr_thr=W["corr"], hit_thr=10.0 * s_nc, nondir=nondir, control=control,
                          want_corr=W["want_corr"])
@@ -284,23 +288,23 @@ def main():
             phase["launch"] += t2 - t1
             phase["gather_merge"] += t3 - t2
             return
-        # slot i % NSLOT held step i-NSLOT: its read must be over before any
-        # rank passes this step's collective and launches into it
+        # slot i % NSLOT held step i-NSLOT: rank 0's read of it must be over
+        # before this rank launches a pass into it
         while reads and reads[0][0] <= i - NSLOT:
             reads.pop(0)[1].result()
-        if comm is not None:
-            # this step's all-reduce was started one step ahead (RCCL gets the
-            # device between the previous pass's kernels); start the next one
-            while len(ar) < AR_AHEAD:
-                ar.append(comm.global_tags_start(local_tags))
-            tags = comm.global_tags_finish(ar.pop(0))
-            ar.append(comm.global_tags_start(local_tags))
+        if board is not None:
+            b = bbase[0] + i
+            if i >= NSLOT:
+                board.wait_read(b - NSLOT)
+            # the background's all-reduce of this step through the board
+            board.post_tags(b, local_tags)
+            tags = board.tags(b)
         else:
             tags = local_tags
         set_background(tags)
         t1 = time.perf_counter()
-        # every rank has completed pass i-DEPTH (it waited for it before
-        # entering this collective): rank 0 reads it while later passes run
+        # rank 0 reads pass i-DEPTH while later passes run (its helper thread
+        # first waits until every rank has completed that pass)
         if rank == 0 and i >= DEPTH:
             reads.append((i - DEPTH, read_step(i - DEPTH)))
         g.set_record_target(nr.my_slot_address(i), cap)
@@ -312,6 +316,8 @@ def main():
         if i >= DEPTH - 1:
             g.run_wait()
             done_times.append(g.timings())
+            if board is not None:
+                board.post_done(bbase[0] + len(done_times) - 1)
         t3 = time.perf_counter()
         phase["allreduce"] += t1 - t0
         phase["launch"] += t2 - t1
@@ -323,8 +329,8 @@ def main():
         while it[0] > len(done_times):
             g.run_wait()
             done_times.append(g.timings())
-        while ar:  # all-reduces started for steps that will not run
-            comm.global_tags_finish(ar.pop(0))
+            if board is not None:
+                board.post_done(bbase[0] + len(done_times) - 1)
         if not pipelined:
             return None
         if comm is not None:
@@ -338,6 +344,8 @@ def main():
                 res = f.result()
             for j in range(max(0, last - DEPTH + 1), last + 1):  # steps not read during the loop
                 res = consume(nr.read(capi.REGION_DTYPE, j))
+                if board is not None:
+                    board.post_read(bbase[0] + j)
         return res
 
     def barrier():
@@ -358,6 +366,7 @@ def main():
     for k in phase:
         phase[k] = 0.0
     done_times.clear()
+    bbase[0] += it[0]
     it[0] = 0
     barrier()
     if comm is not None:
@@ -463,6 +472,8 @@ def main():
         comm.dist.barrier()
         if nr is not None:
             nr.close()
+        if board is not None:
+            board.close()
         comm.dist.destroy_process_group()
 
 

@@ -293,27 +293,42 @@ def test_node_records_world2(tmp_path):
     assert not os.path.exists(f"/dev/shm/unipeak_test_{port}")
 
 
-def _async_tags_worker(rank, world, port, out_dir):
+def _board_worker(rank, world, port, out_dir):
+    import time
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = shard.Comm(dist, rank, world, "cpu")
-    # bench.py's order: the all-reduce of step i+1 is started before step i's
-    # result is used, every rank issuing the same sequence
-    pending = comm.global_tags_start(10 * (rank + 1))
-    got = []
-    for step in range(4):
-        v = comm.global_tags_finish(pending)
-        pending = comm.global_tags_start(10 * (rank + 1) + step + 1)
-        got.append(v)
-    got.append(comm.global_tags_finish(pending))
-    np.save(os.path.join(out_dir, f"t{rank}.npy"), np.array(got))
-    dist.destroy_process_group()
+    board = shard.StepBoard(comm, f"test_{port}", timeout_s=30.0)
+    try:
+        got = []
+        for step in range(shard.StepBoard.RING + 6):  # wraps the tag ring
+            if rank == 1 and step % 7 == 0:
+                time.sleep(0.01)  # a slow rank: the others wait on the board
+            board.post_tags(step, 10 * (rank + 1) + step)
+            got.append(board.tags(step))
+            board.post_done(step)
+            if rank == 0:
+                board.wait_done(step)  # every rank completed this step's pass
+                board.post_read(step)
+            else:
+                board.wait_read(step)
+        np.save(os.path.join(out_dir, f"b{rank}.npy"), np.array(got))
+        dist.barrier()
+    finally:
+        board.close()
+        dist.destroy_process_group()
 
 
-def test_gloo_background_allreduce_one_step_ahead(tmp_path):
+def test_step_board_world3(tmp_path):
+    """the pipelined bench's per-step exchange: tag totals summed over the
+    ranks (the background's all-reduce) and the pass/read ordering flags"""
     import torch.multiprocessing as mp
-    mp.spawn(_async_tags_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    for r in range(2):
-        got = np.load(tmp_path / f"t{r}.npy")
-        assert got.tolist() == [30, 32, 34, 36, 38]
+    port = _free_port()
+    world = 3
+    mp.spawn(_board_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    n = shard.StepBoard.RING + 6
+    want = [sum(10 * (r + 1) + s for r in range(world)) for s in range(n)]
+    for r in range(world):
+        assert np.load(tmp_path / f"b{r}.npy").tolist() == want
+    assert not os.path.exists(f"/dev/shm/unipeak_board_test_{port}")

@@ -12,7 +12,10 @@ So the layout is:
 * ``Comm.gather_records()`` -- one max-count all-reduce + one gather of the
   fixed-size records to rank 0 (RCCL when the ranks own GPUs);
 * ``merge()``     -- rank 0 concatenates the per-rank, unit-major record
-  blocks in global unit order (a slice per unit, no sort).
+  blocks in global unit order (a slice per unit, no sort);
+* one node, pipelined steps: ``NodeRecords`` (every rank's K3 writes its
+  records into node-shared pinned host memory) and ``StepBoard`` (the
+  per-step tag totals and the pass/read ordering as host flags).
 
 Units of one rank are run in ascending global order, so each rank's records
 are already unit-major; the CLI engine (host/engine.cpp) applies the same
@@ -20,6 +23,9 @@ plan inside one process over several devices and then restores the
 reference's emission order from the replayed event clock.
 """
 from __future__ import annotations
+
+import os
+import time
 
 import numpy as np
 
@@ -169,46 +175,6 @@ class Comm:
             self.dist.all_reduce(self._tags)
             v = int(self._tags.item())
         return v
-
-    def global_tags_start(self, local_tags: int):
-        """Start the same all-reduce without waiting for it (steps ahead):
-        its RCCL kernel runs whenever the device has room, on a high-priority
-        side stream, and global_tags_finish() collects it."""
-        torch = self.torch
-        if self.device == "cpu":
-            t = torch.tensor([int(local_tags)], dtype=torch.int64)
-            return (self.dist.all_reduce(t, async_op=True), t)
-        if getattr(self, "_ring", None) is None:
-            # high priority: its kernels go ahead of queued pass kernels
-            self._side = torch.cuda.Stream(device=self.device, priority=-1)
-            self._ring = [(torch.zeros(1, dtype=torch.int64, pin_memory=True),
-                           torch.zeros(1, dtype=torch.int64, device=self.device),
-                           torch.zeros(1, dtype=torch.int64, pin_memory=True),
-                           torch.cuda.Event()) for _ in range(8)]
-            self._ri = 0
-        h_in, d, h_out, ev = self._ring[self._ri]
-        self._ri = (self._ri + 1) % len(self._ring)
-        h_in[0] = int(local_tags)
-        with torch.cuda.stream(self._side):
-            d.copy_(h_in, non_blocking=True)
-            self.dist.all_reduce(d, async_op=True).wait()  # the side stream waits, the host does not
-            # the sum lands in pinned host memory by an async copy; finish
-            # waits for its event only (.item() on the busy device waited
-            # ~0.35 ms per step behind queued pass kernels)
-            h_out.copy_(d, non_blocking=True)
-            ev.record(self._side)
-        return ("gpu", ev, h_out)
-
-    def global_tags_finish(self, handle) -> int:
-        """The all-reduced tag total of a global_tags_start() handle (the
-        ring holds 8 handles: at most 8 may be in flight)."""
-        if handle[0] == "gpu":
-            _, ev, h = handle
-            ev.synchronize()
-            return int(h[0])
-        work, t = handle
-        work.wait()
-        return int(t.item())
 
     def max_over_ranks(self, x: float) -> float:
         t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=self.device)
@@ -389,3 +355,89 @@ class NodeRecords:
                 pass
         if self.owner:
             self.shm.unlink()
+
+
+class StepBoard:
+    """Node-shared host board that orders the pipelined steps of the ranks of
+    one node without a collective call per step: each step's tag totals (the
+    background's all-reduce, regions.cpp:205-213: every rank posts its total
+    and sums the board), each rank's completed passes, and rank 0's finished
+    record reads (a rank reuses a NodeRecords slot only after rank 0 has read
+    it).  Host flags only: a value is written before its stamp, and x86 keeps
+    stores (and loads) in program order, so a reader that sees the stamp sees
+    the value."""
+
+    RING = 64  # tag entries per rank (ranks stay within one step of each other)
+    ROW = 8 + 2 * RING  # int64 per rank: done, read, pad, tags[RING], stamps[RING]
+
+    def __init__(self, comm, tag, timeout_s=120.0):
+        from multiprocessing import resource_tracker, shared_memory
+        self.rank, self.world = comm.rank, comm.world
+        self.timeout_s = timeout_s
+        name = f"unipeak_board_{tag}"
+        size = self.world * self.ROW * 8
+        self.owner = comm.rank == 0
+        if self.owner:
+            try:  # a stale segment of an earlier crashed run
+                old = shared_memory.SharedMemory(name=name)
+                old.close()
+                old.unlink()
+            except FileNotFoundError:
+                pass
+            self.shm = shared_memory.SharedMemory(name=name, create=True, size=size)
+            np.frombuffer(self.shm.buf, np.int64)[:] = 0
+        comm.dist.barrier()
+        if not self.owner:
+            self.shm = shared_memory.SharedMemory(name=name)
+            resource_tracker.unregister(self.shm._name, "shared_memory")
+        self.b = np.frombuffer(self.shm.buf, np.int64).reshape(self.world, self.ROW)
+        comm.dist.barrier()  # every rank attached before anyone posts
+
+    def _spin(self, ready, what):
+        t0 = time.perf_counter()
+        n = 0
+        while not ready():
+            n += 1
+            if n > 64:
+                os.sched_yield()
+                if time.perf_counter() - t0 > self.timeout_s:
+                    raise RuntimeError(f"step board: timed out waiting for {what}")
+
+    def post_tags(self, step: int, value: int):
+        k = step % self.RING
+        self.b[self.rank, 8 + k] = int(value)
+        self.b[self.rank, 8 + self.RING + k] = step + 1
+
+    def tags(self, step: int) -> int:
+        """sum of every rank's posted total of `step` (waits for all)"""
+        k = step % self.RING
+        st = self.b[:, 8 + self.RING + k]
+        self._spin(lambda: bool((st == step + 1).all()), f"the tag totals of step {step}")
+        return int(self.b[:, 8 + k].sum())
+
+    def post_done(self, step: int):
+        """this rank has completed passes 0..step"""
+        self.b[self.rank, 0] = step + 1
+
+    def wait_done(self, step: int):
+        done = self.b[:, 0]
+        self._spin(lambda: bool((done > step).all()), f"every rank's pass {step}")
+
+    def post_read(self, step: int):
+        """rank 0 has read every rank's records of steps 0..step"""
+        self.b[0, 1] = step + 1
+
+    def wait_read(self, step: int):
+        self._spin(lambda: self.b[0, 1] > step, f"rank 0's read of step {step}")
+
+    def close(self):
+        self.b = None
+        try:
+            self.shm.close()
+        except BufferError:
+            pass
+        if self.owner:
+            try:
+                self.shm.unlink()
+            except FileNotFoundError:
+                pass
