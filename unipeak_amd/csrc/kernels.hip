@@ -1311,8 +1311,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
     double2 *cslab = (NONDIR && P.want_corr && P.corr_scratch)
                          ? (double2 *)P.corr_scratch + (uint64_t)wave * P.corr_cap : nullptr;
 
+    // K1 saw the whole run: its peak is known and, unless the strand
+    // correlation is wanted, no score is needed here -- only the counts
+    const bool known = P.peak_pos != nullptr && !(NONDIR && P.want_corr);
+    // Region descriptors (start, end, unit, peak position, peak value) come
+    // one region ahead: lanes 0..5 read the next region's six words with one
+    // vector load at the top of an iteration, and with one pooled directional
+    // sample the next region's count bytes are fetched before this region's
+    // kurtosis pass, so the loads of region i+1 overlap the work of region i
+    // (a wave holds ~10 regions; their dependent load chains were the cost).
+    constexpr bool kPrefetch = POOL == 0 && !NONDIR;
+    auto desc_load = [&](uint64_t r) -> uint32_t {
+        if (lane >= (known ? 6 : 3)) return 0u;
+        const uint32_t *src = lane == 0   ? P.starts + r
+                              : lane == 1 ? P.ends + r
+                              : lane == 2 ? P.reg_unit + r
+                              : lane == 3 ? P.peak_pos + r
+                                          : (const uint32_t *)(P.peak_val + r) + (lane - 4);
+        return *src;
+    };
+    uint32_t dsc = wave < nreg ? desc_load(wave) : 0u;
+    bool pre_ok = false;  // praw holds the count bytes of region ri
+    uint32_t praw[kPrefetch ? kStatCache : 1];
     for (uint64_t ri = wave; ri < nreg; ri += nwaves) {
-        const uint32_t left = P.starts[ri], right = P.ends[ri], u = P.reg_unit[ri];
+        const uint32_t left = rl_u(dsc, 0), right = rl_u(dsc, 1), u = rl_u(dsc, 2);
+        const uint64_t rn = ri + nwaves;
+        const uint32_t dsc_n = rn < nreg ? desc_load(rn) : 0u;
         const UnitDesc U = P.units[u];
         uint32_t esum[4] = {0, 0, 0, 0};  // exptSums[s] lives in lane s%64, slot s/64
         uint32_t esum1 = 0;               // S == 1: lane-local partial of exptSums[0]
@@ -1332,14 +1356,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
 #pragma unroll
             for (int w = 0; w < NWT; ++w) dst[w] = ((uint32_t)t[32 * w] >> sh) & 15u;
         };
-        // K1 saw the whole run: its peak is known and, unless the strand
-        // correlation is wanted, no score is needed here -- only the counts
-        const bool known = P.peak_pos != nullptr && !(NONDIR && P.want_corr);
         uint32_t kpos = 0;
         double kval = 0.0;
         if (known) {
-            kpos = P.peak_pos[ri];
-            kval = P.peak_val[ri];
+            kpos = rl_u(dsc, 3);
+            kval = __longlong_as_double((long long)(((uint64_t)rl_u(dsc, 5) << 32) | rl_u(dsc, 4)));
 #ifdef UPK_EXP_NOCOMBINE
             if (false) {
 #else
@@ -1377,8 +1398,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 const uint32_t sh = 4 * (uint32_t)(n0 & 1);
                 gu8 *t0 = track_u8(U, S, 0, P.nc[0]) + (n0 >> 1);
                 uint32_t r0[kStatCache], r1[NONDIR ? kStatCache : 1];
+                if (kPrefetch && pre_ok) {
 #pragma unroll
-                for (int w = 0; w < kStatCache; ++w) r0[w] = w < nw ? t0[32 * w] : 0u;
+                    for (int w = 0; w < kStatCache; ++w) r0[w] = praw[kPrefetch ? w : 0];
+                } else {
+#pragma unroll
+                    for (int w = 0; w < kStatCache; ++w) r0[w] = w < nw ? t0[32 * w] : 0u;
+                }
                 if constexpr (NONDIR) {
                     gu8 *t1 = track_u8(U, S, 1, P.nc[0]) + (n0 >> 1);
 #pragma unroll
@@ -1556,6 +1582,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
         const uint32_t count = wave_sum_u32(cnt_acc);
         const uint32_t psum = wave_sum_u32(sum_acc);
 
+        // next region's count bytes (its descriptor arrived during pass 1)
+        pre_ok = false;
+        if constexpr (kPrefetch) {
+            if (known && S == 1 && rn < nreg) {
+                const uint32_t ln = rl_u(dsc_n, 0), rgn = rl_u(dsc_n, 1);
+                const int nwn = (int)((rgn - ln) / 64u) + 1;
+                if (nwn <= kStatCache) {
+                    const UnitDesc Un = P.units[rl_u(dsc_n, 2)];
+                    gu8 *tn = track_u8(Un, S, 0, P.nc[0]) + ((kPadPos + (int64_t)ln - 1 + lane) >> 1);
+#pragma unroll
+                    for (int w = 0; w < kStatCache; ++w) praw[w] = w < nwn ? tn[32 * w] : 0u;
+                    pre_ok = true;
+                }
+            }
+        }
         // ---- pass 2: kurtosis (data.cpp:164-182; powi semantics) ----
         const double x_bar = (double)psum / (double)count;
         double sum2 = 0.0, sum4 = 0.0;
@@ -1710,6 +1751,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
             }
             ((uint64_t *)P.out)[ri * 7 + lane] = w;
         }
+        dsc = dsc_n;
     }
 }
 
