@@ -405,19 +405,55 @@ __device__ __forceinline__ void rec_end(RecList &R, uint32_t pos, uint32_t pk_po
     ++R.ne;
 }
 
+// Wave reductions through DPP (VALU only; a __shfl_xor step is an LDS
+// bpermute plus its address arithmetic): row_shr 1, 2, 4, 8 leave each
+// 16-lane row's total in its lane 15, row_bcast 15 / 31 carry rows 0-1 and
+// 0-2 into rows 1 and 2-3, lane 63 ends with the wave's total, read back as
+// a wave-uniform value.  The ops are associative and commutative (u32 wrap
+// sums, min, max of non-NaN), so the result equals the butterfly's.  `id` is
+// the identity that lanes without a source keep.  Every lane must be active.
+template <int CTRL, int ROWS, bool ZERO>
+__device__ __forceinline__ uint32_t dpp32(uint32_t id, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, CTRL, ROWS, 0xf, ZERO);
+}
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t v, uint32_t id, Op op) {
+    v = op(v, dpp32<0x111, 0xf, false>(id, v));
+    v = op(v, dpp32<0x112, 0xf, false>(id, v));
+    v = op(v, dpp32<0x114, 0xf, false>(id, v));
+    v = op(v, dpp32<0x118, 0xf, false>(id, v));
+    v = op(v, dpp32<0x142, 0xa, false>(id, v));
+    v = op(v, dpp32<0x143, 0xc, false>(id, v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp64(double id, double v) {
+    const uint64_t a = (uint64_t)__double_as_longlong(id), b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = dpp32<CTRL, ROWS, false>((uint32_t)a, (uint32_t)b);
+    const uint32_t hi = dpp32<CTRL, ROWS, false>((uint32_t)(a >> 32), (uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t w = (uint32_t)__shfl_xor((int)v, o);
-        v = w < v ? w : v;
-    }
-    return v;
+    return wave_reduce_u32(v, 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return b < a ? b : a; });
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    return wave_reduce_u32(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
 }
 
 __device__ __forceinline__ double wave_max_d(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = __builtin_fmax(v, __shfl_xor(v, o));
-    return v;
+    const double ninf = -__builtin_inf();
+    v = __builtin_fmax(v, dpp64<0x111, 0xf>(ninf, v));
+    v = __builtin_fmax(v, dpp64<0x112, 0xf>(ninf, v));
+    v = __builtin_fmax(v, dpp64<0x114, 0xf>(ninf, v));
+    v = __builtin_fmax(v, dpp64<0x118, 0xf>(ninf, v));
+    v = __builtin_fmax(v, dpp64<0x142, 0xa>(ninf, v));
+    v = __builtin_fmax(v, dpp64<0x143, 0xc>(ninf, v));
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 63);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
 // scatter up to kHB hits (window word W, bits b[], pooled counts c[], in
@@ -1266,11 +1302,7 @@ __global__ void __launch_bounds__(256) unit_last_kernel(const UnitDesc *units, u
 // ------------------------------------------------------------------------
 // K3: region statistics, one wave per region (grid-stride).
 // ------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-    return v;
-}
+
 
 // pooled counts of the 2NH+1 words around block start x0 for one strand
 template <int NH, int POOL>
