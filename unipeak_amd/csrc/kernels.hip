@@ -533,8 +533,10 @@ __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], 
 constexpr int kScrIdx = 8 + kBlocks * kWave + 8;
 constexpr int kScrWords = kScrIdx + kScrIdx / 16 + 2;  // even: 8-byte aligned per wave
 __device__ __forceinline__ int scr_at(int i) { return i + (i >> 4); }
-constexpr size_t kScreenLds = kKTab * sizeof(double) + 4 * kScrWords * sizeof(uint32_t);
-constexpr size_t kScanLds = kScreenLds + 4 * kStepWords * kWave * sizeof(double);
+// K1a needs no kernel weights: its chunk-sum areas start at LDS offset 0, so
+// the lane reads of the screen fold into the ds_read2 offset fields
+constexpr size_t kScreenLds = 4 * kScrWords * sizeof(uint32_t);
+constexpr size_t kScanLds = kKTab * sizeof(double) + kScreenLds + 4 * kStepWords * kWave * sizeof(double);
 #ifndef UPK_XFRONT
 #define UPK_XFRONT 2
 #endif
@@ -624,7 +626,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     const int bw = P.bw;
     double *ktab = lds_ + kKPad;
     if constexpr (MODE != kModeScreen) ktab = load_ktab(lds_, P.kern, bw);
-    uint32_t *scr = (uint32_t *)(lds_ + kKTab) + (threadIdx.x >> 6) * kScrWords;
+    uint32_t *scr = (uint32_t *)(MODE == kModeScreen ? lds_ : lds_ + kKTab) + (threadIdx.x >> 6) * kScrWords;
     // this wave's block scores (K1b has no screen area)
     double *scs = (MODE == kModeExact ? lds_ + kKTab : (double *)((uint32_t *)(lds_ + kKTab) + 4 * kScrWords)) +
                   (threadIdx.x >> 6) * (kStepWords * kWave);
