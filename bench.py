@@ -184,6 +184,7 @@ def main():
     copy_gbps = g.hbm_copy_gbps(1 << 30, 5)
 
     phase = {"allreduce": 0.0, "launch": 0.0, "wait": 0.0, "gather_merge": 0.0}
+    sub = {"submit": 0.0, "target": 0.0, "run_async": 0.0}  # parts of "launch"
     # one node (torchrun --nnodes=1): records meet in node-shared host memory
     gather_mode = os.environ.get("UNIPEAK_GATHER") or (
         "shm" if int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world else "rccl")
@@ -307,12 +308,17 @@ def main():
         # first waits until every rank has completed that pass)
         if rank == 0 and i >= DEPTH:
             reads.append((i - DEPTH, read_step(i - DEPTH)))
+        ta = time.perf_counter()
         g.set_record_target(nr.my_slot_address(i), cap)
         if timed[0]:  # K1a events on every K1A_EVERY-th timed pass only (an event pair idles the GPU)
             g.set_timing(1 if i % K1A_EVERY == 0 else 0)
+        tb = time.perf_counter()
         g.run_async()
         it[0] += 1
         t2 = time.perf_counter()
+        sub["submit"] += ta - t1
+        sub["target"] += tb - ta
+        sub["run_async"] += t2 - tb
         if i >= DEPTH - 1:
             g.run_wait()
             done_times.append(g.timings())
@@ -365,6 +371,8 @@ def main():
     timed[0] = True
     for k in phase:
         phase[k] = 0.0
+    for k in sub:
+        sub[k] = 0.0
     done_times.clear()
     bbase[0] += it[0]
     it[0] = 0
@@ -408,7 +416,8 @@ def main():
     if rank == 0:
         print("[bench] per-step phases (ms): " + ", ".join(
             f"{k} {v / args.steps * 1e3:.3f}" for k, v in phase.items()) +
-            f"; record read {read_s[0] / max(read_s[1], 1) * 1e3:.3f} ms x{read_s[1]} (helper thread)",
+            f"; record read {read_s[0] / max(read_s[1], 1) * 1e3:.3f} ms x{read_s[1]} (helper thread)"
+            "; launch = " + ", ".join(f"{k} {v / args.steps * 1e3:.3f}" for k, v in sub.items()),
             file=sys.stderr, flush=True)
         value = genome / dt / 1e9
         if sim_world > 1:  # not a headline line: one rank's shard of an N-GPU plan
