@@ -147,3 +147,38 @@ def test_many_units_many_blocks(gpu_lib, oracle):
         assert np.array_equal(ref_sums, gcnt[m])
         assert ref["peak_score"].tobytes() == regs[m]["peak_score"].tobytes()
 
+
+
+def test_launcher_thread_under_graph_capture(gpu_lib):
+    """bench-shaped: UP_MAX_IN_FLIGHT passes in flight, K1x..K3 captured as
+    graphs (timing level 1) on the library's launcher thread while this
+    thread waits for, times and reads the older passes"""
+    capi = gpu_lib
+    rng = np.random.default_rng(11)
+    bw = 50
+    with capi.Lib(0) as g:
+        g.set_params(bw, 1, 0.003)
+        _load(g, rng, [int(x) for x in rng.integers(300_000, 3_000_000, size=9)], bw)
+        n = g.run()
+        ref, _ = g.regions(n)
+        cap = n + 16
+        depth = capi.MAX_IN_FLIGHT
+        bufs = [_target(cap, 1, capi.REGION_DTYPE.itemsize) for _ in range(2 * depth)]
+        for b, off in bufs:
+            g.host_register(b[off:].ctypes.data, len(b) - off)
+        g.set_timing(1)
+        npass = 60
+        for i in range(npass + depth - 1):
+            if i < npass:
+                b, off = bufs[i % len(bufs)]
+                g.set_record_target(b[off:].ctypes.data, cap)
+                g.run_async()
+            if i >= depth - 1:
+                j = i - depth + 1
+                assert g.run_wait() == n
+                assert g.timings()[0] > 0
+                b, off = bufs[j % len(bufs)]
+                recs, _ = _parse(b, off, cap, 1, capi.REGION_DTYPE)
+                assert recs.tobytes() == ref.tobytes()
+        g.set_record_target(0, 0)
+        g.set_timing(2)

@@ -6,10 +6,13 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/unipeak_hip.h"
@@ -37,6 +40,7 @@ struct Unit {
     uint64_t *d_ovf = nullptr;     // uploaded entries, sorted by (track, pos)
     uint32_t *d_ovf_off = nullptr; // [ntracks + 1]
     bool ovf_dirty = false;
+    uint32_t ovf_max = 0;          // largest escaped count of any track
 };
 
 template <typename T>
@@ -120,6 +124,11 @@ struct up_ctx {
     uint32_t wskip = 0;
     float fw[9] = {};                // fine screen weights per chunk distance
     float fthr = 0.f;
+    // K1b keys (ScanParams::qmode): score = alpha * Q * (1 +- q_delta)
+    bool q_ok = false;               // weights proportional to bw^2 - d^2 within q_delta
+    double q_alpha = 0.0, q_delta = 1.0;
+    uint32_t qno = 0, qyes = 0;
+    uint32_t ovf_max_all = 0;        // largest escaped count of any unit
     DevBuf<uint32_t> d_stage;          // dense uint32 staging for synth / pack
     DevBuf<unsigned long long> d_pack_ovf;
     DevBuf<uint32_t> d_pack_n;
@@ -166,6 +175,14 @@ struct up_ctx {
         uint8_t *target = nullptr;   // record target of this pass (device address) or null
         void *target_hostp = nullptr;// host address of a host target
         uint64_t target_cap = 0;
+        // what the caller set when it enqueued the pass (the launcher thread
+        // launches it later): record target, timing level, K3 grid estimate
+        uint8_t *req_target = nullptr;
+        void *req_target_hostp = nullptr;
+        uint64_t req_target_cap = 0, req_last_nreg = 0;
+        int req_tl = 0;
+        bool lpending = false;       // queued for / being launched by the launcher thread
+        int lrc = 0;                 // its launch result
         uint64_t cap = 0;            // reg_cap at launch
         uint32_t ovf_cap = 0;
         int tl = 0;                  // timing level at launch
@@ -175,6 +192,16 @@ struct up_ctx {
     } pass[kSlots];
     uint64_t seq_launched = 0, seq_done = 0;
     int cur_slot = 0;                // slot of the last completed pass (host records)
+    // Launcher thread: up_run_async hands the pass's HIP calls (K1a launch,
+    // events, the K1x..K3 graph, ~40 us of host time) to it and returns, so
+    // the caller's own per-step work overlaps them (at 8 GPUs a step is
+    // ~0.1 ms and the host side bounds it).  UNIPEAK_LAUNCHER=0: launch on
+    // the caller's thread.
+    std::thread launcher;
+    std::mutex lmu;
+    std::condition_variable lcv;
+    std::deque<int> lq;              // slots to launch, in order
+    bool lbusy = false, lstop = false, use_launcher = true;
     // head-hit (quirk Q1) replay
     hipEvent_t host_work = nullptr;  // marks work on `stream` that a pass must follow
     DevBuf<uint32_t> d_resync, d_emu_n, d_emu_err, d_emu_counts, d_ring_hits, d_reg_hit, d_reg_hits;
@@ -287,6 +314,7 @@ int up_open(int hip_device, up_ctx **out) {
     if (const char *e = getenv("UNIPEAK_K1A_PER_CU")) c->k1a_per_cu = atoi(e);
     if (const char *e = getenv("UNIPEAK_GRAPHS")) c->use_graphs = e[0] != '0';
     if (const char *e = getenv("UNIPEAK_K1B_PER_CU")) c->k1b_per_cu = atoi(e);
+    if (const char *e = getenv("UNIPEAK_LAUNCHER")) c->use_launcher = e[0] != '0';
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     {
         int least = 0, greatest = 0;
@@ -321,8 +349,11 @@ static void free_units(up_ctx *c) {
 
 static void drop_target(up_ctx *c);
 
+static void launcher_stop(up_ctx *c);
+
 void up_close(up_ctx *c) {
     if (!c) return;
+    launcher_stop(c);
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->stream);
     sync_all(c);
@@ -355,6 +386,8 @@ void up_close(up_ctx *c) {
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
+
+static void set_q_params(up_ctx *c);
 
 int up_set_params(up_ctx *c, const up_params *p) {
     if (!c || !p) return UP_E_ARG;
@@ -435,9 +468,60 @@ int up_set_params(up_ctx *c, const up_params *p) {
         // screen off (huge coefficients): every tag within reach goes exact
         c->fthr = (huge || !(wf > 0.0)) ? 0.f : (float)(p->region_thr * (1.0 - 1e-6));
     }
+    set_q_params(c);
     c->have_params = true;
     if (old_bw != p->bw) c->units_dirty = true;
     return UP_OK;
+}
+
+// K1b keys.  Kernel::Kernel (kernel.cpp:12-35) builds w_d = 3(1 - (d/bw)^2)/4
+// times a scale, so the FP64 weight K_d = alpha (bw^2 - d^2) (1 + e_d) with
+// alpha = K_0 / bw^2 and |e_d| <= E, measured here in long double (a few
+// ulp for |d| << bw, up to ~bw/2 ulp next to the window edge where
+// 1 - (d/bw)^2 cancels).  An FP64 score is a sum of <= 2bw+1 non-negative
+// rounded products, added in some order, (+ the f + r add): within
+// (2bw+3) ulp of its real value.  So score = alpha Q (1 +- delta) with
+// delta = 2 (E + (2bw+4) 2^-53) (a factor 2 to spare).  The edge weights
+// K_{+-bw} must be exactly 0 (they are: 1 - 1 = 0).
+static void set_q_params(up_ctx *c) {
+    c->q_ok = false;
+    const int bw = c->p.bw;
+    if (bw < 1 || bw > kMaxBw || (int)c->kern.size() != 2 * bw + 1 || !(c->p.region_thr > 0)) return;
+    const long double b2 = (long double)bw * bw;
+    const double k0 = c->kern[bw];
+    if (!(k0 > 0) || c->kern[0] != 0.0 || c->kern[2 * bw] != 0.0) return;
+    const double alpha = k0 / (double)(bw * bw);
+    long double E = 0;
+    for (int d = -bw + 1; d <= bw - 1; ++d) {
+        const long double ideal = (long double)alpha * (b2 - (long double)d * d);
+        const long double e = fabsl((long double)c->kern[bw + d] / ideal - 1.0L);
+        if (!(e < 1e-9L)) return;  // not this kernel's shape
+        E = e > E ? e : E;
+    }
+    const double delta = 2.0 * ((double)E + (2.0 * bw + 4.0) * 0x1p-53);
+    // decided: Q <= qno -> alpha Q (1 + delta) < thr; Q >= qyes -> alpha Q (1 - delta) >= thr
+    const double thr = c->p.region_thr;
+    const double lo = thr / (alpha * (1.0 + delta)) * (1.0 - 1e-12) - 1.0;
+    const double hi = thr / (alpha * (1.0 - delta)) * (1.0 + 1e-12) + 1.0;
+    if (!(hi < 4294967295.0)) return;
+    c->qno = lo < 0 ? 0u : (uint32_t)std::floor(lo);
+    c->qyes = (uint32_t)std::ceil(hi);
+    if (c->qyes < 1) c->qyes = 1;
+    c->q_alpha = alpha;
+    c->q_delta = delta;
+    c->q_ok = true;
+}
+
+// Q keys for this pass: integer pooled counts (no -z coefficients), Q below
+// 2^32 for the largest possible window, and distinct Q ordering the FP64
+// scores: alpha (Q+1)(1 - delta) > alpha Q (1 + delta) for every Q <= Qmax
+static bool q_mode(const up_ctx *c) {
+    if (!c->q_ok || !c->coef.empty() || c->nc.empty()) return false;
+    const int bw = c->p.bw;
+    const double cmax = (double)std::max<uint32_t>(kEsc - 1, c->ovf_max_all) * (double)c->nc.size() *
+                        (c->p.nondir ? 2.0 : 1.0);
+    const double qmax = (double)bw * bw * (2.0 * bw + 1.0) * cmax;
+    return qmax < 4294967295.0 && 2.0 * c->q_delta * (qmax + 1.0) < 0.5;
 }
 
 // track geometry (bytes): positions 1..len plus the scan domain up to
@@ -730,6 +814,7 @@ static int sync_units(up_ctx *c) {
             u.d_ovf_off = nullptr;
             // entries sorted by (track, position), indexed per kOvfBlk positions
             std::vector<uint64_t> e;
+            u.ovf_max = 0;
             const uint32_t nb = ovf_nblk(u.len);
             std::vector<uint32_t> off(u.ovf.size() * (size_t)(nb + 1), 0);
             for (size_t t = 0; t < u.ovf.size(); ++t) {
@@ -739,6 +824,7 @@ static int sync_units(up_ctx *c) {
                     const uint32_t kb = (uint32_t)((kv.first - 1) >> kOvfBlkShift);  // positions are 1-based
                     while (b <= kb) o[b++] = (uint32_t)e.size();
                     e.push_back(((uint64_t)kv.first << 32) | kv.second);
+                    u.ovf_max = std::max(u.ovf_max, kv.second);
                 }
                 while (b <= nb) o[b++] = (uint32_t)e.size();
             }
@@ -754,6 +840,8 @@ static int sync_units(up_ctx *c) {
                         (uint64_t)(uintptr_t)u.d_ovf, (uint64_t)(uintptr_t)u.d_ovf_off};
     }
     c->nstrips = strip;
+    c->ovf_max_all = 0;
+    for (const Unit &u : c->units) c->ovf_max_all = std::max(c->ovf_max_all, u.ovf_max);
     HIPCHK(c->d_units.ensure(d.size()));
     HIPCHK(hipMemcpy(c->d_units.p, d.data(), d.size() * sizeof(UnitDesc), hipMemcpyHostToDevice));
     c->units_dirty = false;
@@ -792,6 +880,9 @@ static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps) {
     P.xref = ps.d_xref.p;
     P.xcount = ps.d_xcount.p;
     P.spk = ps.d_spk.p;
+    P.qmode = q_mode(c) ? 1 : 0;
+    P.qno = c->qno;
+    P.qyes = c->qyes;
     return P;
 }
 
@@ -890,6 +981,7 @@ static StatParams stat_params(up_ctx *c, up_ctx::Pass &ps) {
     P.out = nullptr;  // set by up_run (mapped host records)
     P.out_counts = nullptr;
     P.cap = 0;
+    P.qmode = q_mode(c) ? 1 : 0;
     return P;
 }
 
@@ -1214,7 +1306,7 @@ static int enqueue_rest(up_ctx *c, int slot, const ScanParams &SP, const StatPar
                        c->hp_status[slot].dev, thdr);
     HIPCHK(hipGetLastError());
     if (events) HIPCHK(hipEventRecord(ps.ev[3], ps.stream));
-    dispatch_stats(c, ps.stream, P, std::max<uint64_t>(c->last_nreg, 1024));
+    dispatch_stats(c, ps.stream, P, std::max<uint64_t>(ps.req_last_nreg, 1024));
     HIPCHK(hipGetLastError());
     if (events) HIPCHK(hipEventRecord(ps.ev[4], ps.stream));
     return UP_OK;
@@ -1263,9 +1355,9 @@ static int launch_pass(up_ctx *c, int slot) {
         HIPCHK(c->hp_regions[slot].ensure(cap + 1));
         HIPCHK(c->hp_counts[slot].ensure((cap + 1) * S));
     }
-    ps.target = c->target;
-    ps.target_hostp = c->target_hostp;
-    ps.target_cap = c->target_cap;
+    ps.target = ps.req_target;
+    ps.target_hostp = ps.req_target_hostp;
+    ps.target_cap = ps.req_target_cap;
     ps.cap = cap;
     ps.ovf_cap = c->ovf_cap;
     // the pass follows everything enqueued on the context stream (track
@@ -1276,8 +1368,12 @@ static int launch_pass(up_ctx *c, int slot) {
     // host saw its previous pass done)
     hipStream_t s1 = c->k1a_stream;
     ps.stream = c->chain[c->nlaunch++ & 1];
-    HIPCHK(hipEventRecord(c->host_work, c->stream));
-    HIPCHK(hipStreamWaitEvent(s1, c->host_work, 0));
+    // (nothing to follow once the context stream has drained: two API
+    // calls per pass fewer, ~5 us of host time, which bounds 8-GPU steps)
+    if (hipStreamQuery(c->stream) != hipSuccess) {
+        HIPCHK(hipEventRecord(c->host_work, c->stream));
+        HIPCHK(hipStreamWaitEvent(s1, c->host_work, 0));
+    }
     if (!ps.counters_armed) {  // K2b re-arms them at the end of every pass
         HIPCHK(hipMemsetAsync(ps.d_ovf_count.p, 0, sizeof(uint32_t), s1));
         HIPCHK(hipMemsetAsync(ps.d_xcount.p, 0, 2 * sizeof(uint32_t), s1));
@@ -1293,7 +1389,7 @@ static int launch_pass(up_ctx *c, int slot) {
         graph = false;
     }
 #endif
-    ps.tl = c->timing;
+    ps.tl = ps.req_tl;
     StatParams P = stat_params(c, ps);
     P.cap = cap;
     P.peak_pos = ps.d_peak_pos.p;
@@ -1319,9 +1415,10 @@ static int launch_pass(up_ctx *c, int slot) {
     c->k1a_waves = 0;
     dispatch_scan<false, kModeScreen>(c, s1, SP, 0, ns);   // K1a: stream + screen
     HIPCHK(hipGetLastError());
-    if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[1], s1));
-    HIPCHK(hipEventRecord(ps.k1a_end, s1));
-    HIPCHK(hipStreamWaitEvent(ps.stream, ps.k1a_end, 0));
+    hipEvent_t k1a_end = ps.k1a_end;  // a timed pass's end-of-K1a event serves as well
+    if (tl >= 1) k1a_end = ps.ev[1];
+    HIPCHK(hipEventRecord(k1a_end, s1));
+    HIPCHK(hipStreamWaitEvent(ps.stream, k1a_end, 0));
     const uint32_t kw = c->k1a_waves, kx = c->k1a_xcap;
     if (!graph || tl >= 2) {
         if (int r = enqueue_rest(c, slot, SP, P, cap, kw, kx, tl >= 2)) return r;
@@ -1334,7 +1431,7 @@ static int launch_pass(up_ctx *c, int slot) {
     key_add(key, P);
     key_add(key, kw);
     key_add(key, kx);
-    key_add(key, std::max<uint64_t>(c->last_nreg, 1024));
+    key_add(key, std::max<uint64_t>(ps.req_last_nreg, 1024));
     key_add(key, (uint32_t)c->units.size());
     key_add(key, c->ovf_cap);
     key_add(key, pool_mode(c));
@@ -1350,7 +1447,7 @@ static int launch_pass(up_ctx *c, int slot) {
     size_t gi = 0;
     while (gi < ps.graphs.size() && ps.graphs[gi].first != key) ++gi;
     if (gi == ps.graphs.size()) {
-        HIPCHK(hipStreamBeginCapture(ps.stream, hipStreamCaptureModeThreadLocal));
+        HIPCHK(hipStreamBeginCapture(ps.stream, hipStreamCaptureModeRelaxed));
         const int r = enqueue_rest(c, slot, SP, P, cap, kw, kx, false);
         hipGraph_t g = nullptr;
         const hipError_t e = hipStreamEndCapture(ps.stream, &g);
@@ -1382,18 +1479,69 @@ static int prepare_run(up_ctx *c) {
     return sync_units(c);
 }
 
+static void launcher_main(up_ctx *c) {
+    (void)hipSetDevice(c->dev);
+    std::unique_lock<std::mutex> lk(c->lmu);
+    for (;;) {
+        c->lcv.wait(lk, [&] { return c->lstop || !c->lq.empty(); });
+        if (c->lq.empty()) return;  // stopping, nothing queued
+        const int slot = c->lq.front();
+        c->lq.pop_front();
+        c->lbusy = true;
+        lk.unlock();
+        const int r = launch_pass(c, slot);
+        lk.lock();
+        c->pass[slot].lrc = r;
+        c->pass[slot].lpending = false;
+        c->lbusy = false;
+        c->lcv.notify_all();
+    }
+}
+
+// every queued pass launched (the launcher idle)
+static void launcher_drain(up_ctx *c) {
+    std::unique_lock<std::mutex> lk(c->lmu);
+    c->lcv.wait(lk, [&] { return c->lq.empty() && !c->lbusy; });
+}
+
+static void launcher_stop(up_ctx *c) {
+    if (!c->launcher.joinable()) return;
+    {
+        std::lock_guard<std::mutex> lk(c->lmu);
+        c->lstop = true;
+    }
+    c->lcv.notify_all();
+    c->launcher.join();
+}
+
 int up_run_async(up_ctx *c) {
     if (!c) return UP_E_ARG;
     if (c->seq_launched - c->seq_done >= kSlots) return UP_E_STATE;  // at most kSlots passes in flight
+    if (busy(c) && c->units_dirty) return UP_E_STATE;  // passes in flight read the unit table
     int r = prepare_run(c);
     if (r) return r;
     const int slot = (int)(c->seq_launched % kSlots);
-    c->pass[slot].t0 = std::chrono::steady_clock::now();
+    up_ctx::Pass &ps = c->pass[slot];
+    ps.t0 = std::chrono::steady_clock::now();
+    ps.lrc = 0;
     if (c->units.empty()) {
         ++c->seq_launched;
         return UP_OK;
     }
-    if ((r = launch_pass(c, slot))) {
+    ps.req_target = c->target;
+    ps.req_target_hostp = c->target_hostp;
+    ps.req_target_cap = c->target_cap;
+    ps.req_tl = c->timing;
+    ps.req_last_nreg = c->last_nreg;
+    if (c->use_launcher) {
+        if (!c->launcher.joinable()) c->launcher = std::thread(launcher_main, c);
+        {
+            std::lock_guard<std::mutex> lk(c->lmu);
+            ps.lpending = true;
+            c->lq.push_back(slot);
+        }
+        c->lcv.notify_one();
+    } else if ((r = launch_pass(c, slot))) {
         sync_all(c);
         c->seq_done = c->seq_launched;  // drop whatever was in flight
         return r;
@@ -1420,10 +1568,16 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
         return UP_OK;
     }
     auto fail = [&](int rc) {
+        launcher_drain(c);
         sync_all(c);
         c->seq_done = c->seq_launched;
         return rc;
     };
+    {   // the launcher thread has enqueued this pass
+        std::unique_lock<std::mutex> lk(c->lmu);
+        c->lcv.wait(lk, [&] { return !ps.lpending; });
+    }
+    if (ps.lrc) return fail(ps.lrc);
     if (hipEventSynchronize(ps.done) != hipSuccess) return fail(UP_E_HIP);
     uint64_t nreg = 0;
     for (int attempt = 0;; ++attempt) {
@@ -1454,16 +1608,11 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
         if (!again) break;
         // rerun this pass alone with grown areas (a later pass in flight
         // finishes first; its own status tells whether it needs the same)
+        // (the launcher first enqueues what is queued: this thread then owns
+        // the launch state)
+        launcher_drain(c);
         if (hipDeviceSynchronize() != hipSuccess) return fail(UP_E_HIP);
-        void *keep_t = c->target, *keep_h = c->target_hostp;
-        const uint64_t keep_cap = c->target_cap;
-        c->target = ps.target;
-        c->target_hostp = ps.target_hostp;
-        c->target_cap = ps.target_cap;
-        int r = launch_pass(c, slot);
-        c->target = (uint8_t *)keep_t;
-        c->target_hostp = keep_h;
-        c->target_cap = keep_cap;
+        int r = launch_pass(c, slot);  // same record target and timing (ps.req_*)
         if (r) return fail(r);
         if (hipEventSynchronize(ps.done) != hipSuccess) return fail(UP_E_HIP);
     }
@@ -1566,8 +1715,10 @@ int up_get_regions(up_ctx *c, up_region *out, uint32_t *counts, size_t cap) {
 }
 
 static void drop_target(up_ctx *c) {
-    if (c->target_host && busy(c))  // a pass in flight may still write it
+    if (c->target_host && busy(c)) {  // a pass in flight may still write it
+        launcher_drain(c);
         sync_all(c);
+    }
     if (c->target_host) (void)hipHostUnregister(c->target_host);
     c->target_host = nullptr;
     c->target = nullptr;

@@ -100,6 +100,12 @@ struct ScanParams {
                             // inside the strip) and of the run open at its last position
                             // ([2..3], from its start or the strip's first position)
     uint32_t ovf_cap;
+    // Integer screen of K1b ("K1b keys"): with qmode set, a
+    // live word's flags come from Q(x) = sum_h c_h (bw^2 - (x-h)^2), exact in
+    // uint32 arithmetic, where Q <= qno proves score < thr and Q >= qyes
+    // proves score >= thr; only words with a lane in between run the FP64 walk
+    int32_t qmode;
+    uint32_t qno, qyes;
 #if defined(UPK_DEBUG_COUNTS) || defined(UPK_DEBUG_TIMES)
     unsigned long long *dbg;  // counters: exact blocks, live words
 #endif
@@ -129,6 +135,7 @@ struct StatParams {
     uint32_t *out_counts; // [n][S]
     double *corr_scratch; // -D -y: per K3 wave corr_cap (f, r) pairs, or null
     uint32_t corr_cap;
+    int32_t qmode;        // K1 peaks are Q keys (ScanParams::qmode): K3 scores the peak
 };
 
 }  // namespace upk

@@ -442,6 +442,19 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return wave_reduce_u32(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
 }
 
+// inclusive wave prefix sum (u32, wrapping): the same DPP steps, each lane
+// adding the partial of the lane n below it (row_shr, 0 past the row start),
+// then the row totals carried by row_bcast 15 / 31
+__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t v) {
+    v += dpp32<0x111, 0xf, true>(0u, v);
+    v += dpp32<0x112, 0xf, true>(0u, v);
+    v += dpp32<0x114, 0xf, true>(0u, v);
+    v += dpp32<0x118, 0xf, true>(0u, v);
+    v += dpp32<0x142, 0xa, false>(0u, v);
+    v += dpp32<0x143, 0xc, false>(0u, v);
+    return v;
+}
+
 __device__ __forceinline__ double wave_max_d(double v) {
     const double ninf = -__builtin_inf();
     v = __builtin_fmax(v, dpp64<0x111, 0xf>(ninf, v));
@@ -645,6 +658,19 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
     const int R = (bw + kChunk - 1) / kChunk;
     const int S = P.S;
+    // K1b keys (ScanParams::qmode): integer pooled counts only (no -z)
+    constexpr bool kQ = MODE == kModeExact && !PROF && POOL != 2;
+    const bool qm = kQ && P.qmode != 0;
+    const double kthr = qm ? 0.5 : P.thr;  // a flagged position's key is >= 1
+    const uint32_t bw2 = (uint32_t)(bw * bw);
+    // Q's window sums read prefix sums bw positions up and bw + 1 down, i.e.
+    // lanes rotated by bw (mod 64) from one of two words.  The rotation is
+    // one ds_bpermute, so each source lane picks the word its unique reader
+    // needs: hi side words 2NH-1 / 2NH after the output word's first window
+    // word, lo side words 0 / 1 (bw >> 6 == NH - 1 for every bw of this NH).
+    const int hadr = 4 * ((lane + bw) & 63), ladr = 4 * ((lane - bw - 1) & 63);
+    const bool hsel = ((((lane - bw) & 63) + bw - 64 * (NH - 1)) >> 6) != 0;
+    const bool lsel = ((((lane + bw + 1) & 63) - bw - 1 + 64 * NH) >> 6) != 0;
     // halo words only matter where they reach an output word
     uint64_t edge_lo[NH], edge_hi[NH];
 #pragma unroll
@@ -833,23 +859,32 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 
         RecList R_{0, 0, kInline};
         uint64_t prevF = 0, F0 = 0;
-        double lb = -__builtin_inf();  // open run: this lane's best f+r so far
+        double lb = -__builtin_inf();  // open run: this lane's best key so far
         uint32_t lp = 0;               // and its (first) position
+        bool lt = false;               // a later position of this lane equals lb
         bool pk_ok = false;            // the run started inside this strip
+        // the run's (first) largest key and its position; with Q keys a
+        // second position holding the largest Q is marked by +0.5 (K3 then
+        // orders the tied positions by their FP64 scores)
+        auto run_peak = [&](double &m, uint32_t &pp) {
+            m = wave_max_d(lb);
+            pp = wave_min_u32(lb == m ? lp : 0xFFFFFFFFu);
+            if (kQ && qm) {
+                const uint64_t at = __ballot(lb == m);
+                if ((at & (at - 1)) != 0 || __ballot(lb == m && lt) != 0) m += 0.5;
+            }
+        };
         auto close_run = [&](uint32_t end_pos) {
-#ifdef UPK_EXP_NOPEAK_REDUCE
-            const double m = lb;
-            const uint32_t pp = lp;
-#else
-            const double m = wave_max_d(lb);
-            const uint32_t pp = wave_min_u32(lb == m ? lp : 0xFFFFFFFFu);
-#endif
+            double m;
+            uint32_t pp;
+            run_peak(m, pp);
             rec_end(R_, end_pos, pk_ok ? pp : 0u, m, P, strip, lane);
             if (!pk_ok && lane == 0) {  // the run open at p0: its part in this strip
                 P.spk[4ull * strip] = (uint64_t)__double_as_longlong(m);
                 P.spk[4ull * strip + 1] = pp;
             }
             lb = -__builtin_inf();
+            lt = false;
         };
 
         for (int j = 0; j < kBlocks; ++j) {
@@ -904,6 +939,70 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 atomicAdd(&P.dbg[3], (unsigned long long)(tq1 - tq0));
             }
 #endif
+            // ---- K1b keys: exact integer Q of every live word ----
+            // Q(x) = sum over hits h within bw of c_h (bw^2 - (x-h)^2), from
+            // wave prefix sums of c, c*j, c*j^2 over the window (j = window
+            // index; uint32 wrap arithmetic is exact since Q < 2^32, which
+            // the host guarantees).  score(x) = alpha * Q(x) * (1 +- delta)
+            // for the FP64 weights and any summation order, so Q <= qno
+            // proves no flag, Q >= qyes a flag, and distinct Q order the
+            // FP64 scores (delta * Q << 1): only words with an undecided
+            // lane go through the FP64 walk below.
+            uint32_t xw = lw;          // output words the FP64 walk computes
+            uint32_t qv[kQ ? SW : 1];  // Q at each live word's lane position
+            if constexpr (kQ) {
+                if (qm) {
+                    xw = 0;
+                    uint32_t P0[NWIN], P1[NWIN], P2[NWIN];
+                    // the prefix sums start at the first live word's window
+                    // (W is a difference of two prefixes: any common base
+                    // cancels) and end with the last one's
+                    uint32_t c0 = 0, c1 = 0, c2 = 0;  // totals of the words before
+                    const int wlo = __builtin_ctz(lw), whi = 31 - __builtin_clz(lw) + 2 * NH;
+                    WordLoop<0, NWIN>::run([&](auto wc) {
+                        constexpr int w = decltype(wc)::value;
+                        uint64_t any = hf[w];
+                        if constexpr (NONDIR) any |= hr[NONDIR ? w : 0];
+                        if (w < wlo || w > whi) any = 0;
+                        if (any == 0) {
+                            P0[w] = c0;
+                            P1[w] = c1;
+                            P2[w] = c2;
+                        } else {
+                            uint32_t c = (uint32_t)wf[w];
+                            if constexpr (NONDIR) c += (uint32_t)wr[NONDIR ? w : 0];
+                            const uint32_t j = 64u * w + (uint32_t)lane;
+                            const uint32_t s0 = wave_scan_u32(c), s1 = wave_scan_u32(c * j),
+                                           s2 = wave_scan_u32(c * (j * j));
+                            P0[w] = s0 + c0;
+                            P1[w] = s1 + c1;
+                            P2[w] = s2 + c2;
+                            c0 += rl_u(s0, 63);
+                            c1 += rl_u(s1, 63);
+                            c2 += rl_u(s2, 63);
+                        }
+                        constexpr int k = w - 2 * NH;  // output word whose window ends with word w
+                        if constexpr (k >= 0) {
+                            if ((lw >> k) & 1u) {
+                                auto win = [&](const uint32_t (&Pa)[NWIN]) {
+                                    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(
+                                        hadr, (int)(hsel ? Pa[k + 2 * NH] : Pa[k + 2 * NH - 1]));
+                                    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(
+                                        ladr, (int)(lsel ? Pa[k + 1] : Pa[k]));
+                                    return hi - lo;
+                                };
+                                const uint32_t W0 = win(P0), W1 = win(P1), W2 = win(P2);
+                                const uint32_t i = 64u * (k + NH) + (uint32_t)lane;
+                                const uint32_t q = bw2 * W0 - (i * i) * W0 + 2u * i * W1 - W2;
+                                qv[k] = q;
+                                if (__ballot(q > P.qno && q < P.qyes)) xw |= 1u << k;
+                            } else {
+                                qv[k] = 0;
+                            }
+                        }
+                    });
+                }
+            }
             // ---- KDE: scatter every hit of the window, ascending ----
             double af[SW], ar[NONDIR ? SW : 1];
 #pragma unroll
@@ -919,7 +1018,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 // output words a hit of window word W reaches: W-2NH .. W
                 constexpr int OLO = W - 2 * NH < 0 ? 0 : W - 2 * NH;
                 constexpr int OHI = W > SW - 1 ? SW - 1 : W;
-                const uint32_t reach = lw & (((2u << OHI) - 1u) & ~((1u << OLO) - 1u));
+                const uint32_t reach = xw & (((2u << OHI) - 1u) & ~((1u << OLO) - 1u));
                 if (!reach) return;
                 uint64_t m = hf[W];
                 if constexpr (W < NH) m &= edge_lo[W];
@@ -956,7 +1055,17 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             for (int k = 0; k < SW; ++k) {
                 if constexpr (NONDIR) sc[k] = af[k] + ar[k];  // forwardScore + reverseScore
                 else sc[k] = af[k];
-                if constexpr (!PROF) sc[k] = ((lw >> k) & 1u) ? sc[k] : -1.0;  // dead word: no flag
+                if constexpr (!PROF) {
+                    if (kQ && qm) {
+                        // key = Q of a flagged position (proven by Q, or by the
+                        // FP64 score of an undecided lane), -1 otherwise
+                        const uint32_t q = qv[kQ ? k : 0];
+                        const bool fl = q >= P.qyes || (q > P.qno && sc[k] >= P.thr);
+                        sc[k] = (((lw >> k) & 1u) && fl) ? (double)q : -1.0;
+                    } else {
+                        sc[k] = ((lw >> k) & 1u) ? sc[k] : -1.0;  // dead word: no flag
+                    }
+                }
                 mx = __builtin_fmax(mx, sc[k]);
             }
             if constexpr (PROF) {
@@ -990,7 +1099,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 const uint64_t anyflag = 0;
                 prevF = __ballot(mx == 1.2345) & 1;
 #else
-                const uint64_t anyflag = __ballot(mx >= P.thr);
+                const uint64_t anyflag = __ballot(mx >= kthr);
 #endif
                 if (anyflag | prevF) {
                     // scores through LDS so the word loop below stays a loop
@@ -1010,7 +1119,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             continue;
                         }
                         const double sck = scs[64 * k + lane];
-                        const uint64_t F = __ballot(sck >= P.thr);
+                        const uint64_t F = __ballot(sck >= kthr);
                         const bool cont = (prevF >> 63) != 0;  // run open at the previous position
                         if (cont && !(F & 1ull)) close_run((uint32_t)(wpos - 1));
                         uint64_t st;
@@ -1048,11 +1157,17 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             rem &= ~seg;
                             if (!(a == 0 && cont)) {  // a new run
                                 lb = -__builtin_inf();
+                                lt = false;
                                 pk_ok = !(j == 0 && k == 0 && a == 0);  // may continue the previous strip
                             }
-                            if (((seg >> lane) & 1ull) && sck > lb) {
-                                lb = sck;
-                                lp = (uint32_t)(wpos + lane);
+                            if ((seg >> lane) & 1ull) {
+                                if (sck > lb) {
+                                    lb = sck;
+                                    lp = (uint32_t)(wpos + lane);
+                                    lt = false;
+                                } else if (sck == lb) {
+                                    lt = true;
+                                }
                             }
                             if (a + len < 64) close_run((uint32_t)(wpos + a + len - 1));
                         }
@@ -1067,8 +1182,9 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         }
         if constexpr (PROF) continue;
         if (prevF >> 63) {  // the run open at the strip's last position: its part here
-            const double m = wave_max_d(lb);
-            const uint32_t pp = wave_min_u32(lb == m ? lp : 0xFFFFFFFFu);
+            double m;
+            uint32_t pp;
+            run_peak(m, pp);
             if (lane == 0) {
                 P.spk[4ull * strip + 2] = (uint64_t)__double_as_longlong(m);
                 P.spk[4ull * strip + 3] = pp;
@@ -1367,6 +1483,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
     uint32_t dsc = wave < nreg ? desc_load(wave) : 0u;
     bool pre_ok = false;  // praw holds the count bytes of region ri
     uint32_t praw[kPrefetch ? kStatCache : 1];
+    bool pk_pre = false;  // pkraw holds the bytes of the window around pk_pos (Q keys)
+    uint32_t pk_pos = 0, pkraw[kPrefetch ? 2 * NH : 1];
     for (uint64_t ri = wave; ri < nreg; ri += nwaves) {
         const uint32_t left = rl_u(dsc, 0), right = rl_u(dsc, 1), u = rl_u(dsc, 2);
         const uint64_t rn = ri + nwaves;
@@ -1411,12 +1529,43 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                     const bool pre = (s > sa || left == sp0) && s == sb && right < sp0 + kStrip - 1;
                     const uint64_t *e = P.spk + 4ull * s + (pre ? 0 : 2);
                     const double v = __longlong_as_double((long long)e[0]);
-                    if (s == sa || v > kval) {
+                    if (P.qmode) {  // Q keys: equal Q in two parts is a tie too
+                        const double fv = __builtin_floor(v), fk = __builtin_floor(kval);
+                        if (s == sa || fv > fk) {
+                            kval = v;
+                            kpos = (uint32_t)e[1];
+                        } else if (fv == fk) {
+                            kval = fk + 0.5;
+                        }
+                    } else if (s == sa || v > kval) {
                         kval = v;
                         kpos = (uint32_t)e[1];
                     }
                 }
             }
+        }
+        // Q keys (K1b, ScanParams::qmode) give the peak position; a key
+        // marked +0.5 (the largest Q at two positions) leaves the first
+        // maximum to the FP64 scores of this region's KDE below
+        const bool kn = known && !(P.qmode && kval != __builtin_floor(kval));
+        // the peak's FP64 score: the pooled counts of its window (2NH words
+        // from kpos - bw, lane = offset t), fetched now and summed after the
+        // region's counts
+        WinT<POOL> pkf[2 * NH], pkr[NONDIR ? 2 * NH : 1];
+        if (kn && P.qmode) {
+            if (kPrefetch && pk_pre && pk_pos == kpos) {  // fetched during the previous region
+                const uint32_t sh = 4 * (uint32_t)((kPadPos + (int64_t)kpos - bw - 1 + lane) & 1);
+                uint32_t c[kPrefetch ? 2 * NH : 1];
+#pragma unroll
+                for (int w = 0; w < (kPrefetch ? 2 * NH : 1); ++w) c[w] = (pkraw[w] >> sh) & 15u;
+                resolve_escapes<kPrefetch ? 2 * NH : 1>(c, U, (uint32_t)P.nc[0], (int64_t)kpos - bw, lane);
+#pragma unroll
+                for (int w = 0; w < (kPrefetch ? 2 * NH : 1); ++w) pkf[w] = c[w];
+            } else {
+                load_words<2 * NH, POOL>(pkf, U, S, 0, (int64_t)kpos - bw, lane, P.nnc, P.nc, P.coef);
+            }
+            if constexpr (NONDIR)
+                load_words<2 * NH, POOL>(pkr, U, S, 1, (int64_t)kpos - bw, lane, P.nnc, P.nc, P.coef);
         }
         int blk = 0;
         bool counted = false;
@@ -1425,7 +1574,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
             // words) are fetched with all loads in flight at once, then
             // scored; escapes resolved at use
             const int nw = (int)((right - left) / 64u) + 1;
-            if (known && S == 1 && nw <= kStatCache) {
+            if (kn && S == 1 && nw <= kStatCache) {
                 best = kval;
                 best_x = kpos;
                 const int64_t n0 = kPadPos + (int64_t)left - 1 + lane;
@@ -1467,7 +1616,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 counted = true;
             }
         }
-        if (known && !counted) {
+        if (kn && !counted) {
             best = kval;
             best_x = kpos;
             for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64, ++blk) {
@@ -1504,7 +1653,56 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 sum_acc += pc * (uint32_t)(uint16_t)(x - left);
             }
         }
-        if (!known) {
+        if (kn && P.qmode) {
+            // score(kpos) as the reference sums it (peakcall.cpp:203-209):
+            // the hit at kpos - bw + t adds kernel[2bw - t] * countSum, in
+            // ascending t; each lane forms its products, the hits' products
+            // are compacted in order and added up from LDS broadcasts
+            double f = 0.0, r = 0.0;
+#pragma unroll
+            for (int q = 0; q < 2 * NH; ++q) {
+                const int t = 64 * q + lane;
+                const bool in = t <= 2 * bw;
+                const double kw = ktab[2 * bw - t];  // padded table: in range
+                const bool hf = in && nz(pkf[q]);
+                const double vf = hf ? kw * (double)pkf[q] : 0.0;
+                bool hr = false;
+                double vr = 0.0;
+                if constexpr (NONDIR) {
+                    hr = in && nz(pkr[NONDIR ? q : 0]);
+                    vr = hr ? kw * (double)pkr[NONDIR ? q : 0] : 0.0;
+                }
+                const uint64_t m = __ballot(hf || hr);
+                if (hf || hr) {
+                    const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    terms[k] = make_double2(vf, vr);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int nh = __builtin_popcountll(m);
+                int k = 0;
+                for (; k + kTermBatch <= nh; k += kTermBatch) {
+                    double2 v[kTermBatch];
+#pragma unroll
+                    for (int i = 0; i < kTermBatch; ++i) v[i] = terms[k + i];
+#pragma unroll
+                    for (int i = 0; i < kTermBatch; ++i) {
+                        f = f + v[i].x;  // a +0 of the other strand leaves a sum as it is
+                        r = r + v[i].y;
+                    }
+                }
+                for (; k < nh; ++k) {
+                    const double2 a = terms[k];
+                    f = f + a.x;
+                    r = r + a.y;
+                }
+                __builtin_amdgcn_wave_barrier();  // terms reused
+            }
+            best = NONDIR ? f + r : f;
+        }
+        if (!kn) {
         if constexpr (POOL == 0) {
             fetch_raw(nf, 0, left);
             if constexpr (NONDIR) fetch_raw(nr, 1, left);
@@ -1608,7 +1806,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 best_x = ox;
             }
         }
-        }  // !known
+        }  // !kn
         if (POOL == 0 && S == 1) {
             const uint32_t t = wave_sum_u32(esum1);
             esum[0] = lane == 0 ? t : 0u;
@@ -1629,6 +1827,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                     for (int w = 0; w < kStatCache; ++w) praw[w] = w < nwn ? tn[32 * w] : 0u;
                     pre_ok = true;
                 }
+            }
+            // and the bytes of its peak's window (Q keys; a run over strip
+            // edges finds its peak position later)
+            pk_pre = false;
+            if (known && P.qmode && rn < nreg && rl_u(dsc_n, 3) != 0) {
+                pk_pos = rl_u(dsc_n, 3);
+                const UnitDesc Un = P.units[rl_u(dsc_n, 2)];
+                const int64_t n0 = kPadPos + (int64_t)pk_pos - bw - 1 + lane;
+                gu8 *tp = track_u8(Un, S, 0, P.nc[0]) + (n0 >> 1);
+#pragma unroll
+                for (int w = 0; w < (kPrefetch ? 2 * NH : 1); ++w) pkraw[w] = tp[32 * w];
+                pk_pre = true;
             }
         }
         // ---- pass 2: kurtosis (data.cpp:164-182; powi semantics) ----
