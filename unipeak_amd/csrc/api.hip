@@ -1379,7 +1379,12 @@ static int launch_pass(up_ctx *c, int slot) {
         HIPCHK(hipMemsetAsync(ps.d_xcount.p, 0, 2 * sizeof(uint32_t), s1));
     }
     ScanParams SP = scan_params(c, ps);
-    bool graph = c->use_graphs;
+    // K1x..K3 as a captured graph only when the caller's thread launches:
+    // capturing on the launcher thread while the caller waits on earlier
+    // passes invalidated captures (hipErrorStreamCaptureInvalidated, ROCm
+    // 7.2, even in relaxed mode), and off the caller's thread the five
+    // plain launches cost nothing on the caller's critical path
+    bool graph = c->use_graphs && !c->use_launcher;
 #if defined(UPK_DEBUG_COUNTS) || defined(UPK_DEBUG_TIMES)
     static const bool dbg = getenv("UNIPEAK_DEBUG_COUNTS") != nullptr;
     if (dbg) {
@@ -1447,7 +1452,7 @@ static int launch_pass(up_ctx *c, int slot) {
     size_t gi = 0;
     while (gi < ps.graphs.size() && ps.graphs[gi].first != key) ++gi;
     if (gi == ps.graphs.size()) {
-        HIPCHK(hipStreamBeginCapture(ps.stream, hipStreamCaptureModeRelaxed));
+        HIPCHK(hipStreamBeginCapture(ps.stream, hipStreamCaptureModeThreadLocal));
         const int r = enqueue_rest(c, slot, SP, P, cap, kw, kx, false);
         hipGraph_t g = nullptr;
         const hipError_t e = hipStreamEndCapture(ps.stream, &g);
