@@ -117,16 +117,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     comm = None
+    # UNIPEAK_SHARE_GPU=1 (rehearsal on a one-GPU box, with
+    # UNIPEAK_DIST_BACKEND=gloo: RCCL refuses two ranks on one GPU): every
+    # rank runs on device 0, so the N-rank path -- StepBoard, node-shared
+    # record slots, rank 0's merge -- runs end to end on real hardware
+    dev = 0 if os.environ.get("UNIPEAK_SHARE_GPU") == "1" else local
     if world > 1 or os.environ.get("UNIPEAK_BENCH_DIST") == "1":
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)  # torch's HIP runtime first (tools/mix_probe.py)
+        torch.cuda.set_device(dev)  # torch's HIP runtime first (tools/mix_probe.py)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29577")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
-        dist.init_process_group("nccl")  # RCCL over xGMI
-        comm = shard.Comm(dist, rank, world, f"cuda:{local}")
+        backend = os.environ.get("UNIPEAK_DIST_BACKEND", "nccl")  # "nccl" = RCCL over xGMI
+        dist.init_process_group(backend)
+        comm = shard.Comm(dist, rank, world, f"cuda:{dev}" if backend == "nccl" else "cpu")
 
     contigs = load_table(W["tables"])
     genome = sum(L for _, L in contigs)
@@ -150,7 +156,7 @@ def main():
                          f"N={world}; run it on more GPUs")
 
     control = [0] * s_nc + [1] * n_ctl
-    g = capi.Lib(local)
+    g = capi.Lib(dev)
     g.set_params(args.bw, S, 0.0029, nondir=nondir, control=control)  # background set per step
     t_gen = time.time()
     for k in mine:  # ascending global order: records come back unit-major
@@ -164,7 +170,7 @@ def main():
     local_tags = sum(g.tag_total(i, st, smp) for i in range(len(mine)) for st in range(nstr)
                      for smp in range(s_nc))
     if sim_world > 1:  # the background needs the genome-wide total: generate the other units too
-        g2 = capi.Lib(local)
+        g2 = capi.Lib(dev)
         g2.set_params(args.bw, S, 0.0029, nondir=nondir, control=control)
         for k in range(len(units)):
             if k in mine:

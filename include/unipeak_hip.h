@@ -154,7 +154,10 @@ int up_run(up_ctx *ctx, uint64_t *n_regions);
  * kernels.  Each pass delivers into the record target that was set when it
  * was launched, so a caller rotates targets; with host delivery the view of
  * a pass stays valid until the UP_MAX_IN_FLIGHT-th following launch.  Units and
- * parameters cannot change while a pass is in flight (UP_E_STATE). */
+ * parameters cannot change while a pass is in flight (UP_E_STATE).  The HIP
+ * calls of an async pass run on the context's own launcher thread
+ * (UNIPEAK_LAUNCHER=0: on the caller's); a launch failure is returned by the
+ * up_run_wait of that pass.  The context is still driven by one caller thread. */
 #define UP_MAX_IN_FLIGHT 5
 int up_run_async(up_ctx *ctx);
 int up_run_wait(up_ctx *ctx, uint64_t *n_regions);
