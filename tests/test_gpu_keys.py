@@ -95,3 +95,19 @@ def test_large_counts(gpu_lib, oracle, big):
     ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, kurt_thr=0.0)
     regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, kurt_thr=0.0)
     compare(ref, ref_sums, regs, gcnt)
+
+
+def test_keys_with_pooled_samples_nondir_corr(gpu_lib, oracle):
+    """several pooled samples use the keys only when K3 runs its own KDE
+    (-D with the strand correlation): K1b keys over pooled integer counts"""
+    from tests.test_gpu_unit import close
+    rng = np.random.default_rng(2024)
+    length, bw, bg, S = 120_000, 50, 0.004, 3
+    pos, cf = random_unit(rng, length, bw, S=S)
+    cr = np.roll(cf, 5, axis=0)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cf, cr, nondir=True, corr_thr=0.2, control=[0, 1, 0])
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cf, cr, nondir=True, corr_thr=0.2,
+                             control=[0, 1, 0], want_corr=True)
+    compare(ref, ref_sums, regs, gcnt)
+    assert close(ref["corr"], regs["corr"])
+    assert len(regs) > 5

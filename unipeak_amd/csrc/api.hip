@@ -517,6 +517,13 @@ static void set_q_params(up_ctx *c) {
 // scores: alpha (Q+1)(1 - delta) > alpha Q (1 + delta) for every Q <= Qmax
 static bool q_mode(const up_ctx *c) {
     if (!c->q_ok || !c->coef.empty() || c->nc.empty()) return false;
+    // several pooled samples: K3 would score each peak from every sample's
+    // window bytes, which cost more than the keys save in K1b (hg19, 8
+    // samples + 1 control: K1b 2.07 -> 1.64 ms but K3 0.82 -> 1.08-1.23 ms,
+    // 541 -> 515-525 Gbp/s) -- unless K3 runs its own KDE anyway (-D with
+    // the strand correlation), where the keys are K1b's gain only
+    const bool k3_kde = c->p.nondir && (c->p.want_corr || c->p.corr_thr > -1);
+    if (c->nc.size() > 1 && !k3_kde) return false;
     const int bw = c->p.bw;
     const double cmax = (double)std::max<uint32_t>(kEsc - 1, c->ovf_max_all) * (double)c->nc.size() *
                         (c->p.nondir ? 2.0 : 1.0);

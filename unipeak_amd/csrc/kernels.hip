@@ -659,7 +659,9 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     const int R = (bw + kChunk - 1) / kChunk;
     const int S = P.S;
     // K1b keys (ScanParams::qmode): integer pooled counts only (no -z)
-    constexpr bool kQ = MODE == kModeExact && !PROF && POOL != 2;
+    // (several pooled samples only with -D, where K3 runs its own KDE:
+    // api.hip q_mode)
+    constexpr bool kQ = MODE == kModeExact && !PROF && (POOL == 0 || (POOL == 1 && NONDIR));
     const bool qm = kQ && P.qmode != 0;
     const double kthr = qm ? 0.5 : P.thr;  // a flagged position's key is >= 1
     const uint32_t bw2 = (uint32_t)(bw * bw);
@@ -1551,8 +1553,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
         // the peak's FP64 score: the pooled counts of its window (2NH words
         // from kpos - bw, lane = offset t), fetched now and summed after the
         // region's counts
-        WinT<POOL> pkf[2 * NH], pkr[NONDIR ? 2 * NH : 1];
-        if (kn && P.qmode) {
+        // (several pooled samples use Q keys only with -D -y, where K3 runs
+        // its own KDE: the peak code exists for one pooled sample only)
+        constexpr int kPK = POOL == 0 ? 2 * NH : 1;
+        WinT<POOL> pkf[kPK], pkr[NONDIR ? kPK : 1];
+        if (POOL == 0 && kn && P.qmode) {
             if (kPrefetch && pk_pre && pk_pos == kpos) {  // fetched during the previous region
                 const uint32_t sh = 4 * (uint32_t)((kPadPos + (int64_t)kpos - bw - 1 + lane) & 1);
                 uint32_t c[kPrefetch ? 2 * NH : 1];
@@ -1562,10 +1567,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
 #pragma unroll
                 for (int w = 0; w < (kPrefetch ? 2 * NH : 1); ++w) pkf[w] = c[w];
             } else {
-                load_words<2 * NH, POOL>(pkf, U, S, 0, (int64_t)kpos - bw, lane, P.nnc, P.nc, P.coef);
+                load_words<kPK, POOL>(pkf, U, S, 0, (int64_t)kpos - bw, lane, P.nnc, P.nc, P.coef);
             }
             if constexpr (NONDIR)
-                load_words<2 * NH, POOL>(pkr, U, S, 1, (int64_t)kpos - bw, lane, P.nnc, P.nc, P.coef);
+                load_words<kPK, POOL>(pkr, U, S, 1, (int64_t)kpos - bw, lane, P.nnc, P.nc, P.coef);
         }
         int blk = 0;
         bool counted = false;
@@ -1653,14 +1658,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 sum_acc += pc * (uint32_t)(uint16_t)(x - left);
             }
         }
-        if (kn && P.qmode) {
+        if (POOL == 0 && kn && P.qmode) {
             // score(kpos) as the reference sums it (peakcall.cpp:203-209):
             // the hit at kpos - bw + t adds kernel[2bw - t] * countSum, in
             // ascending t; each lane forms its products, the hits' products
             // are compacted in order and added up from LDS broadcasts
             double f = 0.0, r = 0.0;
 #pragma unroll
-            for (int q = 0; q < 2 * NH; ++q) {
+            for (int q = 0; q < kPK; ++q) {
                 const int t = 64 * q + lane;
                 const bool in = t <= 2 * bw;
                 const double kw = ktab[2 * bw - t];  // padded table: in range
