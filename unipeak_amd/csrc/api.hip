@@ -101,7 +101,7 @@ struct up_ctx {
     int dev = 0;
     int ncu = 0;                     // compute units of the device
     int k1a_per_cu = 2;              // K1a workgroups per CU (UNIPEAK_K1A_PER_CU; 0 = resident max)
-    int k1b_per_cu = 0;              // K1b workgroups per CU (UNIPEAK_K1B_PER_CU; 0 = twice resident)
+    int k1b_per_cu = 0;              // K1b workgroups per CU (UNIPEAK_K1B_PER_CU; 0 = resident)
     bool use_graphs = true;          // passes as hipGraphs (UNIPEAK_GRAPHS=0: plain launches)
     // streams of the passes (with the context stream: four, HIP's default
     // hardware queues per process, so no two share a queue): every K1a on one
@@ -921,11 +921,11 @@ static void launch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32_t
     const void *k = (const void *)scan_kernel<NH, POOL, ND, PROF, MODE>;
     uint32_t blocks = resident_blocks(c, k, lds);
     if (MODE == kModeExact) {
-        // K1b: grid-stride over the device-side work-list count; twice the
-        // resident grid measured better (the 8-GPU plan's rank: 57 vs 82 us):
-        // a workgroup that retires early hands its slot to one whose waves
-        // start at later (cheaper, single-block) items
-        blocks *= 2;
+        // K1b: grid-stride over the device-side work-list count, the
+        // resident grid.  Round 1 launched twice that (the 8-GPU plan's rank:
+        // 57 vs 82 us with the FP64 walk); with the keys' cheaper items the
+        // resident grid is as fast there and 2.8 % faster at N=1 (hg19, four
+        // alternating pairs: 4,332 vs 4,214 Gbp/s, UNIPEAK_K1B_PER_CU A/B)
         if (c->k1b_per_cu > 0) blocks = (uint32_t)c->k1b_per_cu * (uint32_t)(c->ncu > 0 ? c->ncu : 256);
     } else {
         if (MODE == kModeScreen) {
