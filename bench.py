@@ -150,7 +150,8 @@ def main():
         raise SystemExit("UNIPEAK_SIM_WORLD is for single-process runs")
     units, owner, mine_all = shard.plan(lens, nondir=nondir, world=sim_world or world, n_samples=S)
     mine = mine_all[sim_rank if sim_world > 1 else rank]
-    need = sum(lens[units[k][0]] * nstr * S for k in mine)
+    # resident track bytes: 4-bit counts, two positions per byte
+    need = sum(lens[units[k][0]] * nstr * S for k in mine) / 2
     if need > 250e9:
         raise SystemExit(f"workload {args.workload} needs {need / 1e9:.0f} GB of tracks per GPU at "
                          f"N={world}; run it on more GPUs")
@@ -214,6 +215,10 @@ def main():
     # through two record targets, i.e. two cached graphs)
     DEPTH = int(os.environ.get("UNIPEAK_BENCH_DEPTH", str(capi.MAX_IN_FLIGHT)))
     NSLOT = 2 * capi.MAX_IN_FLIGHT
+    # at most MAX_IN_FLIGHT passes in flight (up_run_async), and rank 0's
+    # reads trail by DEPTH steps while a slot is reused after NSLOT steps
+    if not 1 <= DEPTH <= capi.MAX_IN_FLIGHT or NSLOT < 2 * DEPTH:
+        raise SystemExit(f"UNIPEAK_BENCH_DEPTH={DEPTH}: must be 1..{capi.MAX_IN_FLIGHT}")
     pipelined = comm is None or gather_mode == "shm"
     if pipelined:
         tag = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}_{os.environ.get('MASTER_PORT', '0')}"

@@ -109,9 +109,10 @@ int up_set_params(up_ctx *ctx, const up_params *p);
  * reverse buffer) over one contig pass; units of one buffer must be added in
  * the order the buffer sees them.  nstrands is 1 (directional) or 2
  * (nondirectional: strand 0 forward, 1 reverse).  Tracks start zeroed and
- * cover positions 1..contig_len; in device memory they are uint8 counts with
- * an exact overflow table for counts >= 255 (DESIGN.md "Data layout"), so
- * any uint32 count can be written.
+ * cover positions 1..contig_len; in device memory they are 4-bit counts (two
+ * positions per byte) with the escape nibble 15 and an exact per-unit
+ * overflow table for counts >= 15, so any uint32 count can
+ * be written.
  * Quirk Q1 (misc/peakcall.cpp:177-183): a unit with pooled tags at a position
  * <= bw is replayed by the exact state machine; if all of its adds sit at
  * positions <= bw its leftover state leaks into the buffer's NEXT unit, which
@@ -123,7 +124,9 @@ int up_unit_count(up_ctx *ctx, uint32_t *n);
  * (1-based) at dev_counts[p-1], contig_len elements (same device) */
 int up_unit_pack(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
                  const uint32_t *dev_counts);
-/* write n (pos, count) host pairs (positions 1..len, unique) into a track */
+/* write n (pos, count) host pairs into a track: positions 1..len, each at
+ * most once per call (UP_E_ARG otherwise: one nibble written twice would OR
+ * two counts together); a count of 0 clears the position */
 int up_unit_scatter(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
                     size_t n, const uint32_t *pos, const uint32_t *counts);
 /* fill a track with the synthetic hg19-shaped spec */

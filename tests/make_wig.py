@@ -28,33 +28,33 @@ def contig_table(name):
     return rows
 
 
-def lines_for(pos, cnt, neg):
-    sep = " -" if neg else " "
-    return "\n".join(f"{p}{sep}{c}" for p, c in zip(pos.tolist(), cnt.tolist()))
-
-
-def write_sample(path, name, orc, contigs, seed, nondir, peaks, bw=50):
-    with ThreadPoolExecutor(8) as ex:
-        jobs = {}
-        for st in (0, 1):
-            for ci, (c, L) in enumerate(contigs):
-                jobs[(st, ci)] = ex.submit(
-                    lambda st=st, ci=ci, L=L: orc.synth_track(seed, ci, st, nondir, L, bw, peaks))
-        total = sum(int(f.result()[1].sum()) for f in jobs.values())
-        texts = {k: ex.submit(lines_for, *jobs[k].result(), k[0] == 1) for k in jobs}
-        with open(path, "w") as f:
-            f.write(f"# original_file=synthetic seed {seed}\n# tags={total}\n")
+def write_sample(path, name, orc, contigs, seed, nondir, peaks, bw=50, index=None,
+                 workers=8):
+    """One directional wig (both strand tracks) of the synthetic spec.
+    contigs: [(name, length)]; index: the generator's contig index of each
+    (default 0..n-1, i.e. the position in the table the generator keys on)."""
+    index = list(range(len(contigs))) if index is None else index
+    with ThreadPoolExecutor(workers) as ex:
+        def one(st, ci, L):
+            pos, cnt = orc.synth_track(seed, ci, st, nondir, L, bw, peaks)
+            return int(cnt.sum(dtype=np.uint64)), orc.format_pairs(pos, cnt, st == 1)
+        jobs = {(st, k): ex.submit(one, st, index[k], L)
+                for st in (0, 1) for k, (_, L) in enumerate(contigs)}
+        total = sum(f.result()[0] for f in jobs.values())
+        with open(path, "wb") as f:
+            f.write(f"# original_file=synthetic seed {seed}\n# tags={total}\n".encode())
             for st in (0, 1):
                 if st == 0:
                     f.write(f'track name="{name} +" description="{name}" priority=3 '
-                            'visibility=full type=wiggle_0 alwaysZero=on color=0,0,255\n')
+                            'visibility=full type=wiggle_0 alwaysZero=on color=0,0,255\n'.encode())
                 else:
                     f.write(f'track name="{name} -" description=" " priority=3 visibility=full '
-                            'type=wiggle_0 alwaysZero=on color=255,0,0 altColor=255,0,0\n')
-                for ci, (c, _) in enumerate(contigs):
-                    t = texts[(st, ci)].result()
+                            'type=wiggle_0 alwaysZero=on color=255,0,0 altColor=255,0,0\n'.encode())
+                for k, (c, _) in enumerate(contigs):
+                    t = jobs[(st, k)].result()[1]
                     if t:
-                        f.write(f"variableStep chrom={c}\n{t}\n")
+                        f.write(f"variableStep chrom={c}\n".encode())
+                        f.write(t)
     return total
 
 

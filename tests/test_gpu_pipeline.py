@@ -149,21 +149,41 @@ def test_many_units_many_blocks(gpu_lib, oracle):
 
 
 
-def test_launcher_thread_under_graph_capture(gpu_lib):
-    """bench-shaped: UP_MAX_IN_FLIGHT passes in flight, K1x..K3 captured as
-    graphs (timing level 1) on the library's launcher thread while this
-    thread waits for, times and reads the older passes"""
+def _open(capi, launcher):
+    """a context with the launcher thread on (default) or off
+    (UNIPEAK_LAUNCHER=0: the caller's thread launches, K1x..K3 of a pass go
+    out as a cached hipGraph keyed by every launch argument); up_open reads
+    the variable"""
+    import os
+    old = os.environ.get("UNIPEAK_LAUNCHER")
+    os.environ["UNIPEAK_LAUNCHER"] = "1" if launcher else "0"
+    try:
+        return capi.Lib(0)
+    finally:
+        if old is None:
+            del os.environ["UNIPEAK_LAUNCHER"]
+        else:
+            os.environ["UNIPEAK_LAUNCHER"] = old
+
+
+@pytest.mark.parametrize("launcher,ntargets", [(True, 2), (False, 2), (False, 9)])
+def test_many_passes_rotating_targets(gpu_lib, launcher, ntargets):
+    """bench-shaped: UP_MAX_IN_FLIGHT passes in flight (timing level 1) while
+    this thread waits for, times and reads the older passes.  With the
+    launcher thread K1x..K3 are plain launches on it; without it they are
+    cached graphs -- ntargets record targets per pass slot makes 9 distinct
+    graph keys per slot, past the 8-entry cache (eviction and re-capture)"""
     capi = gpu_lib
     rng = np.random.default_rng(11)
     bw = 50
-    with capi.Lib(0) as g:
+    with _open(capi, launcher) as g:
         g.set_params(bw, 1, 0.003)
         _load(g, rng, [int(x) for x in rng.integers(300_000, 3_000_000, size=9)], bw)
         n = g.run()
         ref, _ = g.regions(n)
         cap = n + 16
         depth = capi.MAX_IN_FLIGHT
-        bufs = [_target(cap, 1, capi.REGION_DTYPE.itemsize) for _ in range(2 * depth)]
+        bufs = [_target(cap, 1, capi.REGION_DTYPE.itemsize) for _ in range(ntargets * depth)]
         for b, off in bufs:
             g.host_register(b[off:].ctypes.data, len(b) - off)
         g.set_timing(1)
@@ -182,3 +202,48 @@ def test_launcher_thread_under_graph_capture(gpu_lib):
                 assert recs.tobytes() == ref.tobytes()
         g.set_record_target(0, 0)
         g.set_timing(2)
+
+
+@pytest.mark.parametrize("launcher", [True, False])
+def test_mixed_host_delivery_and_targets(gpu_lib, launcher):
+    """passes queued with host delivery (no target) and with a registered
+    target alternate while UP_MAX_IN_FLIGHT passes are in flight: each pass
+    keeps the delivery it was queued with (the launcher reads only the
+    request snapshot), and the host view of a host-delivered pass is valid
+    although a target is set for the later passes"""
+    capi = gpu_lib
+    rng = np.random.default_rng(23)
+    bw = 50
+    with _open(capi, launcher) as g:
+        g.set_params(bw, 1, 0.003)
+        _load(g, rng, [int(x) for x in rng.integers(200_000, 2_000_000, size=6)], bw)
+        n = g.run()
+        ref, rcnt = g.regions(n)
+        cap = n + 16
+        depth = capi.MAX_IN_FLIGHT
+        bufs = [_target(cap, 1, capi.REGION_DTYPE.itemsize) for _ in range(2 * depth)]
+        for b, off in bufs:
+            g.host_register(b[off:].ctypes.data, len(b) - off)
+        npass = 31
+        host = [i % 3 == 0 for i in range(npass)]
+        for i in range(npass + depth - 1):
+            if i < npass:
+                if host[i]:
+                    g.set_record_target(0, 0)
+                else:
+                    b, off = bufs[i % len(bufs)]
+                    g.set_record_target(b[off:].ctypes.data, cap)
+                g.run_async()
+            if i >= depth - 1:
+                j = i - depth + 1
+                assert g.run_wait() == n
+                if host[j]:
+                    recs, cnt = g.regions(n)
+                else:
+                    b, off = bufs[j % len(bufs)]
+                    recs, cnt = _parse(b, off, cap, 1, capi.REGION_DTYPE)
+                    with pytest.raises(capi.UpError):
+                        g.regions(n)  # this pass delivered into its target
+                assert recs.tobytes() == ref.tobytes(), j
+                assert np.array_equal(cnt, rcnt), j
+        g.set_record_target(0, 0)

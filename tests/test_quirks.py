@@ -1,0 +1,277 @@
+"""Fixtures for the quirks SURVEY.md §8(c) F3/F4 lists that the earlier
+suites did not reach (Appendix A):
+
+* Q8  a region longer than 65,536 positions: Region::posMean/posKurtosis
+      index positions with a UShort (wraps) and sum `posCount*pos` in a
+      uint32 (wraps) -- misc/data.cpp:133-182;
+* Q10 the hg19+mm9 prefixed table: ContigTable::genomeSize_ is uint32, so
+      5,750,605,500 bp wraps to 1,455,638,204 in the background --
+      misc/data.hpp:97, misc/data.cpp:204-214, src/regions.cpp:205-213;
+* Q14 header number formats: OutStream<<double prints 17 significant
+      digits (`# corr_threshold=0.29999999999999999`, the string the survey
+      recorded from the reference) -- misc/filterstream.cpp:134-137;
+* Q15 std::sort (unstable) by Region::sum() in strand_shift: which of
+      several equal-sum regions are tested depends on libstdc++'s introsort
+      -- src/strand_shift.cpp:198.
+
+CPU tests pin the oracle; gpu tests run the product (C-ABI / bin/) against it.
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.wig import parse_table, write_contigs, write_wig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "bin")
+
+
+def _run(cmd, cwd):
+    r = subprocess.run(cmd, cwd=cwd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise AssertionError(f"{cmd[0]} failed ({r.returncode}):\n{r.stderr[-2000:]}")
+    return r
+
+
+def _both(orc_bin, tmp_path, tool, args, name="out.txt"):
+    _run([orc_bin, tool] + args + ["-o", "ref_" + name], tmp_path)
+    _run([os.path.join(BIN, tool)] + args + ["-o", "got_" + name], tmp_path)
+    a = (tmp_path / ("ref_" + name)).read_bytes()
+    b = (tmp_path / ("got_" + name)).read_bytes()
+    assert a == b, f"{tool} outputs differ\n--- oracle\n{a[:2000].decode()}\n--- bin\n{b[:2000].decode()}"
+    return a.decode()
+
+
+# ---- Q8 ---------------------------------------------------------------------
+
+Q8_BLOCKS = [  # (first, n positions, count, step): one region per block
+    (10_000, 70_000, 1, 1),     # 70 k positions: UShort index wraps once
+    (5_000, 140_000, 7, 1),     # wraps twice; uint32 sum wraps (7 * sum of pos ~ 3e10)
+    (20_000, 66_000, 20, 3),    # escaped counts (>= 15) every third position
+]
+
+
+def q8_unit(first, n, c, step, length=300_000, seed=0):
+    rng = np.random.default_rng(seed)
+    dense = {int(p): c for p in range(first, first + n, step)}
+    for p in rng.integers(200, length - 200, 400):  # background around the block
+        dense[int(p)] = dense.get(int(p), 0) + 1
+    pos = np.array(sorted(dense), np.uint32)
+    return pos, np.array([[dense[int(p)]] for p in pos], np.uint32)
+
+
+def _kurtosis(x, w):
+    xb = (w * x).sum() / w.sum()
+    return (w.sum() - 1) * (w * (x - xb) ** 4).sum() / ((w * (x - xb) ** 2).sum() ** 2)
+
+
+@pytest.mark.parametrize("block", Q8_BLOCKS, ids=lambda b: f"n{b[1]}_c{b[2]}")
+def test_q8_oracle_wraps_position_index(oracle, block):
+    """the oracle's kurtosis of a > 65,536-position region equals an
+    independent numpy restatement of data.cpp:133-182 with the UShort index
+    and the uint32 sum, and differs from the unwrapped moment (the wrap is
+    live in these fixtures)"""
+    pos, cnt = q8_unit(*block)
+    ref, _ = oracle.run_unit(50, 0.003, pos, cnt, kurt_thr=0.0)
+    big = ref[(ref["right"] - ref["left"] + 1) > 65_536]
+    assert len(big) == 1
+    left, right = int(big["left"][0]), int(big["right"][0])
+    m = (pos >= left) & (pos <= right)
+    off = (pos[m] - left).astype(np.uint64)
+    c = cnt[m, 0].astype(np.uint64)
+    w = c.astype(np.float64)
+    # UShort pos (data.cpp:137), HitCount sum += posCount * pos (uint32)
+    xs = off % 65_536
+    s32 = int(((c * xs) % 2**32).sum() % 2**32)
+    xb = s32 / float(c.sum())
+    d = xs.astype(np.float64) - xb
+    k_wrap = (w.sum() - 1) * (w * (d * d) ** 2).sum() / ((w * d * d).sum() ** 2)
+    assert abs(big["kurtosis"][0] - k_wrap) <= 1e-9 * abs(k_wrap)
+    k_true = _kurtosis(off.astype(np.float64), w)
+    assert abs(big["kurtosis"][0] - k_true) > 1e-3 * abs(k_true)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("block", Q8_BLOCKS, ids=lambda b: f"n{b[1]}_c{b[2]}")
+def test_q8_long_region_unit(gpu_lib, oracle, block):
+    from tests.test_gpu_unit import compare, run_gpu
+    pos, cnt = q8_unit(*block)
+    length, bw, bg = 300_000, 50, 0.003
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, kurt_thr=0.0)
+    assert ((ref["right"] - ref["left"] + 1) > 65_536).any()
+    regs, gcnt, f, r, _ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, kurt_thr=0.0)
+    compare(ref, ref_sums, regs, gcnt)
+    # kurtosis filter on (-k 50 decides on the wrapped value)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, kurt_thr=50.0)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, kurt_thr=50.0)
+    compare(ref, ref_sums, regs, gcnt)
+
+
+@pytest.mark.gpu
+def test_q8_long_region_cli(orc_bin, gpu_lib, tmp_path):
+    """F3: a region table holding regions longer than 65,536 positions on
+    both strands, byte-identical (kurtosis column printed %.2f)"""
+    write_contigs(tmp_path / "ct.txt", [("chrL", 400_000), ("chrS", 90_000)])
+    f1, _ = q8_unit(10_000, 70_000, 1, 1, 400_000, 1)
+    r1, rc = q8_unit(150_000, 140_000, 7, 1, 400_000, 2)
+    f2, fc2 = q8_unit(3_000, 80_000, 2, 1, 90_000, 3)
+    fwd = {"chrL": [(int(p), 1) for p in f1], "chrS": [(int(p), int(c)) for p, c in zip(f2, fc2[:, 0])]}
+    rev = {"chrL": [(int(p), int(c)) for p, c in zip(r1, rc[:, 0])]}
+    write_wig(tmp_path / "s.wig", "s", fwd, rev)
+    out = _both(orc_bin, tmp_path, "regions", ["-q", "-f", "-m", "3000000", "-c", "ct.txt", "s.wig"])
+    spans = []
+    for line in out.splitlines():
+        m = re.match(r"^\w+:(\d+)-(\d+)\t", line)
+        if m:
+            spans.append(abs(int(m.group(2)) - int(m.group(1))) + 1)
+    assert sum(s > 65_536 for s in spans) == 3
+
+
+# ---- Q10 --------------------------------------------------------------------
+
+def _prefixed_table():
+    rows = []
+    for t in ("hg19", "mm9"):
+        for line in open(os.path.join(ROOT, "unipeak_amd", "data", f"{t}.txt")):
+            f = line.split()
+            if len(f) >= 2:
+                rows.append((f"{t}_{f[0]}", int(f[1])))
+    return rows
+
+
+def _q10_inputs(tmp_path):
+    from tests.test_cli import gen_sample
+    contigs = _prefixed_table()
+    assert sum(L for _, L in contigs) == 5_750_605_500
+    write_contigs(tmp_path / "ct.txt", contigs)
+    rng = np.random.default_rng(10)
+    sub = [("hg19_chr21", 200_000), ("mm9_chrY", 150_000), ("hg19_chrM", 16_571)]
+    fwd, rev = gen_sample(rng, sub)
+    return write_wig(tmp_path / "s.wig", "s", fwd, rev)
+
+
+def _check_q10_background(text, tags):
+    hdr = dict(l[2:].split("=", 1) for l in text.splitlines() if l.startswith("# ") and "=" in l)
+    # uint32 genome size: 5,750,605,500 mod 2^32; directional: per strand;
+    # printed through a stringstream (6 significant digits, Q14)
+    assert hdr["background"] == "%g" % (tags / 1_455_638_204 / 2)
+    assert hdr["background"] != "%g" % (tags / 5_750_605_500 / 2)
+
+
+def test_q10_oracle_wraps_genome_size(orc_bin, tmp_path):
+    tags = _q10_inputs(tmp_path)
+    _run([orc_bin, "regions", "-q", "-f", "-c", "ct.txt", "-o", "r.txt", "s.wig"], tmp_path)
+    text = (tmp_path / "r.txt").read_text()
+    _check_q10_background(text, tags)
+    assert any(l.startswith("hg19_chr21:") for l in text.splitlines())
+
+
+@pytest.mark.gpu
+def test_q10_hg19mm9_table_cli(orc_bin, gpu_lib, tmp_path):
+    """the prefixed 47-contig hg19+mm9 table through bin/regions"""
+    tags = _q10_inputs(tmp_path)
+    out = _both(orc_bin, tmp_path, "regions", ["-q", "-f", "-c", "ct.txt", "s.wig"])
+    _check_q10_background(out, tags)
+    rows = [l for l in out.splitlines() if l and not l.startswith(("#", "\t"))]
+    assert {r.split(":")[0] for r in rows} >= {"hg19_chr21", "mm9_chrY"}
+
+
+# ---- Q14 --------------------------------------------------------------------
+
+SURVEY_Q14 = "# corr_threshold=0.29999999999999999"  # SURVEY.md Appendix A Q14, recorded
+
+
+def _q14_input(tmp_path):
+    write_contigs(tmp_path / "ct.txt", [("chrA", 10000)])
+    write_wig(tmp_path / "s.wig", "s", {"chrA": [(1000, 10), (1010, 5)]}, {"chrA": [(4000, 9)]})
+
+
+def test_q14_oracle_header_string(orc_bin, tmp_path):
+    """-u is only used (and printed as given) with -D; regions.cpp:105-106
+    prints -1 otherwise"""
+    _q14_input(tmp_path)
+    _run([orc_bin, "regions", "-q", "-D", "-c", "ct.txt", "-o", "o.txt", "s.wig"], tmp_path)
+    assert SURVEY_Q14 in (tmp_path / "o.txt").read_text().splitlines()
+    _run([orc_bin, "regions", "-q", "-c", "ct.txt", "-o", "d.txt", "s.wig"], tmp_path)
+    assert "# corr_threshold=-1" in (tmp_path / "d.txt").read_text().splitlines()
+
+
+@pytest.mark.gpu
+def test_q14_bin_header_string(gpu_lib, tmp_path):
+    _q14_input(tmp_path)
+    _run([os.path.join(BIN, "regions"), "-q", "-D", "-c", "ct.txt", "-o", "o.txt", "s.wig"], tmp_path)
+    hdr, col, _ = parse_table(tmp_path / "o.txt")
+    assert SURVEY_Q14 in hdr
+
+
+# ---- Q15 --------------------------------------------------------------------
+
+Q15_SHIFTS = [int(x) for x in np.random.default_rng(3).permutation(np.arange(25, 56))]
+
+
+def _q15_input(tmp_path):
+    """31 clusters with identical tag content (equal Region::sum()) and
+    distinct strand shifts 25..55 (so the shift histogram names the tested
+    ones), plus 5 heavier clusters that sort first; -g 12 cuts through the
+    tie group"""
+    f, r = [], []
+    c = 2000
+    for s in Q15_SHIFTS:
+        for j in range(-20, 20):
+            f.append((c + j, 3))
+            r.append((c + 2 * s + j, 3))
+        c += 5000
+    for _ in range(5):
+        for j in range(-20, 20):
+            f.append((c + j, 6))
+            r.append((c + 80 + j, 6))
+        c += 5000
+    write_contigs(tmp_path / "ct.txt", [("c1", c + 5000)])
+    write_wig(tmp_path / "s.wig", "s", {"c1": sorted(f)}, {"c1": sorted(r)})
+    return ["-c", "ct.txt", "-x", "80", "-n", "5", "-u", "-1", "-g", "12", "-m", "3000000", "s.wig"]
+
+
+def _hist(text):
+    rows = text.split("\n\n", 1)[1].strip().splitlines()[1:]
+    return {int(a): int(b) for a, b in (l.split("\t") for l in rows)}
+
+
+def test_q15_oracle_tie_order_is_introsort(orc_bin, tmp_path):
+    """the 7 equal-sum regions tested are not the first 7 in input order (a
+    stable sort's choice): the restated introsort decides, as libstdc++'s
+    std::sort does in the reference"""
+    args = _q15_input(tmp_path)
+    _run([orc_bin, "strand_shift"] + args + ["-o", "o.txt"], tmp_path)
+    h = _hist((tmp_path / "o.txt").read_text())
+    assert h.pop(40) == 5  # the heavy clusters
+    assert sum(h.values()) == 7 and all(v == 1 for v in h.values())
+    assert set(h) <= set(Q15_SHIFTS)
+    assert set(h) != set(Q15_SHIFTS[:7])
+
+
+@pytest.mark.gpu
+def test_q15_strand_shift_ties_cli(orc_bin, gpu_lib, tmp_path):
+    args = _q15_input(tmp_path)
+    out = _both(orc_bin, tmp_path, "strand_shift", args)
+    assert sum(_hist(out).values()) == 12
+
+
+# ---- scatter contract ---------------------------------------------------------
+
+@pytest.mark.gpu
+def test_scatter_rejects_duplicate_positions(gpu_lib):
+    """4-bit tracks: one call writing a position twice would OR two counts
+    into one nibble -- the library refuses such a call"""
+    with gpu_lib.Lib(0) as g:
+        g.set_params(50, 1, 0.003)
+        u = g.add_unit(10_000)
+        g.scatter(u, 0, 0, np.array([300, 100, 200], np.uint32), np.array([3, 20, 1], np.uint32))
+        with pytest.raises(gpu_lib.UpError) as e:
+            g.scatter(u, 0, 0, np.array([500, 100, 500], np.uint32), np.array([20, 3, 1], np.uint32))
+        assert e.value.code == -1
+        f, _ = g.profile(u, 10_000)
+        g.scatter(u, 0, 0, np.array([100], np.uint32), np.array([0], np.uint32))  # clears
+        assert g.tag_total(u, 0, 0) == 4

@@ -180,6 +180,8 @@ struct up_ctx {
         uint8_t *req_target = nullptr;
         void *req_target_hostp = nullptr;
         uint64_t req_target_cap = 0, req_last_nreg = 0;
+        uint64_t req_reg_cap = 0;    // record / overflow capacities: the caller's thread
+        uint32_t req_ovf_cap = 0;    // grows them, the launcher thread only reads these
         int req_tl = 0;
         bool lpending = false;       // queued for / being launched by the launcher thread
         int lrc = 0;                 // its launch result
@@ -641,8 +643,17 @@ int up_unit_scatter(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, s
     if (n == 0) return UP_OK;
     if (!pos || !counts) return UP_E_ARG;
     const uint32_t len = c->units[unit].len;
-    for (size_t i = 0; i < n; ++i)
+    bool ascending = true;
+    for (size_t i = 0; i < n; ++i) {
         if (pos[i] == 0 || pos[i] > len) return UP_E_ARG;
+        if (i && pos[i] <= pos[i - 1]) ascending = false;
+    }
+    if (!ascending) {  // positions must be unique: a nibble written twice in
+                       // one call would OR two counts together (4-bit tracks)
+        std::vector<uint32_t> sp(pos, pos + n);
+        std::sort(sp.begin(), sp.end());
+        if (std::adjacent_find(sp.begin(), sp.end()) != sp.end()) return UP_E_ARG;
+    }
     HIPCHK(hipSetDevice(c->dev));
     {   // escapes: the host map holds every count >= kEsc of the track
         Unit &u = c->units[unit];
@@ -861,7 +872,7 @@ static int pool_mode(const up_ctx *c) {
     return c->nc.size() == 1 ? 0 : 1;
 }
 
-static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps) {
+static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps, uint32_t ovf_cap) {
     ScanParams P{};
     P.units = c->d_units.p;
     P.nunits = (uint32_t)c->units.size();
@@ -881,7 +892,7 @@ static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps) {
     P.rec = ps.d_rec.p;
     P.ovf_count = ps.d_ovf_count.p;
     P.ovf_rec = ps.d_ovf_rec.p;
-    P.ovf_cap = c->ovf_cap;
+    P.ovf_cap = ovf_cap;
     P.xlist = ps.d_xlist.p;
     P.xwcount = ps.d_xwcount.p;
     P.xref = ps.d_xref.p;
@@ -1308,7 +1319,7 @@ static int enqueue_rest(up_ctx *c, int slot, const ScanParams &SP, const StatPar
     if (int r = launch_seg_count_head(c, slot)) return r;
     hipLaunchKernelGGL(seg_compact_kernel, dim3(nsb), dim3(kSegBlock), 0, ps.stream, c->d_units.p,
                        (uint32_t)c->units.size(), ps.d_info.p, ps.d_cnt.p, ps.d_bsum.p, ps.d_rec.p,
-                       ps.d_ovf_rec.p, c->ovf_cap, ps.d_starts.p, ps.d_ends.p, ps.d_runit.p, ps.d_peak_pos.p,
+                       ps.d_ovf_rec.p, ps.ovf_cap, ps.d_starts.p, ps.d_ends.p, ps.d_runit.p, ps.d_peak_pos.p,
                        ps.d_peak_val.p, ns, (uint64_t)cap, ps.d_ovf_count.p, ps.d_xcount.p, ps.d_nreg.p,
                        c->hp_status[slot].dev, thdr);
     HIPCHK(hipGetLastError());
@@ -1344,8 +1355,12 @@ static int launch_pass(up_ctx *c, int slot) {
     if (!ps.d_xcount.p || !ps.d_ovf_count.p) ps.counters_armed = false;
     HIPCHK(ps.d_xcount.ensure(2));  // front / back ends of the work list
     HIPCHK(ps.d_ovf_count.ensure(1));
-    const uint64_t cap = c->reg_cap;
-    HIPCHK(ps.d_ovf_rec.ensure((size_t)c->ovf_cap * kOvfStride));
+    // every per-pass decision reads the request snapshot (ps.req_*), never
+    // the live context: the caller may change the record target or grow the
+    // capacities while this pass waits for the launcher thread
+    const uint64_t cap = ps.req_reg_cap;
+    const uint32_t ovf_cap = ps.req_ovf_cap;
+    HIPCHK(ps.d_ovf_rec.ensure((size_t)ovf_cap * kOvfStride));
     HIPCHK(ps.d_peak_pos.ensure(cap + 1));
     HIPCHK(ps.d_peak_val.ensure(cap + 1));
     HIPCHK(ps.d_starts.ensure(cap + 1));
@@ -1358,7 +1373,7 @@ static int launch_pass(up_ctx *c, int slot) {
     const bool corr = c->p.nondir && (c->p.want_corr || c->p.corr_thr > -1);
     const uint32_t corr_cap = 1024;
     if (corr) HIPCHK(ps.d_corr.ensure((size_t)(c->ncu > 0 ? c->ncu : 256) * 8 * 4 * corr_cap * 2));
-    if (!c->target) {
+    if (!ps.req_target) {
         HIPCHK(c->hp_regions[slot].ensure(cap + 1));
         HIPCHK(c->hp_counts[slot].ensure((cap + 1) * S));
     }
@@ -1366,7 +1381,7 @@ static int launch_pass(up_ctx *c, int slot) {
     ps.target_hostp = ps.req_target_hostp;
     ps.target_cap = ps.req_target_cap;
     ps.cap = cap;
-    ps.ovf_cap = c->ovf_cap;
+    ps.ovf_cap = ovf_cap;
     // the pass follows everything enqueued on the context stream (track
     // writes), and its K1a follows the K1a of the previous pass if that one
     // is in flight: one streaming K1a at a time, earlier passes' K1b/K2/K3
@@ -1385,7 +1400,7 @@ static int launch_pass(up_ctx *c, int slot) {
         HIPCHK(hipMemsetAsync(ps.d_ovf_count.p, 0, sizeof(uint32_t), s1));
         HIPCHK(hipMemsetAsync(ps.d_xcount.p, 0, 2 * sizeof(uint32_t), s1));
     }
-    ScanParams SP = scan_params(c, ps);
+    ScanParams SP = scan_params(c, ps, ovf_cap);
     // K1x..K3 as a captured graph only when the caller's thread launches:
     // capturing on the launcher thread while the caller waits on earlier
     // passes invalidated captures (hipErrorStreamCaptureInvalidated, ROCm
@@ -1445,7 +1460,7 @@ static int launch_pass(up_ctx *c, int slot) {
     key_add(key, kx);
     key_add(key, std::max<uint64_t>(ps.req_last_nreg, 1024));
     key_add(key, (uint32_t)c->units.size());
-    key_add(key, c->ovf_cap);
+    key_add(key, ovf_cap);
     key_add(key, pool_mode(c));
     key_add(key, c->p.nondir);
     key_add(key, c->nc.size());
@@ -1545,6 +1560,8 @@ int up_run_async(up_ctx *c) {
     ps.req_target_cap = c->target_cap;
     ps.req_tl = c->timing;
     ps.req_last_nreg = c->last_nreg;
+    ps.req_reg_cap = c->reg_cap;
+    ps.req_ovf_cap = c->ovf_cap;
     if (c->use_launcher) {
         if (!c->launcher.joinable()) c->launcher = std::thread(launcher_main, c);
         {
@@ -1624,7 +1641,9 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
         // the launch state)
         launcher_drain(c);
         if (hipDeviceSynchronize() != hipSuccess) return fail(UP_E_HIP);
-        int r = launch_pass(c, slot);  // same record target and timing (ps.req_*)
+        ps.req_reg_cap = c->reg_cap;   // the grown areas; same record target and timing
+        ps.req_ovf_cap = c->ovf_cap;
+        int r = launch_pass(c, slot);
         if (r) return fail(r);
         if (hipEventSynchronize(ps.done) != hipSuccess) return fail(UP_E_HIP);
     }
@@ -1777,7 +1796,9 @@ int up_host_register(up_ctx *c, void *ptr, uint64_t bytes) {
 int up_regions_view(up_ctx *c, const up_region **regions, const uint32_t **counts, uint64_t *n) {
     if (!c || !regions || !n) return UP_E_ARG;
     if (!c->ran) return UP_E_STATE;
-    if (c->target && !c->host_regions) return UP_E_STATE;  // records went to the device buffer
+    // the completed pass's own delivery decides (the caller may already have
+    // set another target for passes launched after it)
+    if (!c->host_regions && c->pass[c->cur_slot].target) return UP_E_STATE;  // records went to the target
     *n = c->nreg;
     if (c->host_regions) {
         *regions = c->h_regions.data();
@@ -1892,7 +1913,7 @@ int up_unit_profile_range(up_ctx *c, uint32_t unit, uint64_t first, uint32_t cou
     double *d = nullptr;
     HIPCHK(hipMalloc(&d, 2 * (size_t)count * sizeof(double) + 16));
     HIPCHK(hipMemsetAsync(d, 0, 2 * (size_t)count * sizeof(double), c->stream));
-    ScanParams P = scan_params(c, c->pass[0]);  // no pass in flight; records unused
+    ScanParams P = scan_params(c, c->pass[0], c->ovf_cap);  // no pass in flight; records unused
     P.prof_f = d;
     P.prof_r = d + count;
     P.prof_first = (int64_t)first;
