@@ -121,7 +121,7 @@ def test_q8_long_region_cli(orc_bin, gpu_lib, tmp_path):
     fwd = {"chrL": [(int(p), 1) for p in f1], "chrS": [(int(p), int(c)) for p, c in zip(f2, fc2[:, 0])]}
     rev = {"chrL": [(int(p), int(c)) for p, c in zip(r1, rc[:, 0])]}
     write_wig(tmp_path / "s.wig", "s", fwd, rev)
-    out = _both(orc_bin, tmp_path, "regions", ["-q", "-f", "-m", "3000000", "-c", "ct.txt", "s.wig"])
+    out = _both(orc_bin, tmp_path, "regions", ["-q", "-f", "-m", "3000000000", "-c", "ct.txt", "s.wig"])
     spans = []
     for line in out.splitlines():
         m = re.match(r"^\w+:(\d+)-(\d+)\t", line)
