@@ -10,6 +10,7 @@ resident in HBM before timing.  Other BASELINE configs are available with
 
   hg19-dir1    configs[1]  1 directional sample                      (default)
   hg19-nondir1 configs[2]  regions pass of C3: -D -y, 1 sample, both strands
+  hg19-shift   configs[2]  the whole C3 pipeline: strand_shift, then regions -D -y -s <best>
   hg19-8s1c    configs[3]  8 samples + 1 negative control (-e 9), directional
   hg19mm9-32s  configs[4]  hg19+mm9, 32 samples, -D -k 50 -u 0.3 -y (8 GPUs)
 
@@ -62,6 +63,11 @@ WORKLOADS = {
                       want_corr=False, baseline="configs[3]",
                       desc="hg19, 8 pooled directional samples + 1 negative control (-e 9), bw 50, "
                            "-r 25 -k 50 -t 10 (BASELINE configs[3])"),
+    "hg19-shift": dict(tables=["hg19"], nondir=True, samples=1, controls=0, kurt=50.0, corr=0.3,
+                       want_corr=True, baseline="configs[2]", shift_pipeline=True,
+                       desc="hg19, 1 nondirectional sample, the whole configs[2] pipeline per step: "
+                            "strand_shift (KDE pass, sort by sum, strandCorr(0..150) table, shift "
+                            "histogram) then regions -D -y -s <best> (BASELINE configs[2])"),
     "hg19mm9-32s": dict(tables=["hg19", "mm9"], nondir=True, samples=32, controls=0, kurt=50.0,
                         corr=0.3, want_corr=True, baseline="configs[4]",
                         desc="hg19+mm9 (names prefixed), 32 nondirectional samples, -D -k 50 -u 0.3 -y, "
@@ -113,6 +119,8 @@ def main():
     args = ap.parse_args()
     W = WORKLOADS[args.workload]
 
+    if W.get("shift_pipeline"):
+        return shift_pipeline(args, W)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -481,8 +489,22 @@ def main():
                          "frac_of_copy_rate": round(achieved / copy_gbps, 4)},
             "setup_s": round(gen_s, 2),
         }
+        # SURVEY §8(d)'s pricing: one uint32 count per bp per strand per
+        # non-control sample (8 * S_nc B/bp over both strands), beside the
+        # 4-bit layout's algorithmic bytes the kernel actually reads
+        survey_bytes = sum(lens[units[k][0]] * nstr * s_nc for k in mine_all[0]) * 4 if world == 1 else None
+        rf = res["roofline"]
+        rf["frac_step"] = round(alg_bytes / dt / 1e9 / HBM_PEAK_GBS, 4)  # whole pass at the step rate
+        rf["step_note"] = ("frac_step = K1a's algorithmic bytes / ms_per_step (the whole step: K1a plus the "
+                           "exact, segmentation and statistics kernels it overlaps, and rank 0's record read)")
+        if survey_bytes:
+            rf["bytes_rule_survey"] = "8 * S_nc B/bp (SURVEY 8(d): uint32 counts, both strands)"
+            rf["bytes_per_launch_survey"] = int(survey_bytes)
+            rf["frac_survey_rule"] = round(survey_bytes / (k1a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            rf["survey_rule_note"] = ("above 1: the kernel does not read SURVEY's uint32 bytes -- the tracks are "
+                                      "4-bit counts with an exact overflow table (DESIGN.md §3)")
         if world == 1 and not args.no_cpu_baseline and args.workload == "hg19-dir1":
-            res["cpu_baseline"] = cpu_baseline(contigs, args, value)
+            res["cpu_baseline"] = cpu_baseline(contigs, args, value, bg_set[0], last[1])
         print(json.dumps(res), flush=True)
     g.set_record_target(0, 0)
     g.close()
@@ -497,9 +519,149 @@ def main():
         comm.dist.destroy_process_group()
 
 
-def cpu_baseline(contigs, args, gpu_value):
-    """Oracle (plain-C restatement of ProfileBuffer) on 1 core over a bounded
-    sample of the same synthetic genome, hot path only (hits pre-parsed)."""
+def shift_pipeline(args, W):
+    """configs[2] end to end on the device-resident genome, one step =
+      strand_shift (src/strand_shift.cpp:133-259): one nondirectional pass
+        (corr off, unscaled -t, Q13), the regions sorted by Region::sum()
+        descending, strandCorr(0..150) of every region longer than 303
+        positions (K4, up_shift_scan), the first 1000 with corr >= -u into
+        the shift histogram, smoothed with Kernel(5), argmax over
+        [minShift, maxShift+1-5);
+      regions -D -y -s <best> (src/regions.cpp): one nondirectional pass
+        over the tracks moved by the shift (forward +s, reverse -s, as the
+        wiggle reader applies -s), strand correlation per region.
+    Tracks of both passes are resident before timing (two contexts: the
+    -s tracks are the spec's tracks moved by the shift the first pass
+    finds, 75 for this generator; checked every step).  N = 1 only.
+    The host sort is numpy's stable argsort (the CLI's std::sort order of
+    equal sums, quirk Q15, only changes which tie is tested; tests cover it)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        raise SystemExit("hg19-shift runs on one GPU")
+    contigs = load_table(W["tables"])
+    genome = sum(L for _, L in contigs)
+    mappable = genome & 0xFFFFFFFF
+    lens = [L for _, L in contigs]
+    bw, max_shift, min_shift, n_test, u_thr = args.bw, 150, 25, 1000, 0.3
+    shift = 75  # the generator's strand shift (DESIGN.md §8); verified below
+    ctx = []
+    for off in (0, shift):
+        g = capi.Lib(0)
+        g.set_params(bw, 1, 0.0029, nondir=True)
+        tags = 0
+        for ci, L in enumerate(lens):
+            u = g.add_unit(L)
+            for st in (0, 1):
+                g.synth(u, st, 0, args.seed, ci, st, nondir=True, peaks=True,
+                        offset=(off if st == 0 else -off))
+                tags += g.tag_total(u, st, 0)
+        ctx.append((g, tags))
+    (ga, tags_a), (gb, tags_b) = ctx
+    # strand_shift.cpp:131-142: background per position over both strands,
+    # corr off, -t not scaled by the sample count (Q13)
+    ga.set_params(bw, 1, tags_a / mappable, region_thr=25.0, kurt_thr=W["kurt"], corr_thr=-1.0,
+                  hit_thr=10.0, nondir=True)
+    gb.set_params(bw, 1, tags_b / mappable, region_thr=25.0, kurt_thr=W["kurt"], corr_thr=W["corr"],
+                  hit_thr=10.0, nondir=True, want_corr=True)
+    mk = capi.kernel_weights(5, 1.0)
+    ph = {k: 0.0 for k in ("shift_pass", "sort_select", "shift_scan", "histogram", "regions_pass",
+                           "shift_pass_up_run", "regions_pass_up_run")}
+    info = {}
+
+    def step(timed):
+        t0 = time.perf_counter()
+        n = ga.run()
+        tr = time.perf_counter()
+        regs, _ = ga.regions_view()
+        t1 = time.perf_counter()
+        order = np.argsort(-regs["sum"].astype(np.int64), kind="stable")
+        span = (regs["right"].astype(np.int64) - regs["left"] + 1)[order]
+        elig = order[span > 2 * max_shift + 3]
+        t2 = time.perf_counter()
+        table = ga.shift_scan(elig, max_shift)
+        t3 = time.perf_counter()
+        # strand_shift.cpp:205-228: first maximum from bestCorr = -1 (NaN
+        # never wins), the first n_test qualifying regions
+        tb = np.concatenate([np.full((len(table), 1), -1.0),
+                             np.where(np.isnan(table), -np.inf, table)], axis=1)
+        arg = np.argmax(tb, axis=1)                # 0: no corr above -1
+        bcorr = tb[np.arange(len(tb)), arg]
+        best = np.maximum(arg - 1, 0)
+        ok = np.flatnonzero(bcorr >= u_thr)[:n_test]
+        freq = np.bincount(best[ok], minlength=max_shift + 1).astype(np.float64)
+        # strand_shift.cpp:241-248: dens[i - 5 + j] += freq[i] * k5[j]; every
+        # dens[k] receives its terms in ascending i, as in the reference loop
+        dens = np.zeros(max_shift + 1)
+        for d in range(-5, 6):
+            lo, hi = max(0, -d), min(max_shift + 1, max_shift + 1 - d)
+            dens[lo:hi] += freq[lo + d:hi + d] * mk[5 - d]
+        cand = dens[min_shift:max_shift + 1 - 5]
+        bs = int(min_shift + np.argmax(cand)) if cand.max() > 0 else 0
+        t4 = time.perf_counter()
+        if bs != shift:
+            raise SystemExit(f"strand_shift found {bs}, the -s tracks were moved by {shift}")
+        t4b = time.perf_counter()
+        nb = gb.run()
+        t4c = time.perf_counter()
+        regs_b, _ = gb.regions_view()
+        acc = int(np.count_nonzero(regs_b["accepted"]))
+        t5 = time.perf_counter()
+        if timed:
+            for k, v in zip(ph, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, tr - t0, t4c - t4b)):
+                ph[k] += v
+        info.update(shift_candidates=int(n), eligible=int(len(elig)), tested=int(len(ok)), best_shift=bs,
+                    regions_candidates=int(nb), regions_accepted=acc)
+
+    for g, _ in ctx:
+        g.set_timing(1)
+    for _ in range(args.warmup):
+        step(False)
+    ka = []
+    kb = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+        ka.append(ga.timings()[0])
+        kb.append(gb.timings()[0])
+    dt = (time.perf_counter() - t0) / args.steps
+    alg = genome  # K1a of each pass: both strands x 0.5 B per bp
+    k1a = float(np.mean(ka + kb))
+    res = {
+        "metric": METRIC, "value": round(genome / dt / 1e9, 3), "unit": "Gbp/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (device-generated hg19-shaped tag counts, DESIGN.md §8)",
+        "config": {"workload": W["desc"], "baseline_config": W["baseline"], "genome_bp": genome,
+                   "units": len(lens), "samples": 1, "parallelism": "one GPU"},
+        "pipeline": info,
+        "phases_ms": {k: round(v / args.steps * 1e3, 4) for k, v in ph.items()},
+        "roofline": {"bound": "hbm", "achieved": round(alg / (k1a * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(alg / (k1a * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": None, "kernel": "scan_kernel<..., kModeScreen> (K1a), both passes",
+                     "kernel_ms": round(k1a, 4), "bytes_per_launch": int(alg),
+                     "bytes_rule": "0.5 B (4-bit count) per bp per strand, both strands"},
+    }
+    print(json.dumps(res), flush=True)
+    for g, _ in ctx:
+        g.close()
+
+
+def cpu_baseline(contigs, args, gpu_value, background, gpu_regions):
+    """The oracle (plain-C restatement of ProfileBuffer, oracle/) on the host
+    cores, over the same synthetic genome with the GPU pass's background:
+      value      1 core, hot path only (hits pre-generated, untimed), the
+                 reference's own single-threaded mode (README:60-61);
+      all_cores  the reference's contig-subset method (README:37): every
+                 (contig, strand) unit on its own buffer, P threads;
+      end_to_end the oracle CLI restatement of bin/regions on the synthetic
+                 genome written as a wiggle file, beside this build's
+                 bin/regions on the same file (tables compared).
+    The candidate / accepted counts of the 1-core run are checked against
+    the GPU pass's."""
+    import shutil
+    import subprocess
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
     from tests.oracle_binding import Oracle
     orc = Oracle()
     names = [n for n, _ in contigs] if args.cpu_sample == "all" else args.cpu_sample.split(",")
@@ -509,16 +671,68 @@ def cpu_baseline(contigs, args, gpu_value):
     lens = np.zeros(max(idx) + 1, np.uint32)
     for i in idx:
         lens[i] = contigs[i][1]
-    genome = sum(L for _, L in contigs)
-    bg = 22_600_000 / genome / 2  # fixed (hot path cost does not depend on it)
-    npass, nrej, sec = orc.baseline(lens, args.seed, args.bw, 25.0, 50.0, 10.0, bg)
+    npass, nrej, sec = orc.baseline(lens, args.seed, args.bw, 25.0, 50.0, 10.0, background)
     bp = int(lens.sum())
-    return {"value": round(bp / sec / 1e9, 4), "unit": "Gbp/s", "cores": 1, "kind": "port",
-            "seconds": round(sec, 2),
-            "sample": f"hg19 {'full genome' if args.cpu_sample == 'all' else args.cpu_sample} synthetic, "
-                      f"directional, 1 sample, both strands ({bp} bp), oracle ProfileBuffer restatement, "
-                      f"hits pre-parsed",
-            "gpu_over_cpu": round(gpu_value / (bp / sec / 1e9), 1)}
+    out = {"value": round(bp / sec / 1e9, 4), "unit": "Gbp/s", "cores": 1, "kind": "port",
+           "seconds": round(sec, 2),
+           "sample": f"hg19 {'full genome' if args.cpu_sample == 'all' else args.cpu_sample} synthetic, "
+                     f"directional, 1 sample, both strands ({bp} bp), oracle ProfileBuffer restatement, "
+                     f"hits pre-parsed, same background as the GPU pass",
+           "gpu_over_cpu": round(gpu_value / (bp / sec / 1e9), 1)}
+    if args.cpu_sample == "all":
+        out["regions_match_gpu"] = bool(npass + nrej == gpu_regions[0] and npass == gpu_regions[1])
+        out["regions"] = {"candidates": int(npass + nrej), "accepted": int(npass)}
+    # all cores: the box's CPU share (sched affinity; at most 16 per GPU)
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    P = max(1, min(16, ncpu))
+    jobs = sorted(((int(lens[c]), c, st) for c in idx for st in (0, 1)), reverse=True)
+    with ThreadPoolExecutor(P) as ex:  # ctypes releases the GIL; generation untimed
+        hits = list(ex.map(lambda j: orc.synth_track(args.seed, j[1], j[2], False, j[0], args.bw, True),
+                           jobs))
+        t0 = time.perf_counter()
+        rs = list(ex.map(lambda a: orc.baseline_unit(a[1][0], a[1][1], a[0][1], a[0][2], args.bw, 25.0,
+                                                     50.0, 10.0, background), zip(jobs, hits)))
+        wall = time.perf_counter() - t0
+    del hits
+    out["all_cores"] = {"value": round(bp / wall / 1e9, 4), "unit": "Gbp/s", "cores": P,
+                        "host_cpus_visible": ncpu, "wall_s": round(wall, 3),
+                        "regions": {"candidates": int(sum(a + b for a, b in rs)),
+                                    "accepted": int(sum(a for a, _ in rs))},
+                        "note": "(contig, strand) units on P threads, largest first; hits pre-generated"}
+    if args.cpu_sample != "all" or os.environ.get("UNIPEAK_BENCH_E2E", "1") == "0":
+        return out
+    # end to end through the CLIs on the same synthetic genome
+    from tests.make_wig import write_sample
+    d = tempfile.mkdtemp(prefix="unipeak_e2e_", dir="/tmp")
+    try:
+        with open(os.path.join(d, "contigs.txt"), "w") as f:
+            for n, L in contigs:
+                f.write(f"{n}\t{L}\n")
+        write_sample(os.path.join(d, "s0.wig"), "s0", orc, contigs, args.seed, False, True, args.bw,
+                     workers=P)
+        e2e = {}
+        for tag, exe in (("oracle_cli", [os.path.join(ROOT, "oracle", "_build", "orc"), "regions"]),
+                         ("bin_regions", [os.path.join(ROOT, "bin", "regions")])):
+            t0 = time.perf_counter()
+            r = subprocess.run(exe + ["-q", "-f", "-c", "contigs.txt", "-o", f"{tag}.txt", "s0.wig"],
+                               cwd=d, capture_output=True, timeout=300)
+            e2e[tag + "_s"] = round(time.perf_counter() - t0, 3)
+            if r.returncode != 0:
+                e2e[tag + "_error"] = r.stderr.decode()[-300:]
+        e2e["oracle_cli_gbps"] = round(bp / e2e["oracle_cli_s"] / 1e9, 4)
+        e2e["bin_regions_gbps"] = round(bp / e2e["bin_regions_s"] / 1e9, 4)
+        a, b = (os.path.join(d, f"{t}.txt") for t in ("oracle_cli", "bin_regions"))
+        e2e["tables_identical"] = bool(os.path.exists(a) and os.path.exists(b) and
+                                       open(a, "rb").read() == open(b, "rb").read())
+        e2e["note"] = ("wall time of each CLI process on the synthetic hg19 wiggle file (parse + hot path + "
+                       "write; bin/regions includes HIP initialisation); oracle_cli is 1 core")
+        out["end_to_end"] = e2e
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return out
 
 
 if __name__ == "__main__":

@@ -133,6 +133,13 @@ int up_unit_scatter(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
 int up_unit_synth(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
                   uint64_t seed, uint32_t contig_index, int32_t synth_strand,
                   int32_t nondir, int32_t with_peaks);
+/* the same track moved by `offset` positions, as the wiggle reader's -s
+ * shift moves it (forward strand +s, reverse -s, misc/format.cpp:693-705):
+ * position p holds the spec's count at p - offset; counts that leave
+ * [1, contig_len] are dropped */
+int up_unit_synth_offset(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
+                         uint64_t seed, uint32_t contig_index, int32_t synth_strand,
+                         int32_t nondir, int32_t with_peaks, int32_t offset);
 /* total tags of one track (sum of its counts, uint64) */
 int up_unit_tag_total(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
                       uint64_t *total);

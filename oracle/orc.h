@@ -131,12 +131,13 @@ int orc_baseline_run(uint32_t n_contigs, const uint32_t *lens, uint64_t seed,
                      double hit_thr, double background, uint64_t *n_pass,
                      uint64_t *n_reject, double *seconds);
 
-/* one (contig, strand) unit of the same baseline on its own buffer (units
- * are independent after a flush; callers run them on several threads) */
-int orc_baseline_unit(uint32_t len, uint32_t contig, int strand, uint64_t seed,
-                      uint16_t bw, double region_thr, double kurt_thr,
+/* one (contig, strand) unit of the same baseline on its own buffer over
+ * pre-generated hits (units are independent after a flush; callers run
+ * them on several threads) */
+int orc_baseline_unit(const uint32_t *pos, const uint32_t *cnt, size_t n, uint32_t contig,
+                      int strand, uint16_t bw, double region_thr, double kurt_thr,
                       double hit_thr, double background, uint64_t *n_pass,
-                      uint64_t *n_reject, double *seconds);
+                      uint64_t *n_reject);
 
 /* "pos count\n" / "pos -count\n" wiggle lines (out: 24 bytes per pair) */
 size_t orc_format_pairs(const uint32_t *pos, const uint32_t *cnt, size_t n, int neg,

@@ -143,33 +143,22 @@ int orc_baseline_run(uint32_t n_contigs, const uint32_t *lens, uint64_t seed,
 /* One (contig, strand) unit of the hot-path baseline on its own buffer
  * (flushContig resets the position state, misc/peakcall.cpp:224-231, so
  * units are independent -- the reference's contig-subset method, README:37,
- * run as threads): generation untimed, add/flush timed. */
-int orc_baseline_unit(uint32_t len, uint32_t contig, int strand, uint64_t seed,
-                      uint16_t bw, double region_thr, double kurt_thr,
+ * run as threads) over pre-generated hits: only the add/flush calls run. */
+int orc_baseline_unit(const uint32_t *pos, const uint32_t *cnt, size_t n, uint32_t contig,
+                      int strand, uint16_t bw, double region_thr, double kurt_thr,
                       double hit_thr, double background, uint64_t *n_pass,
-                      uint64_t *n_reject, double *seconds) {
+                      uint64_t *n_reject) {
     const uint32_t W = 2u * bw + 1;
     double *k = (double *)malloc(W * sizeof(double));
     orc_kernel(bw, 1 / background, k);
     uint8_t ctl = 0;
     orc_buf *b = orc_buf_new(k, W, region_thr, kurt_thr, -1, hit_thr, strand == 0, 1, &ctl,
                              NULL, 0, NULL, NULL, NULL, NULL);
-    const size_t cap = (size_t)(len / 64) + 4096;
-    uint32_t *pos = (uint32_t *)malloc(cap * sizeof(uint32_t));
-    uint32_t *cnt = (uint32_t *)malloc(cap * sizeof(uint32_t));
-    size_t n = orc_synth_track(seed, contig, strand, 0, len, bw, 1, pos, cnt, cap);
-    if (n > cap) n = cap;
-    struct timespec t0, t1;
-    clock_gettime(CLOCK_MONOTONIC, &t0);
     for (size_t i = 0; i < n; ++i) orc_buf_add(b, &cnt[i], contig, pos[i], strand == 0);
     orc_buf_flush(b);
-    clock_gettime(CLOCK_MONOTONIC, &t1);
-    *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
     *n_pass = orc_buf_nregions(b);
     *n_reject = orc_buf_nrejects(b);
     orc_buf_free(b);
-    free(pos);
-    free(cnt);
     free(k);
     return 0;
 }

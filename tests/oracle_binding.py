@@ -47,9 +47,8 @@ class Oracle:
         L.orc_baseline_run.argtypes = [c.c_uint32, vp, c.c_uint64, c.c_uint16, c.c_double,
                                        c.c_double, c.c_double, c.c_double, vp, vp, vp]
         L.orc_baseline_unit.restype = c.c_int
-        L.orc_baseline_unit.argtypes = [c.c_uint32, c.c_uint32, c.c_int, c.c_uint64, c.c_uint16,
-                                        c.c_double, c.c_double, c.c_double, c.c_double, vp, vp,
-                                        vp]
+        L.orc_baseline_unit.argtypes = [vp, vp, c.c_size_t, c.c_uint32, c.c_int, c.c_uint16,
+                                        c.c_double, c.c_double, c.c_double, c.c_double, vp, vp]
         L.orc_format_pairs.restype = c.c_size_t
         L.orc_format_pairs.argtypes = [vp, vp, c.c_size_t, c.c_int, vp]
         self.L = L
@@ -122,16 +121,18 @@ class Oracle:
                                 ctypes.byref(sec))
         return npass.value, nrej.value, sec.value
 
-    def baseline_unit(self, length, contig, strand, seed, bw, region_thr, kurt_thr, hit_thr,
+    def baseline_unit(self, pos, cnt, contig, strand, bw, region_thr, kurt_thr, hit_thr,
                       background):
-        """one (contig, strand) unit of the hot-path baseline -> (pass, reject, seconds)"""
+        """one (contig, strand) unit of the hot-path baseline over given hits
+        -> (pass, reject)"""
+        pos = np.ascontiguousarray(pos, np.uint32)
+        cnt = np.ascontiguousarray(cnt, np.uint32)
         npass = ctypes.c_uint64()
         nrej = ctypes.c_uint64()
-        sec = ctypes.c_double()
-        self.L.orc_baseline_unit(length, contig, strand, seed, bw, region_thr, kurt_thr, hit_thr,
-                                 background, ctypes.byref(npass), ctypes.byref(nrej),
-                                 ctypes.byref(sec))
-        return npass.value, nrej.value, sec.value
+        self.L.orc_baseline_unit(pos.ctypes.data, cnt.ctypes.data, pos.size, contig, strand, bw,
+                                 region_thr, kurt_thr, hit_thr, background, ctypes.byref(npass),
+                                 ctypes.byref(nrej))
+        return npass.value, nrej.value
 
     def format_pairs(self, pos, cnt, neg):
         """wiggle data lines for (pos, count) pairs as bytes"""

@@ -189,3 +189,23 @@ def test_head_hits_nondir_with_corr(gpu_lib, oracle, seed):
                              kurt_thr=0.0, want_corr=True)
     compare(ref, ref_sums, regs, gcnt)
     assert close(ref["corr"], regs["corr"])
+
+
+@pytest.mark.parametrize("offset,strand", [(75, 0), (-75, 1), (-300, 0), (400, 1)])
+def test_synthetic_track_offset(gpu_lib, oracle, offset, strand):
+    """up_unit_synth_offset == the spec's track moved by the -s offset, with
+    what leaves [1, len] dropped (the wiggle reader's bounds)"""
+    length, bw = 60_000, 50
+    pos, cnt = oracle.synth_track(1000, 3, strand, True, length, bw)
+    p = pos.astype(np.int64) + offset
+    keep = (p >= 1) & (p <= length)
+    pos, cnt = p[keep].astype(np.uint32), cnt[keep]
+    with gpu_lib.Lib(0) as g:
+        g.set_params(bw, 1, 0.003)
+        u = g.add_unit(length)
+        g.synth(u, 0, 0, 1000, 3, strand, nondir=True, peaks=True, offset=offset)
+        assert g.tag_total(u, 0, 0) == int(cnt.sum())
+        g.run()
+        f, _ = g.profile(u, length)
+    ref = oracle.profile(bw, 0.003, length, pos, cnt.reshape(-1, 1))
+    assert ref.tobytes() == f.tobytes()

@@ -332,3 +332,75 @@ def test_step_board_world3(tmp_path):
     for r in range(world):
         assert np.load(tmp_path / f"b{r}.npy").tolist() == want
     assert not os.path.exists(f"/dev/shm/unipeak_board_test_{port}")
+
+
+def _pipeline_worker(rank, world, port, out_dir, nsteps, depth, nslot):
+    """bench.py's per-step host protocol of one node without the GPU: the
+    board's tag all-reduce, a pass = this rank writing its records of step i
+    into NodeRecords slot i % nslot (only after rank 0 read step i - nslot),
+    post_done, and rank 0 reading step i - depth once every rank is done"""
+    import json
+    import time
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = shard.Comm(dist, rank, world, "cpu")
+    tag = f"pipe_{port}"
+    nr = shard.NodeRecords(comm, cap=64, n_samples=1, rec_bytes=REGION_DTYPE.itemsize, tag=tag,
+                           nslots=nslot)
+    board = shard.StepBoard(comm, tag, timeout_s=60.0)
+    bad = 0
+    try:
+        dist.barrier()
+        t0 = time.perf_counter()
+        for i in range(nsteps + depth):
+            if i < nsteps:
+                if i >= nslot:
+                    board.wait_read(i - nslot)
+                board.post_tags(i, rank + i)
+                if board.tags(i) != sum(r + i for r in range(world)):
+                    bad += 1
+                k = 1 + (rank + i) % 7  # this rank's records of step i
+                slot = nr.mine[(i % nslot) * nr.slot:(i % nslot + 1) * nr.slot]
+                recs = np.zeros(k, REGION_DTYPE)
+                recs["unit"] = rank
+                recs["left"] = i
+                slot[8:8 + k * REGION_DTYPE.itemsize] = recs.view(np.uint8)
+                slot[:8] = np.frombuffer(np.uint64(k).tobytes(), np.uint8)
+                board.post_done(i)
+            j = i - depth
+            if rank == 0 and j >= 0:
+                board.wait_done(j)
+                for w, (r, _) in enumerate(nr.read(REGION_DTYPE, j)):
+                    if len(r) != 1 + (w + j) % 7 or (r["unit"] != w).any() or (r["left"] != j).any():
+                        bad += 1
+                del r
+                board.post_read(j)
+        dt = (time.perf_counter() - t0) / nsteps
+        del slot  # no view of the segment may outlive it
+        with open(os.path.join(out_dir, f"p{rank}.json"), "w") as f:
+            json.dump({"bad": bad, "us_per_step": dt * 1e6}, f)
+        dist.barrier()
+    finally:
+        board.close()
+        nr.close()
+        dist.destroy_process_group()
+
+
+def test_node_pipeline_world8(tmp_path):
+    """8 ranks x 200 steps of the one-node pipelined protocol (StepBoard +
+    NodeRecords, depth 5, 10 slots): every step's tag sum and every rank's
+    records reach rank 0 intact; the host cost per step is printed (the
+    8-GPU bench step is ~0.1 ms of GPU time)"""
+    import json
+    import torch.multiprocessing as mp
+    port = _free_port()
+    world, nsteps = 8, 200
+    mp.spawn(_pipeline_worker, args=(world, port, str(tmp_path), nsteps, 5, 10), nprocs=world,
+             join=True)
+    res = [json.load(open(tmp_path / f"p{r}.json")) for r in range(world)]
+    assert all(r["bad"] == 0 for r in res)
+    print(f"\n  host protocol: {max(r['us_per_step'] for r in res):.1f} us/step (slowest rank, "
+          f"{os.cpu_count()} CPUs shared by {world} spinning ranks)")
+    assert not os.path.exists(f"/dev/shm/unipeak_pipe_{port}")
+    assert not os.path.exists(f"/dev/shm/unipeak_board_pipe_{port}")

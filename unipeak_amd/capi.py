@@ -67,7 +67,7 @@ _lib = None
 EXPORTS = [
     "up_version", "up_strerror", "up_device_count", "up_kernel_weights", "up_open",
     "up_close", "up_set_params", "up_add_unit", "up_unit_count", "up_unit_pack",
-    "up_unit_scatter", "up_unit_synth", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
+    "up_unit_scatter", "up_unit_synth", "up_unit_synth_offset", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
     "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan",
     "up_timings", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
     "up_host_register", "up_unit_profile_range", "up_run_async", "up_run_wait", "up_set_timing",
@@ -98,6 +98,8 @@ def load_library(path=LIB_PATH):
         "up_unit_scatter": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.c_size_t, vp, vp]),
         "up_unit_synth": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.c_uint64,
                                     c.c_uint32, c.c_int32, c.c_int32, c.c_int32]),
+        "up_unit_synth_offset": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.c_uint64,
+                                           c.c_uint32, c.c_int32, c.c_int32, c.c_int32, c.c_int32]),
         "up_unit_tag_total": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16,
                                         c.POINTER(c.c_uint64)]),
         "up_unit_set_last_add": (c.c_int, [vp, c.c_uint32, c.c_uint32]),
@@ -201,9 +203,13 @@ class Lib:
                                    pos.ctypes.data, counts.ctypes.data))
 
     def synth(self, unit, strand, sample, seed, contig_index, synth_strand, nondir=False,
-              peaks=True):
-        _ck(self.L.up_unit_synth(self.ctx, unit, strand, sample, seed, contig_index,
-                                 synth_strand, int(nondir), int(peaks)))
+              peaks=True, offset=0):
+        if offset:
+            _ck(self.L.up_unit_synth_offset(self.ctx, unit, strand, sample, seed, contig_index,
+                                            synth_strand, int(nondir), int(peaks), int(offset)))
+        else:
+            _ck(self.L.up_unit_synth(self.ctx, unit, strand, sample, seed, contig_index,
+                                     synth_strand, int(nondir), int(peaks)))
 
     def tag_total(self, unit, strand, sample):
         v = ctypes.c_uint64()

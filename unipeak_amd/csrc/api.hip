@@ -211,6 +211,10 @@ struct up_ctx {
     DevBuf<double> d_reg_f, d_reg_r;
     DevBuf<up_region> d_emu_out;
     DevBuf<double> d_ring_f, d_ring_r;   // K0 window in global memory (very wide kernels)
+    // K4 (up_shift_scan) buffers, kept across calls
+    DevBuf<uint64_t> d_sh_idx, d_sh_off;
+    DevBuf<double> d_sh_slab, d_sh_out;
+    DevBuf<uint8_t> d_sh_pref;
     DevBuf<double> d_emu_scores;         // K0: stored scores of the replayed regions (f, r)
     DevBuf<uint64_t> d_emu_score_off;
     DevBuf<unsigned long long> d_emu_nscores;
@@ -369,6 +373,8 @@ void up_close(up_ctx *c) {
     c->d_unit_buffer.release(); c->d_reg_f.release(); c->d_reg_r.release(); c->d_emu_out.release();
     c->d_ring_f.release(); c->d_ring_r.release(); c->d_ring_has.release();
     c->d_emu_scores.release(); c->d_emu_score_off.release(); c->d_emu_nscores.release();
+    c->d_sh_idx.release(); c->d_sh_off.release(); c->d_sh_slab.release(); c->d_sh_out.release();
+    c->d_sh_pref.release();
     for (int k = 0; k < kSlots; ++k) {
         c->hp_regions[k].release(); c->hp_counts[k].release(); c->hp_status[k].release(); c->hp_head[k].release();
         for (auto &e : c->pass[k].ev) (void)hipEventDestroy(e);
@@ -695,6 +701,14 @@ static uint64_t hmix(uint64_t z) {
 
 int up_unit_synth(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uint64_t seed,
                   uint32_t contig_index, int32_t synth_strand, int32_t nondir, int32_t with_peaks) {
+    return up_unit_synth_offset(c, unit, strand, sample, seed, contig_index, synth_strand, nondir,
+                                with_peaks, 0);
+}
+
+int up_unit_synth_offset(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uint64_t seed,
+                         uint32_t contig_index, int32_t synth_strand, int32_t nondir,
+                         int32_t with_peaks, int32_t offset) {
+    if (offset < -32768 || offset > 32767) return UP_E_ARG;  // a short, like -s
     int r = check_track(c, unit, strand, sample);
     if (r) return r;
     if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
@@ -722,7 +736,7 @@ int up_unit_synth(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uin
     HIPCHK(hipMemsetAsync(trk, 0, (size_t)len * sizeof(uint32_t), c->stream));
     const uint64_t npos = (uint64_t)(hi - lo + 1);
     hipLaunchKernelGGL(synth_bg_kernel, dim3((unsigned)((npos + 255) / 256)), dim3(256), 0,
-                       c->stream, trk, tkey, lo, hi, thr);
+                       c->stream, trk, tkey, lo, hi, thr, (int64_t)offset, (int64_t)len);
     HIPCHK(hipGetLastError());
     if (with_peaks) {
         std::vector<uint32_t> tags;
@@ -742,7 +756,10 @@ int up_unit_synth(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uin
                 for (int m = 0; m < 12; ++m) s += (int64_t)(hmix(b + (uint64_t)m) >> 32);
                 const int64_t off = (60 * (s - 6 * 4294967296ll) + 2147483648ll) >> 32;
                 const int64_t p = centre + shift + off;
-                if (p >= lo && p <= hi) tags.push_back((uint32_t)p);
+                // generated on [lo, hi]; the -s offset then moves it, and the
+                // wiggle reader's bounds drop what leaves [1, len]
+                if (p >= lo && p <= hi && p + offset >= 1 && p + offset <= (int64_t)len)
+                    tags.push_back((uint32_t)(p + offset));
             }
         }
         if (!tags.empty()) {
@@ -1840,56 +1857,54 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
         HIPCHK(hipMemcpy(st.data(), ps.d_starts.p, c->nreg * 4, hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(en.data(), ps.d_ends.p, c->nreg * 4, hipMemcpyDeviceToHost));
     }
-    std::vector<uint64_t> off(n);
+    // global slab space only for regions whose scores do not stay in K4's
+    // LDS: replayed ones (their stored scores are copied in) and long ones
+    std::vector<uint64_t> off(n, 0);
+    std::vector<uint8_t> pref(n + 1, 0);
     uint64_t tot = 0;
     for (size_t j = 0; j < n; ++j) {
         if (idx[j] >= c->nreg) return UP_E_ARG;
-        off[j] = tot;
-        tot += 2ull * (en[idx[j]] - st[idx[j]] + 1);
-    }
-    uint64_t *d_idx = nullptr, *d_off = nullptr;
-    double *d_slab = nullptr, *d_out = nullptr;
-    uint8_t *d_pref = nullptr;
-    HIPCHK(hipMalloc(&d_idx, n * 8));
-    HIPCHK(hipMalloc(&d_off, n * 8));
-    HIPCHK(hipMalloc(&d_slab, (tot + 1) * 8));
-    HIPCHK(hipMalloc(&d_out, n * ((size_t)max_shift + 1) * 8));
-    HIPCHK(hipMalloc(&d_pref, n + 1));
-    HIPCHK(hipMemcpy(d_idx, idx, n * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d_off, off.data(), n * 8, hipMemcpyHostToDevice));
-    {
-        std::vector<uint8_t> pref(n + 1, 0);
-        for (size_t j = 0; j < n && c->host_regions; ++j) {
-            if (!c->h_emulated[idx[j]]) continue;
-            const uint64_t so = c->h_score_off[idx[j]];
-            if (so == ~0ull) return UP_E_INTERNAL;
-            const uint64_t len = (uint64_t)en[idx[j]] - st[idx[j]] + 1;
-            HIPCHK(hipMemcpyAsync(d_slab + off[j], c->d_emu_scores.p + so, 2 * len * sizeof(double),
-                                  hipMemcpyDeviceToDevice, c->stream));
-            pref[j] = 1;
+        const uint64_t len = (uint64_t)en[idx[j]] - st[idx[j]] + 1;
+        pref[j] = c->host_regions && c->h_emulated[idx[j]] ? 1 : 0;
+        if (pref[j] || len > (uint64_t)kShiftLds) {
+            off[j] = tot;
+            tot += 2ull * len;
         }
-        HIPCHK(hipMemcpyAsync(d_pref, pref.data(), n + 1, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
     }
+    const size_t nout = n * ((size_t)max_shift + 1);
+    HIPCHK(c->d_sh_idx.ensure(n));
+    HIPCHK(c->d_sh_off.ensure(n));
+    HIPCHK(c->d_sh_slab.ensure(tot + 1));
+    HIPCHK(c->d_sh_out.ensure(nout));
+    HIPCHK(c->d_sh_pref.ensure(n + 1));
+    uint64_t *d_idx = c->d_sh_idx.p, *d_off = c->d_sh_off.p;
+    double *d_slab = c->d_sh_slab.p, *d_out = c->d_sh_out.p;
+    uint8_t *d_pref = c->d_sh_pref.p;
+    HIPCHK(hipMemcpyAsync(d_idx, idx, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_off, off.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    for (size_t j = 0; j < n; ++j) {
+        if (!pref[j]) continue;
+        const uint64_t so = c->h_score_off[idx[j]];
+        if (so == ~0ull) return UP_E_INTERNAL;
+        const uint64_t len = (uint64_t)en[idx[j]] - st[idx[j]] + 1;
+        HIPCHK(hipMemcpyAsync(d_slab + off[j], c->d_emu_scores.p + so, 2 * len * sizeof(double),
+                              hipMemcpyDeviceToDevice, c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(d_pref, pref.data(), n + 1, hipMemcpyHostToDevice, c->stream));
     StatParams P = stat_params(c, ps);
     const int nh = P.bw <= 63 ? 1 : 2;
     const int pool = pool_mode(c);
-    const size_t lds = kKTab * sizeof(double);
+    const size_t lds = kShiftLdsBytes;
     const unsigned blocks = (unsigned)std::min<size_t>(n, 8192);
-#define UPK_SH(NH, PL)                                                                        \
-    if (nh == NH && pool == PL)                                                               \
-        hipLaunchKernelGGL((shift_kernel<NH, PL>), dim3(blocks), dim3(64), lds, c->stream, P, \
-                           d_idx, (uint32_t)n, (int)max_shift, d_off, d_slab, d_pref, d_out);
+#define UPK_SH(NH, PL)                                                                              \
+    if (nh == NH && pool == PL)                                                                     \
+        hipLaunchKernelGGL((shift_kernel<NH, PL>), dim3(blocks), dim3(kShiftThreads), lds, c->stream, \
+                           P, d_idx, (uint32_t)n, (int)max_shift, d_off, d_slab, d_pref, d_out);
     UPK_SH(1, 0) UPK_SH(1, 1) UPK_SH(1, 2) UPK_SH(2, 0) UPK_SH(2, 1) UPK_SH(2, 2)
 #undef UPK_SH
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipMemcpy(out, d_out, n * ((size_t)max_shift + 1) * 8, hipMemcpyDeviceToHost));
-    (void)hipFree(d_idx);
-    (void)hipFree(d_off);
-    (void)hipFree(d_slab);
-    (void)hipFree(d_out);
-    (void)hipFree(d_pref);
+    HIPCHK(hipMemcpy(out, d_out, nout * 8, hipMemcpyDeviceToHost));
     return UP_OK;
 }
 

@@ -2005,20 +2005,34 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
 }
 
 // ------------------------------------------------------------------------
-// K4: strandCorr(shift) for shift = 0..max_shift; one wave per region,
-// lanes = shifts.  f/r of the region are first materialised by the wave
-// into a scratch slab (same KDE as K3), then each lane runs the reference's
-// five sequential passes (mean, mean, sd, sd, cross) for its shift.
+// K4: strandCorr(shift) for shift = 0..max_shift (src/strand_shift.cpp:
+// 205-217, Region::strandCorr, misc/data.cpp:22-58, 184-193).  One block of
+// kShiftThreads (three waves) per region, grid-stride over the regions:
+//  1. the region's f and r (same KDE as K3) are materialised by the three
+//     waves, 64 positions per wave step, into LDS (regions up to
+//     kShiftLds positions; longer ones, and replayed regions, which arrive
+//     with the scores the state machine stored, use the global slab);
+//  2. thread t takes shifts t, t + 192, ...: the reference's sums -- mean of
+//     f[0, m), mean of r[2s, 2s + m), the two sums of squared deviations and
+//     the cross sum, each sequential in index order -- as three loops whose
+//     independent chains (s1 | s2, q1 | q2, q3) interleave, the loads of four
+//     iterations issued ahead of their in-order adds.
 // ------------------------------------------------------------------------
+constexpr int kShiftThreads = 192;
+constexpr int kShiftLds = 2048;  // positions of f and r kept in LDS per region
+constexpr size_t kShiftLdsBytes = kKTab * sizeof(double) + 2 * kShiftLds * sizeof(double);
 template <int NH, int POOL>
-__global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t *idx, uint32_t n,
-                                                   int max_shift, const uint64_t *slab_off,
-                                                   double *slab, const uint8_t *prefilled, double *out) {
+__global__ void __launch_bounds__(kShiftThreads) shift_kernel(StatParams P, const uint64_t *idx, uint32_t n,
+                                                              int max_shift, const uint64_t *slab_off,
+                                                              double *slab, const uint8_t *prefilled,
+                                                              double *out) {
     extern __shared__ double lds_[];
     const int bw = P.bw;
     const double *ktab = load_ktab(lds_, P.kern, bw);
+    double *lf = lds_ + kKTab, *lr = lf + kShiftLds;
     constexpr int NWT = 2 * NH + 1;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int nwv = kShiftThreads / 64;
     uint64_t wm[2 * NH + 1];
 #pragma unroll
     for (int d = -NH; d <= NH; ++d) wm[d + NH] = win_mask(d, bw);
@@ -2027,10 +2041,13 @@ __global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t 
         const uint32_t left = P.starts[ri], right = P.ends[ri], u = P.reg_unit[ri];
         const UnitDesc U = P.units[u];
         const uint32_t len = right - left + 1;
-        double *fs = slab + slab_off[j], *rs = fs + len;
+        const bool pre = prefilled[j] != 0;
+        const bool in_lds = !pre && len <= (uint32_t)kShiftLds;
+        double *fs = in_lds ? lf : slab + slab_off[j];
+        double *rs = in_lds ? lr : fs + len;
         // replayed regions arrive with their stored scores; the others are
         // materialised from the dense KDE
-        for (int64_t x0 = left; !prefilled[j] && x0 <= (int64_t)right; x0 += 64) {
+        for (int64_t x0 = (int64_t)left + 64 * wv; !pre && x0 <= (int64_t)right; x0 += 64 * nwv) {
             WinT<POOL> cf[NWT], cr[NWT];
             uint64_t hf[NWT], hr[NWT];
             region_words<NH, POOL>(cf, hf, U, 0, x0, lane, P);
@@ -2040,21 +2057,48 @@ __global__ void __launch_bounds__(64) shift_kernel(StatParams P, const uint64_t 
             const int64_t x = x0 + lane;
             if (x <= (int64_t)right) { fs[x - left] = f; rs[x - left] = r; }
         }
-        __syncthreads();
-        for (int sh = lane; sh <= max_shift; sh += 64) {
+        __syncthreads();  // (global slab writes: visible block-wide after the barrier too)
+        for (int sh = threadIdx.x; sh <= max_shift; sh += kShiftThreads) {
             double c = __builtin_nan("");
             if (len > (uint32_t)(2 * sh + 3)) {
                 const uint32_t m = len - 2 * sh;
                 const double *a = fs, *b = rs + 2 * sh;
+                constexpr uint32_t U4 = 4;
+                const uint32_t m4 = m & ~(U4 - 1);
                 double s1 = 0.0, s2 = 0.0;
-                for (uint32_t i = 0; i < m; ++i) s1 = s1 + a[i];
-                for (uint32_t i = 0; i < m; ++i) s2 = s2 + b[i];
+                uint32_t i = 0;
+                for (; i < m4; i += U4) {
+                    double x[U4], y[U4];
+#pragma unroll
+                    for (uint32_t k = 0; k < U4; ++k) { x[k] = a[i + k]; y[k] = b[i + k]; }
+#pragma unroll
+                    for (uint32_t k = 0; k < U4; ++k) { s1 = s1 + x[k]; s2 = s2 + y[k]; }
+                }
+                for (; i < m; ++i) { s1 = s1 + a[i]; s2 = s2 + b[i]; }
                 const double m1 = s1 / (double)m, m2 = s2 / (double)m;
-                double q1 = 0.0, q2 = 0.0, q3 = 0.0;
-                for (uint32_t i = 0; i < m; ++i) { const double d = a[i] - m1; q1 = q1 + d * d; }
-                for (uint32_t i = 0; i < m; ++i) { const double d = b[i] - m2; q2 = q2 + d * d; }
+                double q1 = 0.0, q2 = 0.0;
+                for (i = 0; i < m4; i += U4) {
+                    double x[U4], y[U4];
+#pragma unroll
+                    for (uint32_t k = 0; k < U4; ++k) { x[k] = a[i + k] - m1; y[k] = b[i + k] - m2; }
+#pragma unroll
+                    for (uint32_t k = 0; k < U4; ++k) { q1 = q1 + x[k] * x[k]; q2 = q2 + y[k] * y[k]; }
+                }
+                for (; i < m; ++i) {
+                    const double x = a[i] - m1, y = b[i] - m2;
+                    q1 = q1 + x * x;
+                    q2 = q2 + y * y;
+                }
                 const double sd1 = sqrt(q1 / ((double)m - 1)), sd2 = sqrt(q2 / ((double)m - 1));
-                for (uint32_t i = 0; i < m; ++i) q3 = q3 + (a[i] - m1) * (b[i] - m2);
+                double q3 = 0.0;
+                for (i = 0; i < m4; i += U4) {
+                    double x[U4];
+#pragma unroll
+                    for (uint32_t k = 0; k < U4; ++k) x[k] = (a[i + k] - m1) * (b[i + k] - m2);
+#pragma unroll
+                    for (uint32_t k = 0; k < U4; ++k) q3 = q3 + x[k];
+                }
+                for (; i < m; ++i) q3 = q3 + (a[i] - m1) * (b[i] - m2);
                 c = q3 / (((double)m - 1) * sd1 * sd2);
             }
             out[(uint64_t)j * (max_shift + 1) + sh] = c;
@@ -2118,15 +2162,16 @@ struct SynthThr {
 
 // synthetic counts are generated into a dense uint32 staging track
 // (position p at stage[p-1]) and packed by pack_kernel
+// (offset: the track moved by -s positions; what leaves [1, len] is dropped)
 __global__ void synth_bg_kernel(uint32_t *stage, uint64_t tkey, int64_t lo, int64_t hi,
-                                SynthThr thr) {
+                                SynthThr thr, int64_t offset, int64_t len) {
     const int64_t x = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x > hi) return;
+    if (x > hi || x + offset < 1 || x + offset > len) return;
     const uint64_t u = mix64(tkey ^ mix64((uint64_t)x));
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) c += u >= thr.t[k];
-    stage[x - 1] = c;
+    stage[x + offset - 1] = c;
 }
 
 // sum of a 4-bit track's counts, escapes excluded (their counts are added on
