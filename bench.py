@@ -578,15 +578,11 @@ def shift_pipeline(args, W):
         span = (regs["right"].astype(np.int64) - regs["left"] + 1)[order]
         elig = order[span > 2 * max_shift + 3]
         t2 = time.perf_counter()
-        table = ga.shift_scan(elig, max_shift)
+        # strand_shift.cpp:205-228: per region the first shift of the largest
+        # correlation above -1 (K4 + a device reduction), then the first
+        # n_test qualifying regions
+        best, bcorr = ga.shift_best(elig, max_shift)
         t3 = time.perf_counter()
-        # strand_shift.cpp:205-228: first maximum from bestCorr = -1 (NaN
-        # never wins), the first n_test qualifying regions
-        tb = np.concatenate([np.full((len(table), 1), -1.0),
-                             np.where(np.isnan(table), -np.inf, table)], axis=1)
-        arg = np.argmax(tb, axis=1)                # 0: no corr above -1
-        bcorr = tb[np.arange(len(tb)), arg]
-        best = np.maximum(arg - 1, 0)
         ok = np.flatnonzero(bcorr >= u_thr)[:n_test]
         freq = np.bincount(best[ok], minlength=max_shift + 1).astype(np.float64)
         # strand_shift.cpp:241-248: dens[i - 5 + j] += freq[i] * k5[j]; every

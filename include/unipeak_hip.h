@@ -202,6 +202,12 @@ int up_host_register(up_ctx *ctx, void *ptr, uint64_t bytes);
  * (indices into up_get_regions order); out is [n][max_shift+1]. */
 int up_shift_scan(up_ctx *ctx, const uint64_t *region_idx, size_t n,
                   uint16_t max_shift, double *out);
+/* the same regions reduced on the device to strand_shift's per-region
+ * choice (src/strand_shift.cpp:209-217): best_shift = the first shift whose
+ * strandCorr is the largest value above -1 (0 if none), best_corr = that
+ * value (-1 if none) */
+int up_shift_best(up_ctx *ctx, const uint64_t *region_idx, size_t n,
+                  uint16_t max_shift, uint16_t *best_shift, double *best_corr);
 
 /* device-side timings of the last up_run in ms: [0]=K1 scan, [1]=K2
  * segment, [2]=K3 stats, [3]=whole up_run wall, [4]=K1 launches */

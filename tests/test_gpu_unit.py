@@ -209,3 +209,36 @@ def test_synthetic_track_offset(gpu_lib, oracle, offset, strand):
         f, _ = g.profile(u, length)
     ref = oracle.profile(bw, 0.003, length, pos, cnt.reshape(-1, 1))
     assert ref.tobytes() == f.tobytes()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_shift_best_is_first_maximum_of_table(gpu_lib, seed):
+    """up_shift_best == strand_shift.cpp:209-217 applied to up_shift_scan's
+    table: shifts ascending, `corr > bestCorr` from -1 (NaN never wins;
+    regions too short for any shift give shift 0, corr -1)"""
+    rng = np.random.default_rng(500 + seed)
+    length, bw = 300_000, 50
+    pos_f, cnt_f = random_unit(rng, length, bw)
+    pos_r, cnt_r = random_unit(rng, length, bw)
+    allp = np.union1d(pos_f, pos_r).astype(np.uint32)
+    cf = np.zeros((allp.size, 1), np.uint32)
+    cr = np.zeros((allp.size, 1), np.uint32)
+    cf[np.searchsorted(allp, pos_f)] = cnt_f
+    cr[np.searchsorted(allp, pos_r)] = cnt_r
+    with gpu_lib.Lib(0) as g:
+        g.set_params(bw, 1, 0.004, nondir=True)
+        u = g.add_unit(length)
+        for st, c in enumerate((cf, cr)):
+            m = c[:, 0] != 0
+            g.scatter(u, st, 0, allp[m], c[m, 0])
+        n = g.run()
+        idx = np.arange(n, dtype=np.uint64)[::-1].copy()
+        for max_shift in (0, 20, 150, 300):
+            tab = g.shift_scan(idx, max_shift)
+            best, bc = g.shift_best(idx, max_shift)
+            for k in range(n):
+                b, c = 0, -1.0
+                for s in range(max_shift + 1):
+                    if tab[k, s] > c:
+                        b, c = s, tab[k, s]
+                assert best[k] == b and bc[k] == c, (k, max_shift)

@@ -68,7 +68,7 @@ EXPORTS = [
     "up_version", "up_strerror", "up_device_count", "up_kernel_weights", "up_open",
     "up_close", "up_set_params", "up_add_unit", "up_unit_count", "up_unit_pack",
     "up_unit_scatter", "up_unit_synth", "up_unit_synth_offset", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
-    "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan",
+    "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan", "up_shift_best",
     "up_timings", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
     "up_host_register", "up_unit_profile_range", "up_run_async", "up_run_wait", "up_set_timing",
 ]
@@ -112,6 +112,7 @@ def load_library(path=LIB_PATH):
         "up_get_regions": (c.c_int, [vp, vp, vp, c.c_size_t]),
         "up_regions_view": (c.c_int, [vp, c.POINTER(vp), c.POINTER(vp), c.POINTER(c.c_uint64)]),
         "up_shift_scan": (c.c_int, [vp, vp, c.c_size_t, c.c_uint16, vp]),
+        "up_shift_best": (c.c_int, [vp, vp, c.c_size_t, c.c_uint16, vp, vp]),
         "up_timings": (c.c_int, [vp, vp, c.c_int]),
         "up_unit_profile": (c.c_int, [vp, c.c_uint32, vp, vp, c.c_uint32]),
         "up_hbm_copy_gbps": (c.c_int, [vp, c.c_uint64, c.c_int, c.POINTER(c.c_double)]),
@@ -278,6 +279,15 @@ class Lib:
         _ck(self.L.up_shift_scan(self.ctx, idx.ctypes.data, idx.size, max_shift,
                                  out.ctypes.data))
         return out
+
+    def shift_best(self, idx, max_shift):
+        """-> (best shift uint16[n], best corr f8[n]) per region (up_shift_best)"""
+        idx = np.ascontiguousarray(idx, np.uint64)
+        best = np.zeros(idx.size, np.uint16)
+        corr = np.zeros(idx.size, np.float64)
+        _ck(self.L.up_shift_best(self.ctx, idx.ctypes.data, idx.size, max_shift, best.ctypes.data,
+                                 corr.ctypes.data))
+        return best, corr
 
     def set_record_target(self, dev_ptr, cap):
         """records of the next runs go to a device buffer (see the header);

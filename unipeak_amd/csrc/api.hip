@@ -1827,8 +1827,22 @@ int up_regions_view(up_ctx *c, const up_region **regions, const uint32_t **count
     return UP_OK;
 }
 
+static int shift_run(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, double *out,
+                     uint16_t *best, double *best_corr);
+
 int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, double *out) {
     if (!c || (n && (!idx || !out))) return UP_E_ARG;
+    return shift_run(c, idx, n, max_shift, out, nullptr, nullptr);
+}
+
+int up_shift_best(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, uint16_t *best,
+                  double *best_corr) {
+    if (!c || (n && (!idx || !best || !best_corr))) return UP_E_ARG;
+    return shift_run(c, idx, n, max_shift, nullptr, best, best_corr);
+}
+
+static int shift_run(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, double *out,
+                     uint16_t *best, double *best_corr) {
     if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     if (!c->ran) return UP_E_STATE;
     if (!c->p.nondir) return UP_E_UNSUPPORTED;
@@ -1871,7 +1885,9 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
             tot += 2ull * len;
         }
     }
-    const size_t nout = n * ((size_t)max_shift + 1);
+    // table mode: n x (max_shift + 1) correlations; best mode: per region
+    // the chosen shift (uint16, packed after the n best correlations)
+    const size_t nout = best ? n + (n + 3) / 4 : n * ((size_t)max_shift + 1);
     HIPCHK(c->d_sh_idx.ensure(n));
     HIPCHK(c->d_sh_off.ensure(n));
     HIPCHK(c->d_sh_slab.ensure(tot + 1));
@@ -1899,12 +1915,19 @@ int up_shift_scan(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shift, 
 #define UPK_SH(NH, PL)                                                                              \
     if (nh == NH && pool == PL)                                                                     \
         hipLaunchKernelGGL((shift_kernel<NH, PL>), dim3(blocks), dim3(kShiftThreads), lds, c->stream, \
-                           P, d_idx, (uint32_t)n, (int)max_shift, d_off, d_slab, d_pref, d_out);
+                           P, d_idx, (uint32_t)n, (int)max_shift, d_off, d_slab, d_pref,               \
+                           best ? nullptr : d_out, best ? (uint16_t *)(d_out + n) : nullptr,            \
+                           best ? d_out : nullptr);
     UPK_SH(1, 0) UPK_SH(1, 1) UPK_SH(1, 2) UPK_SH(2, 0) UPK_SH(2, 1) UPK_SH(2, 2)
 #undef UPK_SH
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipMemcpy(out, d_out, nout * 8, hipMemcpyDeviceToHost));
+    if (best) {
+        HIPCHK(hipMemcpy(best_corr, d_out, n * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(best, d_out + n, n * 2, hipMemcpyDeviceToHost));
+    } else {
+        HIPCHK(hipMemcpy(out, d_out, nout * 8, hipMemcpyDeviceToHost));
+    }
     return UP_OK;
 }
 

@@ -2021,12 +2021,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
 constexpr int kShiftThreads = 192;
 constexpr int kShiftLds = 2048;  // positions of f and r kept in LDS per region
 constexpr size_t kShiftLdsBytes = kKTab * sizeof(double) + 2 * kShiftLds * sizeof(double);
+// With best != nullptr the table is not written: the block reduces it to
+// the reference's choice (strand_shift.cpp:209-217: shifts ascending,
+// `corr > bestCorr` from bestCorr = -1, bestShift = 0; NaN never wins), i.e.
+// the smallest shift holding the largest correlation above -1.
 template <int NH, int POOL>
 __global__ void __launch_bounds__(kShiftThreads) shift_kernel(StatParams P, const uint64_t *idx, uint32_t n,
                                                               int max_shift, const uint64_t *slab_off,
                                                               double *slab, const uint8_t *prefilled,
-                                                              double *out) {
+                                                              double *out, uint16_t *best,
+                                                              double *best_corr) {
     extern __shared__ double lds_[];
+    __shared__ double red_c[kShiftThreads];
+    __shared__ int red_s[kShiftThreads];
     const int bw = P.bw;
     const double *ktab = load_ktab(lds_, P.kern, bw);
     double *lf = lds_ + kKTab, *lr = lf + kShiftLds;
@@ -2058,6 +2065,8 @@ __global__ void __launch_bounds__(kShiftThreads) shift_kernel(StatParams P, cons
             if (x <= (int64_t)right) { fs[x - left] = f; rs[x - left] = r; }
         }
         __syncthreads();  // (global slab writes: visible block-wide after the barrier too)
+        double bc = -1.0;  // this thread's first maximum over its shifts (ascending)
+        int bs = 0;
         for (int sh = threadIdx.x; sh <= max_shift; sh += kShiftThreads) {
             double c = __builtin_nan("");
             if (len > (uint32_t)(2 * sh + 3)) {
@@ -2101,7 +2110,26 @@ __global__ void __launch_bounds__(kShiftThreads) shift_kernel(StatParams P, cons
                 for (; i < m; ++i) q3 = q3 + (a[i] - m1) * (b[i] - m2);
                 c = q3 / (((double)m - 1) * sd1 * sd2);
             }
-            out[(uint64_t)j * (max_shift + 1) + sh] = c;
+            if (best) {
+                if (c > bc) { bc = c; bs = sh; }
+            } else {
+                out[(uint64_t)j * (max_shift + 1) + sh] = c;
+            }
+        }
+        if (best) {  // larger corr wins, equal corr -> smaller shift
+            red_c[threadIdx.x] = bc;
+            red_s[threadIdx.x] = bs;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double c = -1.0;
+                int sbest = 0;
+                for (int t = 0; t < kShiftThreads; ++t) {
+                    const double v = red_c[t];
+                    if (v > c || (v == c && v > -1.0 && red_s[t] < sbest)) { c = v; sbest = red_s[t]; }
+                }
+                best[j] = (uint16_t)sbest;
+                best_corr[j] = c;
+            }
         }
         __syncthreads();
     }

@@ -3,6 +3,7 @@
 #include "cli.hpp"
 
 #include <algorithm>
+#include <unordered_map>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -502,27 +503,61 @@ std::vector<Emitted> order_candidates(const PassResult &out, uint16_t bw, bool a
     return v;
 }
 
+// per device: the positions of `regs` it holds (its local candidate
+// indices); one hash of the device's candidate list instead of a search per
+// region
+static void device_regions(const PassResult &out, const DeviceJob &job,
+                           const std::vector<const Candidate *> &regs, std::vector<uint64_t> &idx,
+                           std::vector<size_t> &where) {
+    std::unordered_map<uint64_t, uint64_t> local;
+    local.reserve(job.cand_idx.size() * 2);
+    for (size_t i = 0; i < job.cand_idx.size(); ++i) local.emplace(job.cand_idx[i], (uint64_t)i);
+    idx.clear();
+    where.clear();
+    for (size_t k = 0; k < regs.size(); ++k) {
+        auto it = local.find((uint64_t)(regs[k] - out.cands.data()));
+        if (it == local.end()) continue;
+        idx.push_back(it->second);
+        where.push_back(k);
+    }
+}
+
 void shift_scan(const EngineParams &ep, PassResult &out, const std::vector<const Candidate *> &regs,
                 uint16_t max_shift, std::vector<double> &table) {
     (void)ep;
     const size_t W = (size_t)max_shift + 1;
     table.assign(regs.size() * W, 0.0);
+    std::vector<uint64_t> idx;
+    std::vector<size_t> where;
     for (DeviceJob &job : g_jobs) {
         if (!job.ctx) continue;
-        std::vector<uint64_t> idx;
-        std::vector<size_t> where;
-        for (size_t k = 0; k < regs.size(); ++k) {
-            const size_t ci = (size_t)(regs[k] - out.cands.data());
-            auto it = std::find(job.cand_idx.begin(), job.cand_idx.end(), (uint64_t)ci);
-            if (it == job.cand_idx.end()) continue;
-            idx.push_back((uint64_t)(it - job.cand_idx.begin()));
-            where.push_back(k);
-        }
+        device_regions(out, job, regs, idx, where);
         if (idx.empty()) continue;
         std::vector<double> t(idx.size() * W);
         check(up_shift_scan(job.ctx, idx.data(), idx.size(), max_shift, t.data()), "up_shift_scan");
         for (size_t j = 0; j < idx.size(); ++j)
             std::copy(t.begin() + j * W, t.begin() + (j + 1) * W, table.begin() + where[j] * W);
+    }
+}
+
+void shift_best(const EngineParams &ep, PassResult &out, const std::vector<const Candidate *> &regs,
+                uint16_t max_shift, std::vector<uint16_t> &best, std::vector<double> &best_corr) {
+    (void)ep;
+    best.assign(regs.size(), 0);
+    best_corr.assign(regs.size(), -1.0);
+    std::vector<uint64_t> idx;
+    std::vector<size_t> where;
+    for (DeviceJob &job : g_jobs) {
+        if (!job.ctx) continue;
+        device_regions(out, job, regs, idx, where);
+        if (idx.empty()) continue;
+        std::vector<uint16_t> b(idx.size());
+        std::vector<double> c(idx.size());
+        check(up_shift_best(job.ctx, idx.data(), idx.size(), max_shift, b.data(), c.data()), "up_shift_best");
+        for (size_t j = 0; j < idx.size(); ++j) {
+            best[where[j]] = b[j];
+            best_corr[where[j]] = c[j];
+        }
     }
 }
 

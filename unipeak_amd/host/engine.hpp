@@ -86,6 +86,10 @@ std::vector<Emitted> order_candidates(const PassResult &out, uint16_t bw, bool a
 // strandCorr(shift) table for accepted candidates (strand_shift), on GPU
 void shift_scan(const EngineParams &ep, PassResult &out, const std::vector<const Candidate *> &regs,
                 uint16_t max_shift, std::vector<double> &table);
+// strand_shift's per-region choice from the same table, reduced on the GPU
+// (up_shift_best): first shift of the largest correlation above -1
+void shift_best(const EngineParams &ep, PassResult &out, const std::vector<const Candidate *> &regs,
+                uint16_t max_shift, std::vector<uint16_t> &best, std::vector<double> &best_corr);
 
 // -w density profile (regions.cpp:276-284): every processed position with a
 // nonzero score, written when the reference's processPosition writes it --

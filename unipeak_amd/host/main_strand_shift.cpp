@@ -106,22 +106,19 @@ int main(int argc, char **argv) {
     std::vector<const Candidate *> elig;
     for (const Candidate *c : regs)
         if ((uint64_t)(c->r.right - c->r.left + 1) > (unsigned)(2 * max_shift + 3)) elig.push_back(c);
-    std::vector<double> table;
-    shift_scan(ep, pr, elig, max_shift, table);
+    // per region the first shift with the largest correlation (:209-217),
+    // reduced on the GPU
+    std::vector<uint16_t> bshift;
+    std::vector<double> bcorr;
+    shift_best(ep, pr, elig, max_shift, bshift, bcorr);
 
     uint16_t tested = 0;
     uint64_t tags_in = 0;
     std::vector<uint64_t> freq((size_t)max_shift + 1, 0);
     const size_t W = (size_t)max_shift + 1;
     for (size_t k = 0; tested < n_test && k < elig.size(); ++k) {
-        uint16_t best = 0;
-        double best_corr = -1;
-        for (size_t s = 0; s < W; ++s) {
-            const double c = table[k * W + s];
-            if (c > best_corr) { best = (uint16_t)s; best_corr = c; }
-        }
-        if (best_corr >= corr_thr) {
-            ++freq[best];
+        if (bcorr[k] >= corr_thr) {
+            ++freq[bshift[k]];
             tags_in += elig[k]->r.sum;
             ++tested;
         }
