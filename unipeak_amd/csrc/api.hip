@@ -608,7 +608,7 @@ static int pack_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample,
     for (int attempt = 0; attempt < 2; ++attempt) {
         HIPCHK(c->d_pack_ovf.ensure(cap));
         HIPCHK(hipMemsetAsync(c->d_pack_n.p, 0, 4, c->stream));
-        const uint64_t groups = (len + 7) / 8;  // 8 positions (one dword) per thread
+        const uint64_t groups = (len + 4 * kPerByte - 1) / (4 * kPerByte);  // one dword per thread
         hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, c->stream,
                            track_ptr(c, unit, strand, sample), src, len, c->d_pack_ovf.p, c->d_pack_n.p, cap);
         HIPCHK(hipGetLastError());

@@ -86,7 +86,7 @@ struct EmuState {
 };
 
 __device__ static bool any_at(const EmuParams &P, uint32_t u, int strand, int s, uint64_t p) {
-    return nib_at(track_u8(P.units[u], P.S, strand, s), (int64_t)p) != 0;
+    return fld_at(track_u8(P.units[u], P.S, strand, s), (int64_t)p) != 0;
 }
 
 // processRegion (peakcall.cpp:33-53) + Region statistics, appended to out

@@ -2,15 +2,21 @@
 // kernels (kernels.hip) and the C-ABI implementation (api.hip).
 //
 // HBM layout (DESIGN.md "Data layout"): every (unit, strand, sample) track is
-// a dense array of 4-bit tag counts, two positions per byte: position p
-// (1-based) is nibble n = kPadPos + p - 1, i.e. bits 4*(n & 1) .. +3 of byte
-// n >> 1 (odd positions in the low nibble).  kPadPos zero positions (kPadBytes
-// bytes) sit in front and at least as many behind the unit's scan domain
-// [1, len + bw], so every halo load is in bounds and reads zeros outside the
-// contig.  A count >= 15 is stored as the escape nibble 15 and its value in
-// the unit's overflow table (entries (pos << 32 | count), sorted by track
-// then position).  Tracks of one unit are contiguous: track(s, k) = base +
-// (s * S + k) * stride bytes.
+// a dense array of kTB-bit tag counts ("fields"), kPerByte positions per
+// byte: position p (1-based) is field n = kPadPos + p - 1, i.e. bits
+// kTB * (n % kPerByte) .. + kTB - 1 of byte n / kPerByte.  kPadPos zero
+// positions (kPadBytes bytes) sit in front and at least as many behind the
+// unit's scan domain [1, len + bw], so every halo load is in bounds and reads
+// zeros outside the contig.  A count >= kEsc (the all-ones field) is stored
+// as kEsc and its value in the unit's overflow table (entries
+// (pos << 32 | count), sorted by track then position).  Tracks of one unit
+// are contiguous: track(s, k) = base + (s * S + k) * stride bytes.
+//
+// kTB = 2 (UPK_TRACK_BITS): counts 0, 1, 2 in place, 3 = escape.  The
+// streaming scan (K1a) reads a quarter byte per position; ~99.6 % of
+// positions hold 0 and counts >= 3 occur at peaks only (a few per peak,
+// resolved through the per-block overflow index).  UPK_TRACK_BITS=4 builds
+// the 4-bit layout of round 2 (escape 15) for A/B measurements.
 #pragma once
 #include <stdint.h>
 
@@ -21,10 +27,20 @@ constexpr int kStripWords = 256;    // one strip (wave task) = 256 words of 64 p
 constexpr int kStrip = kStripWords * kWave;  // 16384 positions per wave task
 constexpr int kStepWords = 16;      // words per block (= one 1024-position dwordx4 wave load)
 constexpr int kBlocks = kStripWords / kStepWords;  // 16 blocks per strip
-constexpr int kChunk = 16;          // positions per lane in the screening load (dwordx4)
+constexpr int kChunk = 16;          // positions per screening chunk (one chunk sum each)
+#ifndef UPK_TRACK_BITS
+#define UPK_TRACK_BITS 2
+#endif
+constexpr int kTB = UPK_TRACK_BITS;               // bits per stored count
+static_assert(kTB == 2 || kTB == 4, "2- or 4-bit tracks");
+constexpr int kPerByte = 8 / kTB;                 // positions per byte
+constexpr int kLogPerByte = kTB == 2 ? 2 : 1;
+constexpr uint32_t kTMask = (1u << kTB) - 1u;     // one field
+constexpr int kWordBytes = kWave / kPerByte;      // bytes of one 64-position word
+constexpr int kChunkBytes = kChunk / kPerByte;    // bytes of one 16-position chunk
 constexpr int kPadBytes = 256;      // zero bytes before position 1 and after the domain
-constexpr int kPadPos = 2 * kPadBytes;  // the same padding in positions (nibbles)
-constexpr int kStripBytes = kStrip / 2;  // one strip of one track
+constexpr int kPadPos = kPerByte * kPadBytes;  // the same padding in positions
+constexpr int kStripBytes = kStrip / kPerByte;  // one strip of one track
 constexpr int kMaxBw = 127;         // register-resident halo: NH <= 2 words
 constexpr int kCap = 32;            // inline run records per strip (starts, ends each)
 constexpr int kOvfHalf = kStrip / 2 + 1;  // max starts (= max ends) of one strip
@@ -33,11 +49,11 @@ constexpr int kOvfHalf = kStrip / 2 + 1;  // max starts (= max ends) of one stri
 // inline per strip, kOvfHalf per spilled strip's overflow slot
 constexpr int kRecStride = 6 * kCap;
 constexpr int kOvfStride = 6 * kOvfHalf;
-constexpr uint32_t kEsc = 15;       // escape nibble: the count lives in the overflow table
+constexpr uint32_t kEsc = kTMask;   // escape field: the count lives in the overflow table
 constexpr int kXEntry = 2 + kWave / 2;  // strip, exact-block mask, 64 x 16-bit chunk masks
 constexpr int kMaxK1aWaves = 16384;     // K1a grid cap (stash regions)
 constexpr int kModeFused = 0, kModeScreen = 1, kModeExact = 2;  // K1 variants
-constexpr uint32_t kBig = 1u << 22; // screen value of a chunk holding a nibble >= 8
+constexpr uint32_t kBig = 1u << 22; // screen value of a chunk holding an escape (4-bit: a count >= 8)
 
 // overflow entries are indexed per block of kOvfBlk positions, so a lookup
 // searches one block's entries instead of the whole track's

@@ -78,20 +78,38 @@ __device__ __forceinline__ double rl_cs(double v, int l) { return rl_d(v, l); }
 __device__ __forceinline__ bool nz(uint32_t v) { return v != 0u; }
 __device__ __forceinline__ bool nz(double v) { return v != 0.0; }
 
-// ---- track access (layout in kernels.h: 4-bit counts, two per byte) ----
+// ---- track access (layout in kernels.h: kTB-bit counts, kPerByte per byte) ----
 __device__ __forceinline__ gu8 *track_u8(const UnitDesc &U, int S, int strand, int sample) {
     return (gu8 *)U.base + ((uint64_t)strand * S + sample) * U.stride;
 }
 
-// nibble (stored count, escape 15) of position p, 1-based
-__device__ __forceinline__ uint32_t nib_at(gu8 *t, int64_t p) {
-    const int64_t n = kPadPos + p - 1;
-    return ((uint32_t)t[n >> 1] >> (4 * (uint32_t)(n & 1))) & 15u;
+// byte and bit offset of field n (n = kPadPos + p - 1 for position p)
+__host__ __device__ __forceinline__ int64_t fbyte(int64_t n) { return n >> kLogPerByte; }
+__host__ __device__ __forceinline__ uint32_t fshift(int64_t n) {
+    return (uint32_t)kTB * (uint32_t)(n & (kPerByte - 1));
 }
 
-// sum of the eight 4-bit counts of a dword (v_dot8_u32_u4 against all-ones)
-__device__ __forceinline__ uint32_t nsum8(uint32_t x, uint32_t acc) {
-    return __builtin_amdgcn_udot8(x, 0x11111111u, acc, false);
+// stored field (count, or the escape kEsc) of position p, 1-based
+__device__ __forceinline__ uint32_t fld_at(gu8 *t, int64_t p) {
+    const int64_t n = kPadPos + p - 1;
+    return ((uint32_t)t[fbyte(n)] >> fshift(n)) & kTMask;
+}
+
+// sum of the fields of a dword (escapes count as kEsc)
+__device__ __forceinline__ uint32_t fsum32(uint32_t x, uint32_t acc) {
+    if constexpr (kTB == 4) {
+        return __builtin_amdgcn_udot8(x, 0x11111111u, acc, false);  // v_dot8_u32_u4 x all-ones
+    } else {
+        return acc + (uint32_t)__builtin_popcount(x & 0x55555555u) +
+               2u * (uint32_t)__builtin_popcount(x & 0xAAAAAAAAu);
+    }
+}
+
+// bits of a dword that make the screen treat a chunk as exact: any escaped
+// field (2-bit: a field of 3; 4-bit: any count >= 8, the escape 15 among them)
+__device__ __forceinline__ uint32_t fbig32(uint32_t x) {
+    if constexpr (kTB == 4) return x & 0x88888888u;
+    else return x & (x >> 1) & 0x55555555u;
 }
 
 // escaped count (>= 15): binary search of the entries of the position's
@@ -133,7 +151,7 @@ __device__ __forceinline__ void resolve_escapes(uint32_t (&c)[N], const UnitDesc
 // exact count of (strand, sample) at position p (1-based)
 __device__ __forceinline__ uint32_t count_at(const UnitDesc &U, int S, int strand, int sample,
                                              int64_t p) {
-    const uint32_t b = nib_at(track_u8(U, S, strand, sample), p);
+    const uint32_t b = fld_at(track_u8(U, S, strand, sample), p);
     return b == kEsc ? ovf_lookup(U, (uint32_t)(strand * S + sample), (uint32_t)p) : b;
 }
 
@@ -147,14 +165,14 @@ __device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], const UnitDesc &
                                            const double *coef) {
     uint32_t c[N];
     auto fetch = [&](int k) {
-        // lane's nibble n0 + 64w = byte (n0 >> 1) + 32w, same half for every w
+        // lane's field n0 + 64w = byte fbyte(n0) + kWordBytes * w, same bits for every w
         const int64_t n0 = kPadPos + x0 - 1 + lane;
-        gu8 *t = track_u8(U, S, strand, nc[k]) + (n0 >> 1);
-        const uint32_t sh = 4 * (uint32_t)(n0 & 1);
+        gu8 *t = track_u8(U, S, strand, nc[k]) + fbyte(n0);
+        const uint32_t sh = fshift(n0);
 #pragma unroll
-        for (int w = 0; w < N; ++w) c[w] = t[32 * w];
+        for (int w = 0; w < N; ++w) c[w] = t[kWordBytes * w];
 #pragma unroll
-        for (int w = 0; w < N; ++w) c[w] = (c[w] >> sh) & 15u;
+        for (int w = 0; w < N; ++w) c[w] = (c[w] >> sh) & kTMask;
         resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[k]), x0, lane);
     };
     if constexpr (POOL == 0) {
@@ -231,32 +249,34 @@ __device__ __forceinline__ void next_hits(uint64_t &m, T v, int (&b)[kHB], doubl
     }
 }
 
-// Same as load_words, but the N*32 bytes of each track are fetched with
-// 16-byte lane loads (one 1 KiB wave load per 32 words) and turned into the
-// lane = position layout through this wave's LDS stage (N*32 <= 1024 bytes).
-// x0 - 1 must be a multiple of 64 (the bytes are then 16-byte aligned).
+// Same as load_words, but the N*kWordBytes bytes of each track are fetched
+// with 16-byte lane loads (one 1 KiB wave load per 1024/kWordBytes words) and
+// turned into the lane = position layout through this wave's LDS stage
+// (N*kWordBytes <= 1024 bytes).  x0 - 1 must be a multiple of 64 (the bytes
+// are then 16-byte aligned).
 template <int N, int POOL>
 __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const UnitDesc &U, int S, int strand,
                                                   int64_t x0, int lane, int nnc, const int32_t *nc,
                                                   const double *coef, uint8_t *stage) {
-    constexpr int NV = (N * 32 + 1023) / 1024;  // wave loads per track
+    constexpr int NL = N * kWordBytes / 16;    // 16-byte lane loads per track
+    constexpr int NV = (NL + 63) / 64;           // wave loads per track
     uint32_t c[N];
     auto fetch = [&](int k) {
-        gu32x4 *t = (gu32x4 *)(track_u8(U, S, strand, nc[k]) + ((kPadPos + x0 - 1) >> 1));
+        gu32x4 *t = (gu32x4 *)(track_u8(U, S, strand, nc[k]) + fbyte(kPadPos + x0 - 1));
         u32x4 v[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q)
-            if (64 * q + lane < N * 2) v[q] = t[64 * q + lane];
+            if (64 * q + lane < NL) v[q] = t[64 * q + lane];
         __builtin_amdgcn_wave_barrier();  // earlier readers of the stage are done
 #pragma unroll
         for (int q = 0; q < NV; ++q)
-            if (64 * q + lane < N * 2) *(u32x4 *)(stage + 16 * (64 * q + lane)) = v[q];
+            if (64 * q + lane < NL) *(u32x4 *)(stage + 16 * (64 * q + lane)) = v[q];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t sh = 4 * (uint32_t)(lane & 1);
+        const uint32_t sh = fshift(lane);
 #pragma unroll
-        for (int w = 0; w < N; ++w) c[w] = ((uint32_t)stage[32 * w + (lane >> 1)] >> sh) & 15u;
+        for (int w = 0; w < N; ++w) c[w] = ((uint32_t)stage[kWordBytes * w + fbyte(lane)] >> sh) & kTMask;
         resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[k]), x0, lane);
     };
     if constexpr (POOL == 0) {
@@ -738,81 +758,107 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 
         // ---- screen: which blocks can hold a flagged position ----
         if constexpr (!PROF && MODE != kModeExact) {
-            // lane l of wave load q holds positions 2048q + 32l .. +31, i.e.
-            // chunks 128q + 2l (dwords x, y) and 128q + 2l + 1 (dwords z, w)
-            uint32_t cs[2 * kLoads];
-            uint32_t big = 0, hs0 = 0, hs1 = 0, hbig = 0, anybig = 0;
+            // lane l of wave load q holds 16 bytes = CPL chunks: chunks
+            // CPL * (64q + l) + i, i < CPL (DPC dwords each)
+            constexpr int CPL = 16 / kChunkBytes, DPC = kChunkBytes / 4;
+            constexpr int HL = 8 * kChunkBytes / 16;  // halo lane loads per side (8 chunks)
+            uint32_t cs[CPL * kLoads];
+            uint32_t big = 0, hs[CPL], hbig = 0, anybig = 0;
 #pragma unroll
-            for (int k = 0; k < 2 * kLoads; ++k) cs[k] = 0;
+            for (int k = 0; k < CPL * kLoads; ++k) cs[k] = 0;
+#pragma unroll
+            for (int i = 0; i < CPL; ++i) hs[i] = 0;
             for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
                 for (int k = 0; k < P.nnc; ++k) {
-                    gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, ncs[k]) + ((kPadPos + p0 - 1) >> 1));
+                    gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, ncs[k]) + fbyte(kPadPos + p0 - 1));
                     u32x4 v[kLoads];
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) v[q] = __builtin_nontemporal_load(t + 64 * q + lane);
-                    // halos: 8 chunks (64 bytes) on each side, two per lane
+                    // halos: 8 chunks on each side, HL lanes per side
                     u32x4 hv = {0u, 0u, 0u, 0u};
-                    if (lane < 8) hv = t[lane < 4 ? lane - 4 : kLoads * kWave + lane - 4];
+                    if (lane < 2 * HL) hv = t[lane < HL ? lane - HL : kLoads * kWave + lane - HL];
                     const uint32_t w = POOL == 2 ? cptr(P.wscreen)[k] : 1u;
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
-                        const uint32_t a = nsum8(v[q].y, nsum8(v[q].x, 0u));
-                        const uint32_t b = nsum8(v[q].w, nsum8(v[q].z, 0u));
-                        cs[2 * q] += POOL == 2 ? a * w : a;
-                        cs[2 * q + 1] += POOL == 2 ? b * w : b;
-                        anybig |= v[q].x | v[q].y | v[q].z | v[q].w;
+                        const uint32_t d[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                        for (int i = 0; i < CPL; ++i) {
+                            uint32_t a = 0;
+#pragma unroll
+                            for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
+                            cs[CPL * q + i] += POOL == 2 ? a * w : a;
+                        }
+                        anybig |= fbig32(d[0]) | fbig32(d[1]) | fbig32(d[2]) | fbig32(d[3]);
                     }
-                    const uint32_t ha = nsum8(hv.y, nsum8(hv.x, 0u)), hb = nsum8(hv.w, nsum8(hv.z, 0u));
-                    hs0 += POOL == 2 ? ha * w : ha;
-                    hs1 += POOL == 2 ? hb * w : hb;
-                    anybig |= hv.x | hv.y | hv.z | hv.w;
+                    {
+                        const uint32_t d[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+                        for (int i = 0; i < CPL; ++i) {
+                            uint32_t a = 0;
+#pragma unroll
+                            for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
+                            hs[i] += POOL == 2 ? a * w : a;
+                        }
+                        anybig |= fbig32(d[0]) | fbig32(d[1]) | fbig32(d[2]) | fbig32(d[3]);
+                    }
                 }
             }
-            // A count >= 8 -- the escape nibble 15 among them, whose true count
-            // the screen does not know -- makes its chunk exact (kBig).  Rare:
-            // the strip is re-read (L2) for the per-chunk bits only when some
-            // lane saw such a nibble.
-            if (__ballot((anybig & 0x88888888u) != 0u) != 0) {
+            // A chunk holding an escaped field (4-bit: a count >= 8, the
+            // escape among them), whose true count the screen does not know,
+            // goes exact (kBig).  Rare: the strip is re-read (L2) for the
+            // per-chunk bits only when some lane saw such a field.
+            if (__ballot(anybig != 0u) != 0) {
                 for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
                     for (int k = 0; k < P.nnc; ++k) {
-                        gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, ncs[k]) + ((kPadPos + p0 - 1) >> 1));
+                        gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, ncs[k]) + fbyte(kPadPos + p0 - 1));
 #pragma unroll 2
                         for (int q = 0; q < kLoads; ++q) {
                             const u32x4 x = t[64 * q + lane];
-                            big |= (((x.x | x.y) & 0x88888888u) ? 1u : 0u) << (2 * q);
-                            big |= (((x.z | x.w) & 0x88888888u) ? 1u : 0u) << (2 * q + 1);
+                            const uint32_t d[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                            for (int i = 0; i < CPL; ++i) {
+                                uint32_t b = 0;
+#pragma unroll
+                                for (int j = 0; j < DPC; ++j) b |= fbig32(d[DPC * i + j]);
+                                big |= (b ? 1u : 0u) << (CPL * q + i);
+                            }
                         }
-                        if (lane < 8) {
-                            const u32x4 x = t[lane < 4 ? lane - 4 : kLoads * kWave + lane - 4];
-                            hbig |= ((x.x | x.y) & 0x88888888u) ? 1u : 0u;
-                            hbig |= ((x.z | x.w) & 0x88888888u) ? 2u : 0u;
+                        if (lane < 2 * HL) {
+                            const u32x4 x = t[lane < HL ? lane - HL : kLoads * kWave + lane - HL];
+                            const uint32_t d[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                            for (int i = 0; i < CPL; ++i) {
+                                uint32_t b = 0;
+#pragma unroll
+                                for (int j = 0; j < DPC; ++j) b |= fbig32(d[DPC * i + j]);
+                                hbig |= (b ? 1u : 0u) << i;
+                            }
                         }
                     }
                 }
             }
-            // a chunk holding a count >= 8 (incl. the escape) goes exact
 #ifdef UPK_EXP_K1A_LOADONLY  // timing experiment: stream + chunk sums only
             if constexpr (MODE == kModeScreen) {
                 uint32_t t = big;
 #pragma unroll
-                for (int q = 0; q < 2 * kLoads; ++q) t += cs[q];
+                for (int q = 0; q < CPL * kLoads; ++q) t += cs[q];
                 const uint64_t info = ((uint64_t)(local == 0) << 34) | ((uint64_t)(local + 1 == U.nstrips) << 35) |
                                       ((uint64_t)(__ballot(t == 0xDEADBEEFu) != 0) << 40);
                 if (lane == 0) P.strip_info[strip] = info;
                 continue;
             }
 #endif
-            // (an even index and the next one share a 16-word group: adjacent words)
+            // (a lane's CPL chunks never straddle a pad word: CPL divides 16)
 #pragma unroll
             for (int q = 0; q < kLoads; ++q) {
-                uint32_t *d = scr + scr_at(8 + 128 * q + 2 * lane);
-                d[0] = ((big >> (2 * q)) & 1u) ? kBig : cs[2 * q];
-                d[1] = ((big >> (2 * q + 1)) & 1u) ? kBig : cs[2 * q + 1];
+                uint32_t *d = scr + scr_at(8 + kWave * CPL * q + CPL * lane);
+#pragma unroll
+                for (int i = 0; i < CPL; ++i) d[i] = ((big >> (CPL * q + i)) & 1u) ? kBig : cs[CPL * q + i];
             }
-            if (lane < 8) {
-                uint32_t *d = scr + scr_at(lane < 4 ? 2 * lane : 8 + kBlocks * kWave + 2 * (lane - 4));
-                d[0] = (hbig & 1u) ? kBig : hs0;
-                d[1] = (hbig & 2u) ? kBig : hs1;
+            if (lane < 2 * HL) {
+                uint32_t *d = scr + scr_at(lane < HL ? CPL * lane : 8 + kBlocks * kWave + CPL * (lane - HL));
+#pragma unroll
+                for (int i = 0; i < CPL; ++i) d[i] = ((hbig >> i) & 1u) ? kBig : hs[i];
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1374,10 +1420,10 @@ __global__ void __launch_bounds__(kSegBlock) seg_compact_kernel(
 }
 
 // per-unit last add (the last position whose pooled count is nonzero): one
-// wave per strip finds its highest nonzero byte over the pooled tracks and
+// wave per strip finds its highest nonzero field over the pooled tracks and
 // folds it into the unit's slot with atomicMax (out zeroed by the caller)
-__device__ __forceinline__ uint32_t top_nib(uint32_t x) {  // index of highest nonzero nibble
-    return (uint32_t)(31 - __builtin_clz(x)) >> 2;
+__device__ __forceinline__ uint32_t top_fld(uint32_t x) {  // index of the highest nonzero field
+    return (uint32_t)(31 - __builtin_clz(x)) / (uint32_t)kTB;
 }
 
 __global__ void __launch_bounds__(256) unit_last_kernel(const UnitDesc *units, uint32_t nunits,
@@ -1397,16 +1443,17 @@ __global__ void __launch_bounds__(256) unit_last_kernel(const UnitDesc *units, u
         uint32_t best = 0;
         for (int st = 0; st < U.nstrands; ++st)
             for (int k = 0; k < nnc; ++k) {
-                gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, nc[k]) + ((kPadPos + p0 - 1) >> 1));
+                gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, nc[k]) + fbyte(kPadPos + p0 - 1));
+                constexpr int PD = 4 * kPerByte;  // positions per dword
 #pragma unroll 4
                 for (int bk = 0; bk < kStripBytes / (kWave * 16); ++bk) {
                     const u32x4 v = __builtin_nontemporal_load(t + 64 * bk + lane);
-                    const int64_t q = p0 + 2048 * bk + 32 * lane;  // position of the lane's first nibble
+                    const int64_t q = p0 + 64 * 4 * PD * bk + 4 * PD * lane;  // the lane's first position
                     uint32_t hi = 0;
-                    if (v.x) hi = (uint32_t)q + top_nib(v.x);
-                    if (v.y) hi = (uint32_t)q + 8 + top_nib(v.y);
-                    if (v.z) hi = (uint32_t)q + 16 + top_nib(v.z);
-                    if (v.w) hi = (uint32_t)q + 24 + top_nib(v.w);
+                    if (v.x) hi = (uint32_t)q + top_fld(v.x);
+                    if (v.y) hi = (uint32_t)q + PD + top_fld(v.y);
+                    if (v.z) hi = (uint32_t)q + 2 * PD + top_fld(v.z);
+                    if (v.w) hi = (uint32_t)q + 3 * PD + top_fld(v.w);
                     best = hi > best ? hi : best;
                 }
             }
@@ -1505,10 +1552,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
         uint32_t nf[NWT], nr[NONDIR ? NWT : 1];
         auto fetch_raw = [&](uint32_t (&dst)[NWT], int strand, int64_t x0) {
             const int64_t n0 = kPadPos + (x0 - 64 * NH) - 1 + lane;
-            gu8 *t = track_u8(U, S, strand, P.nc[0]) + (n0 >> 1);
-            const uint32_t sh = 4 * (uint32_t)(n0 & 1);
+            gu8 *t = track_u8(U, S, strand, P.nc[0]) + fbyte(n0);
+            const uint32_t sh = fshift(n0);
 #pragma unroll
-            for (int w = 0; w < NWT; ++w) dst[w] = ((uint32_t)t[32 * w] >> sh) & 15u;
+            for (int w = 0; w < NWT; ++w) dst[w] = ((uint32_t)t[kWordBytes * w] >> sh) & kTMask;
         };
         uint32_t kpos = 0;
         double kval = 0.0;
@@ -1559,10 +1606,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
         WinT<POOL> pkf[kPK], pkr[NONDIR ? kPK : 1];
         if (POOL == 0 && kn && P.qmode) {
             if (kPrefetch && pk_pre && pk_pos == kpos) {  // fetched during the previous region
-                const uint32_t sh = 4 * (uint32_t)((kPadPos + (int64_t)kpos - bw - 1 + lane) & 1);
+                const uint32_t sh = fshift(kPadPos + (int64_t)kpos - bw - 1 + lane);
                 uint32_t c[kPrefetch ? 2 * NH : 1];
 #pragma unroll
-                for (int w = 0; w < (kPrefetch ? 2 * NH : 1); ++w) c[w] = (pkraw[w] >> sh) & 15u;
+                for (int w = 0; w < (kPrefetch ? 2 * NH : 1); ++w) c[w] = (pkraw[w] >> sh) & kTMask;
                 resolve_escapes<kPrefetch ? 2 * NH : 1>(c, U, (uint32_t)P.nc[0], (int64_t)kpos - bw, lane);
 #pragma unroll
                 for (int w = 0; w < (kPrefetch ? 2 * NH : 1); ++w) pkf[w] = c[w];
@@ -1583,25 +1630,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 best = kval;
                 best_x = kpos;
                 const int64_t n0 = kPadPos + (int64_t)left - 1 + lane;
-                const uint32_t sh = 4 * (uint32_t)(n0 & 1);
-                gu8 *t0 = track_u8(U, S, 0, P.nc[0]) + (n0 >> 1);
+                const uint32_t sh = fshift(n0);
+                gu8 *t0 = track_u8(U, S, 0, P.nc[0]) + fbyte(n0);
                 uint32_t r0[kStatCache], r1[NONDIR ? kStatCache : 1];
                 if (kPrefetch && pre_ok) {
 #pragma unroll
                     for (int w = 0; w < kStatCache; ++w) r0[w] = praw[kPrefetch ? w : 0];
                 } else {
 #pragma unroll
-                    for (int w = 0; w < kStatCache; ++w) r0[w] = w < nw ? t0[32 * w] : 0u;
+                    for (int w = 0; w < kStatCache; ++w) r0[w] = w < nw ? t0[kWordBytes * w] : 0u;
                 }
                 if constexpr (NONDIR) {
-                    gu8 *t1 = track_u8(U, S, 1, P.nc[0]) + (n0 >> 1);
+                    gu8 *t1 = track_u8(U, S, 1, P.nc[0]) + fbyte(n0);
 #pragma unroll
-                    for (int w = 0; w < kStatCache; ++w) r1[w] = w < nw ? t1[32 * w] : 0u;
+                    for (int w = 0; w < kStatCache; ++w) r1[w] = w < nw ? t1[kWordBytes * w] : 0u;
                 }
 #pragma unroll
                 for (int w = 0; w < kStatCache; ++w) {
-                    r0[w] = (r0[w] >> sh) & 15u;
-                    if constexpr (NONDIR) r1[w] = (r1[w] >> sh) & 15u;
+                    r0[w] = (r0[w] >> sh) & kTMask;
+                    if constexpr (NONDIR) r1[w] = (r1[w] >> sh) & kTMask;
                 }
                 resolve_escapes<kStatCache>(r0, U, (uint32_t)P.nc[0], (int64_t)left, lane);
                 if constexpr (NONDIR) resolve_escapes<kStatCache>(r1, U, (uint32_t)(S + P.nc[0]), (int64_t)left, lane);
@@ -1827,9 +1874,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 const int nwn = (int)((rgn - ln) / 64u) + 1;
                 if (nwn <= kStatCache) {
                     const UnitDesc Un = P.units[rl_u(dsc_n, 2)];
-                    gu8 *tn = track_u8(Un, S, 0, P.nc[0]) + ((kPadPos + (int64_t)ln - 1 + lane) >> 1);
+                    gu8 *tn = track_u8(Un, S, 0, P.nc[0]) + fbyte(kPadPos + (int64_t)ln - 1 + lane);
 #pragma unroll
-                    for (int w = 0; w < kStatCache; ++w) praw[w] = w < nwn ? tn[32 * w] : 0u;
+                    for (int w = 0; w < kStatCache; ++w) praw[w] = w < nwn ? tn[kWordBytes * w] : 0u;
                     pre_ok = true;
                 }
             }
@@ -1840,9 +1887,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 pk_pos = rl_u(dsc_n, 3);
                 const UnitDesc Un = P.units[rl_u(dsc_n, 2)];
                 const int64_t n0 = kPadPos + (int64_t)pk_pos - bw - 1 + lane;
-                gu8 *tp = track_u8(Un, S, 0, P.nc[0]) + (n0 >> 1);
+                gu8 *tp = track_u8(Un, S, 0, P.nc[0]) + fbyte(n0);
 #pragma unroll
-                for (int w = 0; w < (kPrefetch ? 2 * NH : 1); ++w) pkraw[w] = tp[32 * w];
+                for (int w = 0; w < (kPrefetch ? 2 * NH : 1); ++w) pkraw[w] = tp[kWordBytes * w];
                 pk_pre = true;
             }
         }
@@ -2138,43 +2185,45 @@ __global__ void __launch_bounds__(kShiftThreads) shift_kernel(StatParams P, cons
 // ------------------------------------------------------------------------
 // aux kernels
 // ------------------------------------------------------------------------
-// host pairs -> one 4-bit track (counts >= 15 become the escape nibble; the
-// host keeps their values in the unit's overflow table).  Two positions share
-// a byte, so each pair clears and sets its own nibble of the dword with
+// host pairs -> one track (counts >= kEsc become the escape field; the host
+// keeps their values in the unit's overflow table).  kPerByte positions share
+// a byte, so each pair clears and sets its own field of the dword with
 // atomics on disjoint bits (positions within one call are unique).
 __global__ void scatter_kernel(uint8_t *track, const uint32_t *__restrict__ pos,
                                const uint32_t *__restrict__ cnt, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint64_t nb = kPadPos + (uint64_t)pos[i] - 1;        // nibble index
-    uint32_t *word = (uint32_t *)(track + ((nb >> 1) & ~3ull));  // its aligned dword
-    const uint32_t sh = 4 * (uint32_t)(nb & 7);
+    const uint64_t nb = kPadPos + (uint64_t)pos[i] - 1;                  // field index
+    uint32_t *word = (uint32_t *)(track + ((uint64_t)fbyte(nb) & ~3ull));  // its aligned dword
+    const uint32_t sh = (uint32_t)kTB * (uint32_t)(nb & (4 * kPerByte - 1));
     const uint32_t c = cnt[i] >= kEsc ? kEsc : cnt[i];
-    atomicAnd(word, ~(15u << sh));
+    atomicAnd(word, ~(kTMask << sh));
     if (c) atomicOr(word, c << sh);
 }
 
-// dense device uint32 counts (position p at src[p-1]) -> 4-bit track;
-// counts >= 15 are appended to an overflow list (pos << 32 | count)
+// dense device uint32 counts (position p at src[p-1]) -> one track, one
+// dword (4 * kPerByte positions) per thread; counts >= kEsc are appended to
+// an overflow list (pos << 32 | count)
 __global__ void pack_kernel(uint8_t *track, const uint32_t *__restrict__ src, uint64_t len,
                             unsigned long long *ovf, uint32_t *novf, uint32_t cap) {
-    const uint64_t i8 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-    if (i8 >= len) return;
+    constexpr int PD = 4 * kPerByte;
+    const uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * PD;
+    if (i0 >= len) return;
     uint32_t out = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint64_t i = i8 + k;
+    for (int k = 0; k < PD; ++k) {
+        const uint64_t i = i0 + k;
         uint32_t c = i < len ? src[i] : 0u;
         if (c >= kEsc) {
             const uint32_t slot = atomicAdd(novf, 1u);
             if (slot < cap) ovf[slot] = ((unsigned long long)(i + 1) << 32) | c;
             c = kEsc;
         }
-        out |= c << (4 * k);
+        out |= c << (kTB * k);
     }
-    // kPadPos and p-1 = i8 are multiples of 8: one aligned dword store (the
-    // nibbles past len are zero, and the track extends past len + kMaxBw)
-    *(uint32_t *)(track + ((kPadPos + i8) >> 1)) = out;
+    // kPadPos and p-1 = i0 are multiples of PD: one aligned dword store (the
+    // fields past len are zero, and the track extends past len + kMaxBw)
+    *(uint32_t *)(track + fbyte(kPadPos + (int64_t)i0)) = out;
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -2202,8 +2251,8 @@ __global__ void synth_bg_kernel(uint32_t *stage, uint64_t tkey, int64_t lo, int6
     stage[x + offset - 1] = c;
 }
 
-// sum of a 4-bit track's counts, escapes excluded (their counts are added on
-// the host from the overflow table)
+// sum of a track's counts, escapes excluded (their counts are added on the
+// host from the overflow table)
 __global__ void track_sum_kernel(const uint8_t *__restrict__ t, uint64_t n, unsigned long long *out) {
     uint64_t acc = 0;
     const u32x4 *v = (const u32x4 *)t;
@@ -2214,8 +2263,9 @@ __global__ void track_sum_kernel(const uint8_t *__restrict__ t, uint64_t n, unsi
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t y = w[k];
-            const uint32_t esc = y & (y >> 1) & (y >> 2) & (y >> 3) & 0x11111111u;  // nibbles == 15
-            acc += nsum8(y, 0u) - kEsc * (uint32_t)__builtin_popcount(esc);
+            const uint32_t esc = kTB == 4 ? y & (y >> 1) & (y >> 2) & (y >> 3) & 0x11111111u  // fields == 15
+                                          : y & (y >> 1) & 0x55555555u;                     // fields == 3
+            acc += fsum32(y, 0u) - kEsc * (uint32_t)__builtin_popcount(esc);
         }
     }
     __shared__ unsigned long long red[256];
