@@ -723,6 +723,40 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     // K1b phase clocks of this wave (s_memtime), added up once at the end
     uint64_t dt_item = 0, dt_load = 0, dt_scat = 0, dt_flag = 0, n_items = 0;
 #endif
+    // K1a software pipeline: the loads of this wave's next (strip, track) --
+    // strips it0, it0 + istep, ...; tracks (strand, pooled sample) in order --
+    // are issued before the current one is reduced, so two tracks' bytes are
+    // in flight per wave instead of one (the stream is latency-bound at the
+    // two waves per SIMD K1a keeps, launch_scan)
+#ifdef UPK_NO_K1A_PF  // A/B: each track's loads issued right before it is reduced
+    constexpr bool kPf = false;
+#else
+    constexpr bool kPf = true;
+#endif
+    constexpr int HL_ = 8 * kChunkBytes / 16;  // halo lane loads per side (8 chunks)
+    u32x4 pv[MODE == kModeScreen && !PROF ? kLoads : 1];
+    u32x4 phv = {0u, 0u, 0u, 0u};
+    uint32_t pf_strip = 0, pf_cur = 0;
+    int pf_st = 0, pf_k = 0;
+    bool pf_ok = false;
+    auto pf_issue = [&](uint32_t strip_n, uint32_t cur_n, int st, int k) {
+        const UnitDesc Un = units[cur_n];
+        const int64_t q0 = 1 + (int64_t)(strip_n - Un.strip0) * kStrip;
+        gu32x4 *t = (gu32x4 *)(track_u8(Un, S, st, ncs[k]) + fbyte(kPadPos + q0 - 1));
+#pragma unroll
+        for (int q = 0; q < (MODE == kModeScreen && !PROF ? kLoads : 1); ++q)
+            pv[q] = __builtin_nontemporal_load(t + 64 * q + lane);
+        phv = u32x4{0u, 0u, 0u, 0u};
+        if (lane < 2 * HL_) phv = t[lane < HL_ ? lane - HL_ : kLoads * kWave + lane - HL_];
+        pf_strip = strip_n;
+        pf_cur = cur_n;
+        pf_st = st;
+        pf_k = k;
+        pf_ok = true;
+    };
+    if constexpr (MODE == kModeScreen && !PROF && kPf) {
+        if (it0 < it_end) pf_issue(it0, find_unit(units, P.nunits, it0), 0, 0);
+    }
     for (uint32_t it = it0; it < it_end; it += istep) {
 #ifdef UPK_DEBUG_TIMES
         const uint64_t t_it0 = __builtin_amdgcn_s_memtime();
@@ -770,13 +804,25 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             for (int i = 0; i < CPL; ++i) hs[i] = 0;
             for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
                 for (int k = 0; k < P.nnc; ++k) {
-                    gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, ncs[k]) + fbyte(kPadPos + p0 - 1));
+                    // this track's loads were issued one step ahead (pf_issue);
+                    // issue the next (strip, track)'s before reducing these
+                    if (!kPf) pf_issue(it, cur, st, k);
                     u32x4 v[kLoads];
 #pragma unroll
-                    for (int q = 0; q < kLoads; ++q) v[q] = __builtin_nontemporal_load(t + 64 * q + lane);
+                    for (int q = 0; q < kLoads; ++q) v[q] = pv[q];
                     // halos: 8 chunks on each side, HL lanes per side
-                    u32x4 hv = {0u, 0u, 0u, 0u};
-                    if (lane < 2 * HL) hv = t[lane < HL ? lane - HL : kLoads * kWave + lane - HL];
+                    const u32x4 hv = phv;
+                    pf_ok = false;
+                    if (!kPf) {
+                    } else if (k + 1 < P.nnc) {
+                        pf_issue(it, cur, st, k + 1);
+                    } else if (st + 1 < (NONDIR ? 2 : 1)) {
+                        pf_issue(it, cur, st + 1, 0);
+                    } else if (it + istep < it_end) {
+                        uint32_t nc_ = cur;
+                        while (it + istep >= units[nc_].strip0 + units[nc_].nstrips) ++nc_;
+                        pf_issue(it + istep, nc_, 0, 0);
+                    }
                     const uint32_t w = POOL == 2 ? cptr(P.wscreen)[k] : 1u;
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
