@@ -498,19 +498,6 @@ __device__ __forceinline__ double wave_max_d(double v) {
 template <int NH, int SW, int W, typename A>
 __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], const double (&c)[kHB],
                                              int lane, int bw, const double *ktab, uint32_t live) {
-#ifdef UPK_EXP_SCATTER_PERWORD
-    WordLoop<W - NH, W + NH + 1>::run([&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        if constexpr (t >= NH && t < NH + SW) {
-            if (!((live >> (t - NH)) & 1u)) return;  // uniform: word holds no flag
-            double kv[kHB];
-#pragma unroll
-            for (int h = 0; h < kHB; ++h) kv[h] = ktab[lane + bw - b[h] + 64 * (t - W)];
-#pragma unroll
-            for (int h = 0; h < kHB; ++h) acc[t - NH] = acc[t - NH] + kv[h] * c[h];
-        }
-    });
-#else
     // Every weight read of the batch -- all output words in reach, live or
     // not (the padded table keeps every index valid) -- is issued before the
     // first multiply, so one LDS latency is paid per batch instead of one per
@@ -527,9 +514,6 @@ __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], 
     for (int h = 0; h < kHB; ++h) base[h] = lane + bw - b[h];
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
-#ifdef UPK_EXP_LIVEREADS
-        if (!((live >> (T0 + q - NH)) & 1u)) continue;  // uniform: no reads for a dead word
-#endif
 #pragma unroll
         for (int h = 0; h < kHB; ++h) kv[q][h] = vk[base[h] + 64 * (T0 + q - W)];  // 0 outside
     }
@@ -541,7 +525,6 @@ __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], 
 #pragma unroll
         for (int h = 0; h < kHB; ++h) acc[t - NH] = acc[t - NH] + kv[q][h] * c[h];
     });
-#endif
 }
 
 // ------------------------------------------------------------------------
@@ -600,23 +583,6 @@ __device__ __forceinline__ uint32_t screen_bits(const uint32_t *rd, uint32_t wsk
 #pragma unroll
     for (int j = 0; j < 16 + 2 * R; ++j) tot += a[j];
     if (__ballot(tot > wskip) == 0) return 0u;
-#ifdef UPK_EXP_NOFINE  // timing experiment (wrong results): no fine screen
-    if (tot != 0xDEADBEEFu) return 0u;
-#endif
-#ifdef UPK_EXP_INTSCREEN  // A/B: the integer kmax * window-sum bound only
-    {
-        uint32_t W = 0;
-#pragma unroll
-        for (int j = 0; j <= 2 * R; ++j) W += a[j];
-        uint32_t m = W > wskip ? 1u : 0u;
-#pragma unroll
-        for (int i = 1; i < 16; ++i) {
-            W += a[i + 2 * R] - a[i - 1];
-            m |= (W > wskip ? 1u : 0u) << i;
-        }
-        return m;
-    }
-#endif
     float f[16 + 2 * R];
 #pragma unroll
     for (int j = 0; j < 16 + 2 * R; ++j) f[j] = (float)a[j];  // exact: sums < 2^24
@@ -711,14 +677,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     uint32_t it_end = MODE == kModeExact ? nfront + nback : strip_end;
     uint32_t xnf = 0, xnb = 0;  // K1a: entries this wave stashed (front / back)
     uint32_t it0 = (MODE == kModeExact ? 0u : strip_begin) + wave, istep = nwaves;
-#ifdef UPK_EXP_CONTIG
-    if constexpr (MODE == kModeExact) {  // contiguous item ranges per wave (locality experiment)
-        const uint32_t per = (it_end + nwaves - 1) / nwaves;
-        it0 = wave * per;
-        it_end = it0 + per < it_end ? it0 + per : it_end;
-        istep = 1;
-    }
-#endif
 #ifdef UPK_DEBUG_TIMES
     // K1b phase clocks of this wave (s_memtime), added up once at the end
     uint64_t dt_item = 0, dt_load = 0, dt_scat = 0, dt_flag = 0, n_items = 0;
@@ -849,6 +807,63 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     }
                 }
             }
+            // Register pre-screen (no LDS): group g = lane l of load q holds
+            // CPL chunks; every chunk's window of +-R chunks lies in groups
+            // g-D .. g+D (D = ceil(R / CPL) <= 2), so the tag sum of those
+            // groups (neighbours by wave_shr/wave_shl DPP, across loads by
+            // readlane) plus both halos bounds it.  Background strips -- most
+            // of the genome -- end here; the others (and any escaped field,
+            // whose count the screen does not know) take the LDS screen below.
+            bool clean = false;
+#ifndef UPK_NO_K1A_DPP
+            if constexpr (MODE == kModeScreen) {
+                const int D = (R + CPL - 1) / CPL;
+                if (D <= 2 && __ballot(anybig != 0u) == 0) {
+                    uint32_t T[kLoads];
+#pragma unroll
+                    for (int q = 0; q < kLoads; ++q) {
+                        T[q] = 0;
+#pragma unroll
+                        for (int i = 0; i < CPL; ++i) T[q] += cs[CPL * q + i];
+                    }
+                    uint32_t hl = 0;
+#pragma unroll
+                    for (int i = 0; i < CPL; ++i) hl += hs[i];
+                    uint32_t htot = 0;  // both halos (lanes 0 .. 2HL-1)
+#pragma unroll
+                    for (int l = 0; l < 2 * HL; ++l) htot += rl_u(hl, l);
+                    uint32_t l1[kLoads], r1[kLoads], bmax = 0;
+#pragma unroll
+                    for (int q = 0; q < kLoads; ++q) {
+                        l1[q] = dpp32<0x138, 0xf, false>(0u, T[q]);  // wave_shr:1 -> T(g - 1)
+                        r1[q] = dpp32<0x130, 0xf, false>(0u, T[q]);  // wave_shl:1 -> T(g + 1)
+                        const uint32_t lf = q > 0 ? rl_u(T[q > 0 ? q - 1 : 0], 63) : 0u;
+                        const uint32_t rf = q + 1 < kLoads ? rl_u(T[q + 1 < kLoads ? q + 1 : q], 0) : 0u;
+                        l1[q] = lane == 0 ? lf : l1[q];
+                        r1[q] = lane == 63 ? rf : r1[q];
+                    }
+#pragma unroll
+                    for (int q = 0; q < kLoads; ++q) {
+                        uint32_t b = T[q] + l1[q] + r1[q];
+                        if (D == 2) {
+                            uint32_t l2 = dpp32<0x138, 0xf, false>(0u, l1[q]);  // T(g - 2)
+                            uint32_t r2 = dpp32<0x130, 0xf, false>(0u, r1[q]);  // T(g + 2)
+                            const uint32_t lf = q > 0 ? rl_u(l1[q > 0 ? q - 1 : 0], 63) : 0u;
+                            const uint32_t rf = q + 1 < kLoads ? rl_u(r1[q + 1 < kLoads ? q + 1 : q], 0) : 0u;
+                            l2 = lane == 0 ? lf : l2;
+                            r2 = lane == 63 ? rf : r2;
+                            b += l2 + r2;
+                        }
+                        bmax = b > bmax ? b : bmax;
+                    }
+                    clean = __ballot(bmax + htot > P.wskip) == 0;
+                }
+            }
+#endif
+            if (clean) {
+                mchunk = 0;
+                exact_blocks = 0;
+            } else {
             // A chunk holding an escaped field (4-bit: a count >= 8, the
             // escape among them), whose true count the screen does not know,
             // goes exact (kBig).  Rare: the strip is re-read (L2) for the
@@ -883,17 +898,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     }
                 }
             }
-#ifdef UPK_EXP_K1A_LOADONLY  // timing experiment: stream + chunk sums only
-            if constexpr (MODE == kModeScreen) {
-                uint32_t t = big;
-#pragma unroll
-                for (int q = 0; q < CPL * kLoads; ++q) t += cs[q];
-                const uint64_t info = ((uint64_t)(local == 0) << 34) | ((uint64_t)(local + 1 == U.nstrips) << 35) |
-                                      ((uint64_t)(__ballot(t == 0xDEADBEEFu) != 0) << 40);
-                if (lane == 0) P.strip_info[strip] = info;
-                continue;
-            }
-#endif
             // (a lane's CPL chunks never straddle a pad word: CPL divides 16)
 #pragma unroll
             for (int q = 0; q < kLoads; ++q) {
@@ -929,10 +933,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 exact_blocks |= ((lanes >> (4 * bk)) & 0xFull) ? (1u << bk) : 0u;
             // the next strip reuses scr only after every lane has read it
             __builtin_amdgcn_wave_barrier();
-#ifdef UPK_EXP_K1A_NOLIST  // timing experiment: no work-list entries (wrong results)
-            if (exact_blocks == 0xFFFFu && lane == 63) P.strip_info[strip] = mchunk;
-            exact_blocks = 0;
-#endif
+            }  // !clean
         }
         if constexpr (MODE == kModeScreen) {
             if (exact_blocks == 0) {  // no run can touch this strip
@@ -1106,9 +1107,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             }
             WordLoop<0, NWIN>::run([&](auto wc) {
                 constexpr int W = decltype(wc)::value;
-#ifdef UPK_EXP_K1B_NOSCATTER  // timing experiment (wrong results)
-                if (hf[W] != 0x5A5A5A5A5A5Aull) return;
-#endif
                 // output words a hit of window word W reaches: W-2NH .. W
                 constexpr int OLO = W - 2 * NH < 0 ? 0 : W - 2 * NH;
                 constexpr int OHI = W > SW - 1 ? SW - 1 : W;
@@ -1189,12 +1187,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     }
                 }
 #endif
-#ifdef UPK_EXP_K1B_NOFLAGS  // timing experiment (wrong results)
-                const uint64_t anyflag = 0;
-                prevF = __ballot(mx == 1.2345) & 1;
-#else
                 const uint64_t anyflag = __ballot(mx >= kthr);
-#endif
                 if (anyflag | prevF) {
                     // scores through LDS so the word loop below stays a loop
                     // (unrolled, its run bookkeeping overflows the I-cache)
@@ -1232,17 +1225,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                         // f+r per lane (Region::addPos, data.cpp:98-101); one
                         // wave reduction when the run closes
                         uint64_t rem = F;
-#ifdef UPK_EXP_NOSEG
-                        rem = 0;
-                        {
-                            uint64_t en = F & ~((F >> 1) | (1ull << 63));
-                            while (en) {
-                                const int b = __builtin_ctzll(en);
-                                en &= en - 1;
-                                rec_end(R_, (uint32_t)(wpos + b), 0u, 0.0, P, strip, lane);
-                            }
-                        }
-#endif
                         while (rem) {
                             const int a = __builtin_ctzll(rem);
                             const uint64_t up = ~(rem >> a);
@@ -1608,11 +1590,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
         if (known) {
             kpos = rl_u(dsc, 3);
             kval = __longlong_as_double((long long)(((uint64_t)rl_u(dsc, 5) << 32) | rl_u(dsc, 4)));
-#ifdef UPK_EXP_NOCOMBINE
-            if (false) {
-#else
             if (kpos == 0) {
-#endif
                 // the run crossed a strip edge: first maximum over its parts,
                 // in position order -- the part of the run open at a strip's
                 // first position that closes inside it, else the part open at
@@ -1943,11 +1921,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
         const double x_bar = (double)psum / (double)count;
         double sum2 = 0.0, sum4 = 0.0;
         int blk2 = 0;
-#ifdef UPK_EXP_NOPASS2
-        for (int64_t x0 = left; x0 < left; x0 += 64, ++blk2) {
-#else
         for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64, ++blk2) {
-#endif
             const int64_t x = x0 + lane;
             const bool valid = x <= (int64_t)right;
             uint32_t pc = 0;
