@@ -1,8 +1,8 @@
-"""The 4-bit track layout and K1's integer screen against
-the oracle: counts >= 8 (the screen sends the chunk to the exact path) and
->= 15 (escape nibble, overflow table) at peaks and in the background, with
+"""The track layout (2-bit fields, escape 3 and the overflow table) and K1's
+integer screen against the oracle: escaped counts (the
+screen sends their chunk to the exact path) at peaks and in the background, with
 counts on both sides of each boundary, thresholds from "almost everything is a region"
-to "almost nothing is", every bandwidth class of the screen window, scaled
+to "almost nothing is", every bandwidth class of the screen window (bw 1 .. 255, NH = 1 .. 4), scaled
 pooling with large and negative coefficients, and device-resident input
 through up_unit_pack."""
 import numpy as np
@@ -66,7 +66,7 @@ def test_tag_total_counts_escapes(gpu_lib):
 
 
 @pytest.mark.parametrize("thr", [0.05, 1.0, 25.0, 400.0])
-@pytest.mark.parametrize("bw", [1, 15, 16, 17, 33, 64, 127])
+@pytest.mark.parametrize("bw", [1, 15, 16, 17, 33, 64, 127, 128, 150, 191, 192, 255])
 def test_screen_thresholds_and_bandwidths(gpu_lib, oracle, thr, bw):
     rng = np.random.default_rng(1000 * bw + int(thr * 10))
     length, bg = 70_000, 0.003

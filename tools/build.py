@@ -28,15 +28,36 @@ def _run(cmd, cwd=ROOT):
     subprocess.run(cmd, cwd=cwd, check=True)
 
 
+def compile_lib(out, extra=(), jobs=None):
+    """libunipeak_hip.so from five translation units compiled in parallel:
+    api.hip (C-ABI, non-templated kernels) and nh_tu.hip once per window
+    width NH = 1..4 (the templated K1/K3/K4 kernels)."""
+    from concurrent.futures import ThreadPoolExecutor
+    csrc = os.path.join(ROOT, "unipeak_amd", "csrc")
+    objdir = os.path.join(ROOT, "build", "obj_" + os.path.basename(out).replace(".so", ""))
+    os.makedirs(objdir, exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
+             "-I", os.path.join(ROOT, "include")] + list(extra)
+    units = [("api", os.path.join(csrc, "api.hip"), [])] + [
+        (f"nh{k}", os.path.join(csrc, "nh_tu.hip"), [f"-DUPK_NH_TU={k}"]) for k in (1, 2, 3, 4)]
+    def one(u):
+        name, src, defs = u
+        obj = os.path.join(objdir, name + ".o")
+        _run([HIPCC] + flags + defs + ["-c", "-o", obj, src])
+        return obj
+    with ThreadPoolExecutor(jobs or min(5, os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(one, units))
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
+    return out
+
+
 def build_lib(force=False):
     out = os.path.join(ROOT, "unipeak_amd", "lib", "libunipeak_hip.so")
     srcs = glob.glob(os.path.join(ROOT, "unipeak_amd", "csrc", "*")) + [
         os.path.join(ROOT, "include", "unipeak_hip.h")]
     if force or _stale(out, srcs):
-        os.makedirs(os.path.dirname(out), exist_ok=True)
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-ffp-contract=off", "-fno-fast-math", "-I", os.path.join(ROOT, "include"),
-              "-o", out, os.path.join(ROOT, "unipeak_amd", "csrc", "api.hip")])
+        compile_lib(out)
     return out
 
 
@@ -76,4 +97,7 @@ def build_all(force=False):
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
+    if len(sys.argv) > 2 and sys.argv[1] == "--variant":  # tools/build.py --variant NAME -DFLAG ...
+        compile_lib(os.path.join(ROOT, "unipeak_amd", "lib", f"libunipeak_hip_{sys.argv[2]}.so"), sys.argv[3:])
+    else:
+        build_all(force="--force" in sys.argv)

@@ -13,10 +13,14 @@ if "--" in args:
     extra = args[args.index("--") + 1:]
     args = args[:args.index("--")]
 flt = args[0] if args else ""
-cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-       "-ffp-contract=off", "-I", f"{ROOT}/include", "-o", "/dev/null", f"{ROOT}/unipeak_amd/csrc/api.hip",
-       "-Rpass-analysis=kernel-resource-usage"] + extra
-out = subprocess.run(cmd, capture_output=True, text=True).stderr
+base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
+        "-ffp-contract=off", "-I", f"{ROOT}/include", "-o", "/dev/null",
+        "-Rpass-analysis=kernel-resource-usage"] + extra
+# api.hip (non-templated kernels) and the per-NH units (templated kernels)
+nhs = [int(x) for x in __import__("os").environ.get("NH", "1,2").split(",")]
+cmds = [base + [f"{ROOT}/unipeak_amd/csrc/api.hip"]] + [
+    base + [f"-DUPK_NH_TU={k}", f"{ROOT}/unipeak_amd/csrc/nh_tu.hip"] for k in nhs]
+out = "\n".join(subprocess.run(c, capture_output=True, text=True).stderr for c in cmds)
 rows, cur = [], None
 for line in out.splitlines():
     m = re.search(r"Function Name: (\S+)", line)

@@ -18,8 +18,51 @@
 #include "../../include/unipeak_hip.h"
 #include "kernels.h"
 
-#include "kernels.hip"  // single translation unit: kernels + C-ABI
+#include "kernels.hip"  // device code shared with the per-NH units (nh_tu.hip)
 #include "emulate.hip"
+
+namespace upk {
+// the templated K1 / K3 / K4 kernels live in four translation units, one per
+// window width NH (nh_tu.hip, built in parallel); these return their addresses
+const void *scan_kernel_nh1(int, bool, bool, int);
+const void *scan_kernel_nh2(int, bool, bool, int);
+const void *scan_kernel_nh3(int, bool, bool, int);
+const void *scan_kernel_nh4(int, bool, bool, int);
+const void *stats_kernel_nh1(int, bool);
+const void *stats_kernel_nh2(int, bool);
+const void *stats_kernel_nh3(int, bool);
+const void *stats_kernel_nh4(int, bool);
+const void *shift_kernel_nh1(int);
+const void *shift_kernel_nh2(int);
+const void *shift_kernel_nh3(int);
+const void *shift_kernel_nh4(int);
+// window words on each side of an output word: ceil((bw + 1) / 64)
+static int window_nh(int bw) { return (bw + 64) / 64; }
+static const void *scan_kernel_for(int bw, int pool, bool nd, bool prof, int mode) {
+    switch (window_nh(bw)) {
+    case 1: return scan_kernel_nh1(pool, nd, prof, mode);
+    case 2: return scan_kernel_nh2(pool, nd, prof, mode);
+    case 3: return scan_kernel_nh3(pool, nd, prof, mode);
+    default: return scan_kernel_nh4(pool, nd, prof, mode);
+    }
+}
+static const void *stats_kernel_for(int bw, int pool, bool nd) {
+    switch (window_nh(bw)) {
+    case 1: return stats_kernel_nh1(pool, nd);
+    case 2: return stats_kernel_nh2(pool, nd);
+    case 3: return stats_kernel_nh3(pool, nd);
+    default: return stats_kernel_nh4(pool, nd);
+    }
+}
+static const void *shift_kernel_for(int bw, int pool) {
+    switch (window_nh(bw)) {
+    case 1: return shift_kernel_nh1(pool);
+    case 2: return shift_kernel_nh2(pool);
+    case 3: return shift_kernel_nh3(pool);
+    default: return shift_kernel_nh4(pool);
+    }
+}
+}  // namespace upk
 
 using namespace upk;
 
@@ -100,7 +143,11 @@ constexpr int kSlots = UP_MAX_IN_FLIGHT;  // passes in flight at most (up_run_as
 struct up_ctx {
     int dev = 0;
     int ncu = 0;                     // compute units of the device
-    int k1a_per_cu = 2;              // K1a workgroups per CU (UNIPEAK_K1A_PER_CU; 0 = resident max)
+    // K1a workgroups per CU (UNIPEAK_K1A_PER_CU; 0 = resident max): 3 with
+    // the 2-bit tracks and the register pre-screen (hg19, same box, two
+    // rounds: K1a alone 0.35 vs 0.44 ms at 2, bench 4,395 vs 4,265 Gbp/s)
+    int k1a_per_cu = 3;
+    bool k3_direct = false;          // UNIPEAK_K3_DIRECT=1: K3 writes host records itself (A/B)
     int k1b_per_cu = 0;              // K1b workgroups per CU (UNIPEAK_K1B_PER_CU; 0 = resident)
     bool use_graphs = true;          // passes as hipGraphs (UNIPEAK_GRAPHS=0: plain launches)
     // streams of the passes (with the context stream: four, HIP's default
@@ -122,7 +169,7 @@ struct up_ctx {
     DevBuf<uint8_t> d_ctl;
     DevBuf<uint32_t> d_wscreen;
     uint32_t wskip = 0;
-    float fw[9] = {};                // fine screen weights per chunk distance
+    float fw[kScrHalo + 1] = {};     // fine screen weights per chunk distance
     float fthr = 0.f;
     // K1b keys (ScanParams::qmode): score = alpha * Q * (1 +- q_delta)
     bool q_ok = false;               // weights proportional to bw^2 - d^2 within q_delta
@@ -166,11 +213,17 @@ struct up_ctx {
         DevBuf<double> d_peak_val;
         DevBuf<uint64_t> d_spk;          // K1 per-strip partial peaks (ScanParams::spk)
         DevBuf<double> d_corr;           // K3 (f, r) slabs for the strand correlation (-D -y)
+        // K3's records and exptSums in device memory; DMA copies deliver them
+        // to a host destination (the pass's record target or hp_regions)
+        DevBuf<uint8_t> d_out;
+        uint8_t *copy_rec = nullptr, *copy_cnt = nullptr;  // host destinations (null: K3 writes in place)
+        uint64_t copied = 0;             // records the pass's DMA copies deliver
         void release() {
             d_info.release(); d_rec.release(); d_ovf_count.release(); d_ovf_rec.release(); d_head.release();
             d_cnt.release(); d_nreg.release(); d_bsum.release(); d_starts.release(); d_ends.release();
             d_runit.release(); d_peak_pos.release(); d_xlist.release(); d_xcount.release();
             d_xwcount.release(); d_xref.release(); d_peak_val.release(); d_spk.release(); d_corr.release();
+            d_out.release();
         }
         uint8_t *target = nullptr;   // record target of this pass (device address) or null
         void *target_hostp = nullptr;// host address of a host target
@@ -318,6 +371,7 @@ int up_open(int hip_device, up_ctx **out) {
     HIPCHK(hipSetDevice(hip_device));
     HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     if (const char *e = getenv("UNIPEAK_K1A_PER_CU")) c->k1a_per_cu = atoi(e);
+    if (const char *e = getenv("UNIPEAK_K3_DIRECT")) c->k3_direct = e[0] == '1';
     if (const char *e = getenv("UNIPEAK_GRAPHS")) c->use_graphs = e[0] != '0';
     if (const char *e = getenv("UNIPEAK_K1B_PER_CU")) c->k1b_per_cu = atoi(e);
     if (const char *e = getenv("UNIPEAK_LAUNCHER")) c->use_launcher = e[0] != '0';
@@ -465,7 +519,7 @@ int up_set_params(up_ctx *c, const up_params *p) {
         // positions of chunks d apart (smallest distance 0, 1, 17, 33, ...),
         // inflated by 1e-4; a chunk can hold a flag only if its bound > fthr
         const int bwi = p->bw;
-        for (int d = 0; d < 9; ++d) {
+        for (int d = 0; d <= kScrHalo; ++d) {
             const int u0 = d == 0 ? 0 : 16 * (d - 1) + 1;
             double kd = 0.0;
             for (int u = u0; u <= bwi; ++u) kd = std::max(kd, std::fabs(c->kern[bwi + u]));
@@ -901,7 +955,7 @@ static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps, uint32_t ovf_cap) {
     P.kern = c->d_kern.p;
     P.wscreen = c->d_wscreen.p;
     P.wskip = c->wskip;
-    for (int d = 0; d < 9; ++d) P.fw[d] = c->fw[d];
+    for (int d = 0; d <= kScrHalo; ++d) P.fw[d] = c->fw[d];
     P.fthr = c->fthr;
     P.bw = c->p.bw;
     P.thr = c->p.region_thr;
@@ -943,10 +997,10 @@ static uint32_t resident_blocks(const up_ctx *c, const void *kernel, size_t lds)
     return (uint32_t)n * (uint32_t)(c->ncu > 0 ? c->ncu : 256);
 }
 
-template <int NH, int POOL, bool ND, bool PROF, int MODE>
-static void launch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32_t b, uint32_t e) {
+template <bool PROF, int MODE>
+static void dispatch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32_t b, uint32_t e) {
     const size_t lds = MODE == kModeScreen ? kScreenLds : MODE == kModeExact ? kExactLds : kScanLds;
-    const void *k = (const void *)scan_kernel<NH, POOL, ND, PROF, MODE>;
+    const void *k = scan_kernel_for(P.bw, pool_mode(c), c->p.nondir != 0, PROF, MODE);
     uint32_t blocks = resident_blocks(c, k, lds);
     if (MODE == kModeExact) {
         // K1b: grid-stride over the device-side work-list count, the
@@ -967,28 +1021,13 @@ static void launch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32_t
         if (blocks > kMaxK1aWaves / 4) blocks = kMaxK1aWaves / 4;
         if (blocks == 0) return;
     }
+    ScanParams Q = P;
     if (MODE == kModeScreen) {  // per-wave work-list stash regions (ScanParams::xlist)
-        ScanParams Q = P;
         c->k1a_waves = 4 * blocks;
         c->k1a_xcap = Q.xcap = (e - b + c->k1a_waves - 1) / c->k1a_waves;
-        hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF, MODE>), dim3(blocks), dim3(256), lds, st, Q, b, e);
-        return;
     }
-    hipLaunchKernelGGL((scan_kernel<NH, POOL, ND, PROF, MODE>), dim3(blocks), dim3(256), lds, st, P, b, e);
-}
-
-template <bool PROF, int MODE>
-static void dispatch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32_t b, uint32_t e) {
-    const int nh = P.bw <= 63 ? 1 : 2;
-    const int pool = pool_mode(c);
-    const bool nd = c->p.nondir != 0;
-#define UPK_SCAN(NH, PL, ND) \
-    if (nh == NH && pool == PL && nd == ND) return launch_scan<NH, PL, ND, PROF, MODE>(c, st, P, b, e);
-    UPK_SCAN(1, 0, false) UPK_SCAN(1, 1, false) UPK_SCAN(1, 2, false)
-    UPK_SCAN(1, 0, true) UPK_SCAN(1, 1, true) UPK_SCAN(1, 2, true)
-    UPK_SCAN(2, 0, false) UPK_SCAN(2, 1, false) UPK_SCAN(2, 2, false)
-    UPK_SCAN(2, 0, true) UPK_SCAN(2, 1, true) UPK_SCAN(2, 2, true)
-#undef UPK_SCAN
+    void *args[] = {&Q, &b, &e};
+    (void)hipLaunchKernel(k, dim3(blocks), dim3(256), args, lds, st);
 }
 
 static StatParams stat_params(up_ctx *c, up_ctx::Pass &ps) {
@@ -1021,24 +1060,13 @@ static StatParams stat_params(up_ctx *c, up_ctx::Pass &ps) {
 }
 
 static void dispatch_stats(up_ctx *c, hipStream_t st, const StatParams &P, uint64_t nreg) {
-    const int nh = P.bw <= 63 ? 1 : 2;
-    const int pool = pool_mode(c);
-    const bool nd = c->p.nondir != 0;
     const size_t lds = kStatLds;
-#define UPK_ST(NH, PL, ND)                                                                       \
-    if (nh == NH && pool == PL && nd == ND) {                                                    \
-        uint64_t blocks = std::min<uint64_t>((nreg + 3) / 4,                                     \
-                                             resident_blocks(c, (const void *)stats_kernel<NH, PL, ND>, lds)); \
-        if (blocks == 0) return;                                                                 \
-        hipLaunchKernelGGL((stats_kernel<NH, PL, ND>), dim3((unsigned)blocks), dim3(256), lds,     \
-                           st, P);                                                                \
-        return;                                                                                  \
-    }
-    UPK_ST(1, 0, false) UPK_ST(1, 1, false) UPK_ST(1, 2, false)
-    UPK_ST(1, 0, true) UPK_ST(1, 1, true) UPK_ST(1, 2, true)
-    UPK_ST(2, 0, false) UPK_ST(2, 1, false) UPK_ST(2, 2, false)
-    UPK_ST(2, 0, true) UPK_ST(2, 1, true) UPK_ST(2, 2, true)
-#undef UPK_ST
+    const void *k = stats_kernel_for(P.bw, pool_mode(c), c->p.nondir != 0);
+    const uint64_t blocks = std::min<uint64_t>((nreg + 3) / 4, resident_blocks(c, k, lds));
+    if (blocks == 0) return;
+    StatParams Q = P;
+    void *args[] = {&Q};
+    (void)hipLaunchKernel(k, dim3((unsigned)blocks), dim3(256), args, lds, st);
 }
 
 // Configurations the parallel scan does not represent run through the
@@ -1343,6 +1371,13 @@ static int enqueue_rest(up_ctx *c, int slot, const ScanParams &SP, const StatPar
     if (events) HIPCHK(hipEventRecord(ps.ev[3], ps.stream));
     dispatch_stats(c, ps.stream, P, std::max<uint64_t>(ps.req_last_nreg, 1024));
     HIPCHK(hipGetLastError());
+    if (ps.copy_rec && ps.copied) {  // K3 staged the records in device memory
+        const int S = c->p.n_samples;
+        HIPCHK(hipMemcpyAsync(ps.copy_rec, P.out, ps.copied * sizeof(up_region), hipMemcpyDeviceToHost,
+                              ps.stream));
+        HIPCHK(hipMemcpyAsync(ps.copy_cnt, P.out_counts, ps.copied * S * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, ps.stream));
+    }
     if (events) HIPCHK(hipEventRecord(ps.ev[4], ps.stream));
     return UP_OK;
 }
@@ -1441,17 +1476,40 @@ static int launch_pass(up_ctx *c, int slot) {
     P.spk = ps.d_spk.p;
     P.corr_scratch = corr ? ps.d_corr.p : nullptr;
     P.corr_cap = corr_cap;
-    // K3 writes the records straight into mapped pinned host memory (or the
-    // caller's record target).  Staging them in device memory and delivering
-    // them with a DMA copy on a second stream measured within run-to-run
-    // noise, so there is one delivery path.
-    if (ps.target) {  // records into the caller's buffer instead
-        P.cap = std::min<uint64_t>(cap, ps.target_cap);
-        P.out = (up_region *)(ps.target + 8);
-        P.out_counts = (uint32_t *)(ps.target + 8 + ps.target_cap * sizeof(up_region));
+    // K3 writes the records into device memory and the pass's stream copies
+    // them (DMA) to their host destination -- the caller's record target or
+    // this slot's pinned host buffers -- so K3's waves never wait on PCIe
+    // writes (they made up the tail of K3: the kernel ends only when its
+    // system-scope writes have landed).  The copies move the previous pass's
+    // record count plus a margin; a pass that yields more gets the rest in
+    // up_run_wait.  A device-memory target is written by K3 directly.
+    ps.copy_rec = ps.copy_cnt = nullptr;
+    ps.copied = 0;
+    const uint64_t rcap = ps.target ? std::min<uint64_t>(cap, ps.target_cap) : cap;
+    if ((ps.target && !ps.target_hostp) || c->k3_direct) {  // device target (or A/B): K3 writes in place
+        P.cap = rcap;
+        if (ps.target) {
+            P.out = (up_region *)(ps.target + 8);
+            P.out_counts = (uint32_t *)(ps.target + 8 + ps.target_cap * sizeof(up_region));
+        } else {
+            P.out = c->hp_regions[slot].dev;
+            P.out_counts = c->hp_counts[slot].dev;
+        }
     } else {
-        P.out = c->hp_regions[slot].dev;
-        P.out_counts = c->hp_counts[slot].dev;
+        const size_t rb = (rcap + 1) * sizeof(up_region), cb = (rcap + 1) * S * sizeof(uint32_t);
+        HIPCHK(ps.d_out.ensure(rb + cb + 256));
+        P.cap = rcap;
+        P.out = (up_region *)ps.d_out.p;
+        P.out_counts = (uint32_t *)(ps.d_out.p + ((rb + 255) & ~(size_t)255));
+        if (ps.target) {
+            ps.copy_rec = (uint8_t *)ps.target_hostp + 8;
+            ps.copy_cnt = (uint8_t *)ps.target_hostp + 8 + ps.target_cap * sizeof(up_region);
+        } else {
+            ps.copy_rec = (uint8_t *)c->hp_regions[slot].p;
+            ps.copy_cnt = (uint8_t *)c->hp_counts[slot].p;
+        }
+        const uint64_t est = ps.req_last_nreg ? ps.req_last_nreg + ps.req_last_nreg / 16 + 64 : 0;
+        ps.copied = std::min<uint64_t>(est, rcap);
     }
     ps.counters_armed = true;  // K2b re-arms them
     const int tl = ps.tl;
@@ -1645,7 +1703,8 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
                             "words reaching thr/2 %llu\n",
                     c->nstrips, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
             fprintf(stderr, "unipeak_hip: K1b clocks: item %llu load %llu scatter %llu flags %llu items %llu "
-                            "max wave %llu waves %llu\n", h[16], h[17], h[18], h[19], h[20], h[21], h[22]);
+                            "max wave %llu waves %llu (Q part of scatter %llu)\n", h[16], h[17], h[18], h[19],
+                    h[20], h[21], h[22], h[23]);
             fprintf(stderr, "unipeak_hip: K1b items by exact blocks:");
             for (int k = 1; k <= 16; ++k) fprintf(stderr, " %d:%llu", k, h[8 + k]);
             fprintf(stderr, "\n");
@@ -1663,6 +1722,18 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
         int r = launch_pass(c, slot);
         if (r) return fail(r);
         if (hipEventSynchronize(ps.done) != hipSuccess) return fail(UP_E_HIP);
+    }
+    if (ps.copy_rec && nreg > ps.copied) {  // more records than the pass's copies moved
+        const int S = c->p.n_samples;
+        const uint8_t *drec = ps.d_out.p;
+        const size_t rb = (ps.target ? std::min<uint64_t>(ps.cap, ps.target_cap) : ps.cap) + 1;
+        const uint8_t *dcnt = ps.d_out.p + (((rb * sizeof(up_region)) + 255) & ~(size_t)255);
+        const uint64_t k = ps.copied, m = nreg - ps.copied;
+        if (hipMemcpy(ps.copy_rec + k * sizeof(up_region), drec + k * sizeof(up_region), m * sizeof(up_region),
+                      hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(ps.copy_cnt + k * S * sizeof(uint32_t), dcnt + k * S * sizeof(uint32_t),
+                      m * S * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(UP_E_HIP);
     }
     c->nreg = nreg;
     c->last_nreg = nreg;
@@ -1908,18 +1979,18 @@ static int shift_run(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shif
     }
     HIPCHK(hipMemcpyAsync(d_pref, pref.data(), n + 1, hipMemcpyHostToDevice, c->stream));
     StatParams P = stat_params(c, ps);
-    const int nh = P.bw <= 63 ? 1 : 2;
-    const int pool = pool_mode(c);
     const size_t lds = kShiftLdsBytes;
     const unsigned blocks = (unsigned)std::min<size_t>(n, 8192);
-#define UPK_SH(NH, PL)                                                                              \
-    if (nh == NH && pool == PL)                                                                     \
-        hipLaunchKernelGGL((shift_kernel<NH, PL>), dim3(blocks), dim3(kShiftThreads), lds, c->stream, \
-                           P, d_idx, (uint32_t)n, (int)max_shift, d_off, d_slab, d_pref,               \
-                           best ? nullptr : d_out, best ? (uint16_t *)(d_out + n) : nullptr,            \
-                           best ? d_out : nullptr);
-    UPK_SH(1, 0) UPK_SH(1, 1) UPK_SH(1, 2) UPK_SH(2, 0) UPK_SH(2, 1) UPK_SH(2, 2)
-#undef UPK_SH
+    {
+        const void *k = shift_kernel_for(P.bw, pool_mode(c));
+        uint32_t nn = (uint32_t)n;
+        int ms = (int)max_shift;
+        double *tab = best ? nullptr : d_out;
+        uint16_t *bs = best ? (uint16_t *)(d_out + n) : nullptr;
+        double *bc = best ? d_out : nullptr;
+        void *args[] = {&P, &d_idx, &nn, &ms, &d_off, &d_slab, &d_pref, &tab, &bs, &bc};
+        (void)hipLaunchKernel(k, dim3(blocks), dim3(kShiftThreads), args, lds, c->stream);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     if (best) {

@@ -546,7 +546,7 @@ __device__ __forceinline__ void scatter_hits(A (&acc)[SW], const int (&b)[kHB], 
 // i lives at word i + i/16, so the reads below (lane l takes indices 16l ..
 // 16l + 31, the same offset on every lane) hit 64 different banks; unpadded,
 // that 16-word lane stride made every read a 16-way bank conflict
-constexpr int kScrIdx = 8 + kBlocks * kWave + 8;
+constexpr int kScrIdx = kScrHalo + kBlocks * kWave + kScrHalo;
 constexpr int kScrWords = kScrIdx + kScrIdx / 16 + 2;  // even: 8-byte aligned per wave
 __device__ __forceinline__ int scr_at(int i) { return i + (i >> 4); }
 // K1a needs no kernel weights: its chunk-sum areas start at LDS offset 0, so
@@ -577,7 +577,7 @@ __device__ __forceinline__ uint32_t screen_bits(const uint32_t *rd, uint32_t wsk
     uint32_t tot = 0;
 #pragma unroll
     for (int j = 0; j < 16 + 2 * R; ++j) {
-        const int i = 8 - R + j;
+        const int i = kScrHalo - R + j;
         a[j] = rd[i + (i >> 4)];
     }
 #pragma unroll
@@ -595,6 +595,18 @@ __device__ __forceinline__ uint32_t screen_bits(const uint32_t *rd, uint32_t wsk
         m |= (b > fthr ? 1u : 0u) << i;
     }
     return m;
+}
+
+// screen_bits for the runtime R = ceil(bw / 16) <= RM (RM = 4 NH: only the
+// windows this NH can have are instantiated, which keeps the K1a register
+// count of the narrow kernels down)
+template <int RM>
+__device__ __forceinline__ uint32_t screen_any(int R, const uint32_t *rd, uint32_t wskip, const float *fw,
+                                               float fthr) {
+    if constexpr (RM > 1) {
+        if (R < RM) return screen_any<RM - 1>(R, rd, wskip, fw, fthr);
+    }
+    return screen_bits<RM>(rd, wskip, fw, fthr);
 }
 
 // MODE kModeScreen (K1a): stream + screen every strip; strips without exact
@@ -679,7 +691,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     uint32_t it0 = (MODE == kModeExact ? 0u : strip_begin) + wave, istep = nwaves;
 #ifdef UPK_DEBUG_TIMES
     // K1b phase clocks of this wave (s_memtime), added up once at the end
-    uint64_t dt_item = 0, dt_load = 0, dt_scat = 0, dt_flag = 0, n_items = 0;
+    uint64_t dt_item = 0, dt_load = 0, dt_scat = 0, dt_flag = 0, n_items = 0, dt_q = 0;
 #endif
     // K1a software pipeline: the loads of this wave's next (strip, track) --
     // strips it0, it0 + istep, ...; tracks (strand, pooled sample) in order --
@@ -691,7 +703,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 #else
     constexpr bool kPf = true;
 #endif
-    constexpr int HL_ = 8 * kChunkBytes / 16;  // halo lane loads per side (8 chunks)
+    constexpr int HL_ = kScrHalo * kChunkBytes / 16;  // halo lane loads per side (kScrHalo chunks)
     u32x4 pv[MODE == kModeScreen && !PROF ? kLoads : 1];
     u32x4 phv = {0u, 0u, 0u, 0u};
     uint32_t pf_strip = 0, pf_cur = 0;
@@ -753,7 +765,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             // lane l of wave load q holds 16 bytes = CPL chunks: chunks
             // CPL * (64q + l) + i, i < CPL (DPC dwords each)
             constexpr int CPL = 16 / kChunkBytes, DPC = kChunkBytes / 4;
-            constexpr int HL = 8 * kChunkBytes / 16;  // halo lane loads per side (8 chunks)
+            constexpr int HL = kScrHalo * kChunkBytes / 16;  // halo lane loads per side (kScrHalo chunks)
             uint32_t cs[CPL * kLoads];
             uint32_t big = 0, hs[CPL], hbig = 0, anybig = 0;
 #pragma unroll
@@ -901,12 +913,12 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             // (a lane's CPL chunks never straddle a pad word: CPL divides 16)
 #pragma unroll
             for (int q = 0; q < kLoads; ++q) {
-                uint32_t *d = scr + scr_at(8 + kWave * CPL * q + CPL * lane);
+                uint32_t *d = scr + scr_at(kScrHalo + kWave * CPL * q + CPL * lane);
 #pragma unroll
                 for (int i = 0; i < CPL; ++i) d[i] = ((big >> (CPL * q + i)) & 1u) ? kBig : cs[CPL * q + i];
             }
             if (lane < 2 * HL) {
-                uint32_t *d = scr + scr_at(lane < HL ? CPL * lane : 8 + kBlocks * kWave + CPL * (lane - HL));
+                uint32_t *d = scr + scr_at(lane < HL ? CPL * lane : kScrHalo + kBlocks * kWave + CPL * (lane - HL));
 #pragma unroll
                 for (int i = 0; i < CPL; ++i) d[i] = ((hbig >> i) & 1u) ? kBig : hs[i];
             }
@@ -914,17 +926,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const uint32_t *rd = scr + 17 * lane;  // index 16l + j = word 17l + j + j/16
-            uint32_t m = 0;
-            switch (R) {
-            case 1: m = screen_bits<1>(rd, P.wskip, P.fw, P.fthr); break;
-            case 2: m = screen_bits<2>(rd, P.wskip, P.fw, P.fthr); break;
-            case 3: m = screen_bits<3>(rd, P.wskip, P.fw, P.fthr); break;
-            case 4: m = screen_bits<4>(rd, P.wskip, P.fw, P.fthr); break;
-            case 5: m = screen_bits<5>(rd, P.wskip, P.fw, P.fthr); break;
-            case 6: m = screen_bits<6>(rd, P.wskip, P.fw, P.fthr); break;
-            case 7: m = screen_bits<7>(rd, P.wskip, P.fw, P.fthr); break;
-            default: m = screen_bits<8>(rd, P.wskip, P.fw, P.fthr); break;
-            }
+            const uint32_t m = screen_any<4 * NH>(R, rd, P.wskip, P.fw, P.fthr);
             const uint64_t lanes = __ballot(m != 0u);  // lane l covers chunks 16l..16l+15
             mchunk = m;
             exact_blocks = 0;
@@ -1098,6 +1100,9 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     });
                 }
             }
+#ifdef UPK_DEBUG_TIMES
+            dt_q += __builtin_amdgcn_s_memtime() - tq1;
+#endif
             // ---- KDE: scatter every hit of the window, ascending ----
             double af[SW], ar[NONDIR ? SW : 1];
 #pragma unroll
@@ -1285,6 +1290,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         atomicAdd(&P.dbg[20], (unsigned long long)n_items);
         atomicMax(&P.dbg[21], (unsigned long long)dt_item);
         atomicAdd(&P.dbg[22], 1ull);
+        atomicAdd(&P.dbg[23], (unsigned long long)dt_q);
     }
 #endif
     if constexpr (MODE == kModeScreen) {
@@ -1295,6 +1301,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     }
 }
 
+#ifndef UPK_NH_TU  // the per-NH translation units hold only the templated kernels
 // K1x: the K1a waves' stash counts -> xref (stash indices of the listed
 // entries, every front entry first) and the totals in xcount.  One block:
 // thread t owns K1a waves [t*per, (t+1)*per).
@@ -1493,6 +1500,8 @@ __global__ void __launch_bounds__(256) unit_last_kernel(const UnitDesc *units, u
         if (lane == 0 && best) atomicMax(&out[u], best);
     }
 }
+
+#endif  // UPK_NH_TU
 
 // ------------------------------------------------------------------------
 // K3: region statistics, one wave per region (grid-stride).
@@ -2202,6 +2211,7 @@ __global__ void __launch_bounds__(kShiftThreads) shift_kernel(StatParams P, cons
     }
 }
 
+#ifndef UPK_NH_TU
 // ------------------------------------------------------------------------
 // aux kernels
 // ------------------------------------------------------------------------
@@ -2303,4 +2313,5 @@ __global__ void synth_peak_kernel(uint32_t *stage, const uint32_t *__restrict__ 
     if (i < n) atomicAdd(&stage[pos[i] - 1], 1u);
 }
 
+#endif  // UPK_NH_TU
 }  // namespace upk
