@@ -101,9 +101,10 @@ def test_replay_multi_sample_control_and_coeffs(gpu_lib, oracle):
 
 
 def test_replay_refuses_pipelined_and_profile(gpu_lib):
+    """bw > 255 (kMaxBw): outside the parallel scan, the whole-buffer replay"""
     capi = gpu_lib
     with capi.Lib(0) as g:
-        g.set_params(200, 1, 0.003)
+        g.set_params(300, 1, 0.003)
         u = g.add_unit(10_000)
         g.scatter(u, 0, 0, np.array([5000], np.uint32), np.array([3], np.uint32))
         assert g.run() >= 0

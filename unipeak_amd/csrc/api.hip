@@ -147,7 +147,6 @@ struct up_ctx {
     // the 2-bit tracks and the register pre-screen (hg19, same box, two
     // rounds: K1a alone 0.35 vs 0.44 ms at 2, bench 4,395 vs 4,265 Gbp/s)
     int k1a_per_cu = 3;
-    bool k3_direct = false;          // UNIPEAK_K3_DIRECT=1: K3 writes host records itself (A/B)
     int k1b_per_cu = 0;              // K1b workgroups per CU (UNIPEAK_K1B_PER_CU; 0 = resident)
     bool use_graphs = true;          // passes as hipGraphs (UNIPEAK_GRAPHS=0: plain launches)
     // streams of the passes (with the context stream: four, HIP's default
@@ -213,17 +212,11 @@ struct up_ctx {
         DevBuf<double> d_peak_val;
         DevBuf<uint64_t> d_spk;          // K1 per-strip partial peaks (ScanParams::spk)
         DevBuf<double> d_corr;           // K3 (f, r) slabs for the strand correlation (-D -y)
-        // K3's records and exptSums in device memory; DMA copies deliver them
-        // to a host destination (the pass's record target or hp_regions)
-        DevBuf<uint8_t> d_out;
-        uint8_t *copy_rec = nullptr, *copy_cnt = nullptr;  // host destinations (null: K3 writes in place)
-        uint64_t copied = 0;             // records the pass's DMA copies deliver
         void release() {
             d_info.release(); d_rec.release(); d_ovf_count.release(); d_ovf_rec.release(); d_head.release();
             d_cnt.release(); d_nreg.release(); d_bsum.release(); d_starts.release(); d_ends.release();
             d_runit.release(); d_peak_pos.release(); d_xlist.release(); d_xcount.release();
             d_xwcount.release(); d_xref.release(); d_peak_val.release(); d_spk.release(); d_corr.release();
-            d_out.release();
         }
         uint8_t *target = nullptr;   // record target of this pass (device address) or null
         void *target_hostp = nullptr;// host address of a host target
@@ -371,7 +364,6 @@ int up_open(int hip_device, up_ctx **out) {
     HIPCHK(hipSetDevice(hip_device));
     HIPCHK(hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, hip_device));
     if (const char *e = getenv("UNIPEAK_K1A_PER_CU")) c->k1a_per_cu = atoi(e);
-    if (const char *e = getenv("UNIPEAK_K3_DIRECT")) c->k3_direct = e[0] == '1';
     if (const char *e = getenv("UNIPEAK_GRAPHS")) c->use_graphs = e[0] != '0';
     if (const char *e = getenv("UNIPEAK_K1B_PER_CU")) c->k1b_per_cu = atoi(e);
     if (const char *e = getenv("UNIPEAK_LAUNCHER")) c->use_launcher = e[0] != '0';
@@ -1371,13 +1363,6 @@ static int enqueue_rest(up_ctx *c, int slot, const ScanParams &SP, const StatPar
     if (events) HIPCHK(hipEventRecord(ps.ev[3], ps.stream));
     dispatch_stats(c, ps.stream, P, std::max<uint64_t>(ps.req_last_nreg, 1024));
     HIPCHK(hipGetLastError());
-    if (ps.copy_rec && ps.copied) {  // K3 staged the records in device memory
-        const int S = c->p.n_samples;
-        HIPCHK(hipMemcpyAsync(ps.copy_rec, P.out, ps.copied * sizeof(up_region), hipMemcpyDeviceToHost,
-                              ps.stream));
-        HIPCHK(hipMemcpyAsync(ps.copy_cnt, P.out_counts, ps.copied * S * sizeof(uint32_t),
-                              hipMemcpyDeviceToHost, ps.stream));
-    }
     if (events) HIPCHK(hipEventRecord(ps.ev[4], ps.stream));
     return UP_OK;
 }
@@ -1476,40 +1461,18 @@ static int launch_pass(up_ctx *c, int slot) {
     P.spk = ps.d_spk.p;
     P.corr_scratch = corr ? ps.d_corr.p : nullptr;
     P.corr_cap = corr_cap;
-    // K3 writes the records into device memory and the pass's stream copies
-    // them (DMA) to their host destination -- the caller's record target or
-    // this slot's pinned host buffers -- so K3's waves never wait on PCIe
-    // writes (they made up the tail of K3: the kernel ends only when its
-    // system-scope writes have landed).  The copies move the previous pass's
-    // record count plus a margin; a pass that yields more gets the rest in
-    // up_run_wait.  A device-memory target is written by K3 directly.
-    ps.copy_rec = ps.copy_cnt = nullptr;
-    ps.copied = 0;
-    const uint64_t rcap = ps.target ? std::min<uint64_t>(cap, ps.target_cap) : cap;
-    if ((ps.target && !ps.target_hostp) || c->k3_direct) {  // device target (or A/B): K3 writes in place
-        P.cap = rcap;
-        if (ps.target) {
-            P.out = (up_region *)(ps.target + 8);
-            P.out_counts = (uint32_t *)(ps.target + 8 + ps.target_cap * sizeof(up_region));
-        } else {
-            P.out = c->hp_regions[slot].dev;
-            P.out_counts = c->hp_counts[slot].dev;
-        }
+    // K3 writes the records straight into mapped pinned host memory (or the
+    // caller's record target).  Staging them in device memory and delivering
+    // them with DMA copies measured slower twice (round 1: within noise with
+    // a second stream; round 3, same box, two rounds each: 4,237 vs 4,405
+    // Gbp/s, K3 + copies 0.203 vs 0.167 ms), so there is one delivery path.
+    if (ps.target) {  // records into the caller's buffer instead
+        P.cap = std::min<uint64_t>(cap, ps.target_cap);
+        P.out = (up_region *)(ps.target + 8);
+        P.out_counts = (uint32_t *)(ps.target + 8 + ps.target_cap * sizeof(up_region));
     } else {
-        const size_t rb = (rcap + 1) * sizeof(up_region), cb = (rcap + 1) * S * sizeof(uint32_t);
-        HIPCHK(ps.d_out.ensure(rb + cb + 256));
-        P.cap = rcap;
-        P.out = (up_region *)ps.d_out.p;
-        P.out_counts = (uint32_t *)(ps.d_out.p + ((rb + 255) & ~(size_t)255));
-        if (ps.target) {
-            ps.copy_rec = (uint8_t *)ps.target_hostp + 8;
-            ps.copy_cnt = (uint8_t *)ps.target_hostp + 8 + ps.target_cap * sizeof(up_region);
-        } else {
-            ps.copy_rec = (uint8_t *)c->hp_regions[slot].p;
-            ps.copy_cnt = (uint8_t *)c->hp_counts[slot].p;
-        }
-        const uint64_t est = ps.req_last_nreg ? ps.req_last_nreg + ps.req_last_nreg / 16 + 64 : 0;
-        ps.copied = std::min<uint64_t>(est, rcap);
+        P.out = c->hp_regions[slot].dev;
+        P.out_counts = c->hp_counts[slot].dev;
     }
     ps.counters_armed = true;  // K2b re-arms them
     const int tl = ps.tl;
@@ -1722,18 +1685,6 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
         int r = launch_pass(c, slot);
         if (r) return fail(r);
         if (hipEventSynchronize(ps.done) != hipSuccess) return fail(UP_E_HIP);
-    }
-    if (ps.copy_rec && nreg > ps.copied) {  // more records than the pass's copies moved
-        const int S = c->p.n_samples;
-        const uint8_t *drec = ps.d_out.p;
-        const size_t rb = (ps.target ? std::min<uint64_t>(ps.cap, ps.target_cap) : ps.cap) + 1;
-        const uint8_t *dcnt = ps.d_out.p + (((rb * sizeof(up_region)) + 255) & ~(size_t)255);
-        const uint64_t k = ps.copied, m = nreg - ps.copied;
-        if (hipMemcpy(ps.copy_rec + k * sizeof(up_region), drec + k * sizeof(up_region), m * sizeof(up_region),
-                      hipMemcpyDeviceToHost) != hipSuccess ||
-            hipMemcpy(ps.copy_cnt + k * S * sizeof(uint32_t), dcnt + k * S * sizeof(uint32_t),
-                      m * S * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
-            return fail(UP_E_HIP);
     }
     c->nreg = nreg;
     c->last_nreg = nreg;
