@@ -4,7 +4,7 @@ the GPU over every unit (K0 replay, unipeak_amd/csrc/emulate.hip):
 * region threshold <= 0 -- processPosition's leap branch is live (quirk Q11:
   the leap position joins the region without setting its left end,
   misc/peakcall.cpp:76-78), so regions are not maximal runs of flags;
-* kernel bandwidth > 127 -- wider than the scan's register-resident halo;
+* kernel bandwidth > 255 -- wider than the scan's register-resident halo;
   windows up to 64 KiB live in LDS, wider ones in global scratch.
 
 Every candidate region (accepted and rejected), peak, counts and FP64 peak

@@ -728,6 +728,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         if (it0 < it_end) pf_issue(it0, find_unit(units, P.nunits, it0), 0, 0);
     }
     for (uint32_t it = it0; it < it_end; it += istep) {
+        const uint32_t item = it;
 #ifdef UPK_DEBUG_TIMES
         const uint64_t t_it0 = __builtin_amdgcn_s_memtime();
         ++n_items;
@@ -739,7 +740,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         uint32_t mchunk = 0xFFFFu;
         uint32_t exact_blocks = 0xFFFFu;
         if constexpr (MODE == kModeExact) {
-            const uint32_t ei = cptr(P.xref)[it];
+            const uint32_t ei = cptr(P.xref)[item];
             const uint32_t *e = P.xlist + (uint64_t)ei * kXEntry;
             const auto *es = cptr(e);  // the uniform words through scalar loads
             strip = es[0];
