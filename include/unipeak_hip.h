@@ -218,6 +218,21 @@ int up_timings(up_ctx *ctx, double *ms, int n);
 /* dense per-position score f+r of one unit (testing/-w): out[len] */
 int up_unit_profile(up_ctx *ctx, uint32_t unit, double *out_f, double *out_r,
                     uint32_t len);
+/* -w for units the exact replay produced (K0: quirk Q1 head hits, -r <= 0,
+ * bw > 255), whose retirements the dense KDE does not reproduce.  With the
+ * capture on before up_run, the replay records every processPosition() with
+ * a nonzero score (misc/peakcall.cpp:80-83: profileOut_->write), and
+ * up_unit_replay_profile returns them for one unit in emission order:
+ * event[i] = index of the unit's add() whose retirement loop wrote it
+ * (UP_FLUSH_EVENT: the unit's flushContig()), pos[i], score[i] = f + r.
+ * resync = 0: the unit was not replayed (up_unit_profile_range gives its
+ * profile); X: the entries cover positions < X and the dense KDE the rest;
+ * UP_FLUSH_EVENT (0xFFFFFFFF): the whole unit was replayed.  Call with
+ * event/pos/score NULL to get n. */
+#define UP_FLUSH_EVENT 0xFFFFFFFFu
+int up_set_profile_capture(up_ctx *ctx, int on);
+int up_unit_replay_profile(up_ctx *ctx, uint32_t unit, uint32_t *resync, uint64_t *n,
+                           uint32_t *event, uint32_t *pos, double *score, uint64_t cap);
 /* the same for positions [first, first + count) (first >= 1; the range may
  * run past the contig end into the scan domain, quirk Q16); out_r may be
  * NULL for directional units */

@@ -321,3 +321,44 @@ def test_strand_shift_cli_replayed_regions(orc_bin, gpu_lib, tmp_path, case):
         args += ["-r", "0"]
     out = compare_tool(orc_bin, tmp_path, "strand_shift", args + ["s0.wig"])
     assert "# best_shift=" in out
+
+
+PROFILE_REPLAY_CASES = [
+    # (name, bw, samples, args, tiny contigs)  -- units produced by the exact replay
+    ("q1_heads_bw50", 50, 1, ["-f", "-k", "0"], ()),
+    ("q1_leak_chain", 50, 1, ["-f", "-k", "0"], ("c1", "c3")),
+    ("q1_nondir", 50, 1, ["-D", "-y", "-k", "0"], ("c2",)),
+    ("whole_replay_r0", 50, 1, ["-f", "-r", "0", "-k", "0"], ()),
+    ("whole_replay_bw300", 300, 2, ["-f", "-k", "0"], ("c1",)),
+    ("parallel_bw200_heads", 200, 1, ["-f", "-k", "0"], ()),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PROFILE_REPLAY_CASES, ids=lambda c: c[0])
+def test_regions_cli_profile_replayed_units(orc_bin, gpu_lib, tmp_path, case):
+    """-w where units come from the exact replay (quirk Q1 head hits and
+    their leak chains, -r <= 0, bw > 255): the profile is written from the
+    replayed state machine's own retirements (misc/peakcall.cpp:80-83), in
+    the reference's order, byte-identical"""
+    name, bw, ns, args, tiny = case
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    contigs = [("c0", 9000), ("c1", 4000), ("c2", 400), ("c3", 7000), ("c4", 5000)]
+    ct = tmp_path / "contigs.txt"
+    write_contigs(ct, contigs)
+    files = []
+    for i in range(ns):
+        fwd, rev = gen_head_sample(rng, contigs, bw, tiny)
+        p = tmp_path / f"s{i}.wig"
+        write_wig(p, f"s{i}", fwd, rev)
+        files.append(str(p))
+    common = ["-q", "-c", str(ct), "-b", str(bw), "-m", "3000"] + args
+    (tmp_path / "ref").mkdir()
+    (tmp_path / "got").mkdir()
+    run([orc_bin, "regions"] + common + ["-w", "ref/p.wig", "-o", "ref/r.txt"] + files, tmp_path)
+    run([os.path.join(BIN, "regions")] + common + ["-w", "got/p.wig", "-o", "got/r.txt"] + files, tmp_path)
+    assert (tmp_path / "ref/r.txt").read_bytes() == (tmp_path / "got/r.txt").read_bytes()
+    a, b = (tmp_path / "ref/p.wig").read_bytes(), (tmp_path / "got/p.wig").read_bytes()
+    assert a.count(b"\n") > 100
+    assert a == b, "profile differs at byte %d" % next(
+        (i for i, (x, y) in enumerate(zip(a, b)) if x != y), min(len(a), len(b)))

@@ -71,6 +71,7 @@ EXPORTS = [
     "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan", "up_shift_best",
     "up_timings", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
     "up_host_register", "up_unit_profile_range", "up_run_async", "up_run_wait", "up_set_timing",
+    "up_set_profile_capture", "up_unit_replay_profile",
 ]
 
 
@@ -119,6 +120,9 @@ def load_library(path=LIB_PATH):
         "up_set_record_target": (c.c_int, [vp, vp, c.c_uint64]),
         "up_host_register": (c.c_int, [vp, vp, c.c_uint64]),
         "up_unit_profile_range": (c.c_int, [vp, c.c_uint32, c.c_uint64, c.c_uint32, vp, vp]),
+        "up_set_profile_capture": (c.c_int, [vp, c.c_int]),
+        "up_unit_replay_profile": (c.c_int, [vp, c.c_uint32, u32p, c.POINTER(c.c_uint64), vp, vp, vp,
+                                             c.c_uint64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -312,3 +316,19 @@ class Lib:
         r = np.zeros(length, np.float64)
         _ck(self.L.up_unit_profile(self.ctx, unit, f.ctypes.data, r.ctypes.data, length))
         return f, r
+
+    def set_profile_capture(self, on):
+        _ck(self.L.up_set_profile_capture(self.ctx, int(bool(on))))
+
+    def replay_profile(self, unit):
+        """(resync, event[], pos[], score[]) of a replayed unit (up_unit_replay_profile)"""
+        rs, n = ctypes.c_uint32(), ctypes.c_uint64()
+        _ck(self.L.up_unit_replay_profile(self.ctx, unit, ctypes.byref(rs), ctypes.byref(n), None, None,
+                                          None, 0))
+        ev = np.zeros(n.value, np.uint32)
+        pos = np.zeros(n.value, np.uint32)
+        sc = np.zeros(n.value, np.float64)
+        if n.value:
+            _ck(self.L.up_unit_replay_profile(self.ctx, unit, ctypes.byref(rs), ctypes.byref(n),
+                                              ev.ctypes.data, pos.ctypes.data, sc.ctypes.data, n.value))
+        return rs.value, ev, pos, sc

@@ -257,6 +257,17 @@ struct up_ctx {
     DevBuf<double> d_reg_f, d_reg_r;
     DevBuf<up_region> d_emu_out;
     DevBuf<double> d_ring_f, d_ring_r;   // K0 window in global memory (very wide kernels)
+    // -w of replayed units (up_set_profile_capture): K0's nonzero
+    // retirements, device buffers and the last run's host copy, per unit
+    bool prof_capture = false;
+    uint64_t pf_cap = 1u << 20;
+    DevBuf<uint32_t> d_pf_unit, d_pf_event, d_pf_pos;
+    DevBuf<double> d_pf_score;
+    DevBuf<unsigned long long> d_pf_n;
+    std::vector<uint32_t> h_pf_event, h_pf_pos;
+    std::vector<double> h_pf_score;
+    std::vector<uint64_t> h_pf_off;      // [units + 1]: each unit's slice of the h_pf_* arrays
+    std::vector<uint32_t> h_resync;      // per unit: 0 not replayed, X resync, ~0 replayed to the end
     // K4 (up_shift_scan) buffers, kept across calls
     DevBuf<uint64_t> d_sh_idx, d_sh_off;
     DevBuf<double> d_sh_slab, d_sh_out;
@@ -421,6 +432,8 @@ void up_close(up_ctx *c) {
     c->d_emu_scores.release(); c->d_emu_score_off.release(); c->d_emu_nscores.release();
     c->d_sh_idx.release(); c->d_sh_off.release(); c->d_sh_slab.release(); c->d_sh_out.release();
     c->d_sh_pref.release();
+    c->d_pf_unit.release(); c->d_pf_event.release(); c->d_pf_pos.release(); c->d_pf_score.release();
+    c->d_pf_n.release();
     for (int k = 0; k < kSlots; ++k) {
         c->hp_regions[k].release(); c->hp_counts[k].release(); c->hp_status[k].release(); c->hp_head[k].release();
         for (auto &e : c->pass[k].ev) (void)hipEventDestroy(e);
@@ -1195,6 +1208,20 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
         E.out_score_off = c->d_emu_score_off.p;
         E.nscores = c->d_emu_nscores.p;
         E.scores_cap = c->d_emu_scores.n;
+        if (c->prof_capture) {
+            HIPCHK(c->d_pf_unit.ensure(c->pf_cap));
+            HIPCHK(c->d_pf_event.ensure(c->pf_cap));
+            HIPCHK(c->d_pf_pos.ensure(c->pf_cap));
+            HIPCHK(c->d_pf_score.ensure(c->pf_cap));
+            HIPCHK(c->d_pf_n.ensure(1));
+            HIPCHK(hipMemsetAsync(c->d_pf_n.p, 0, sizeof(unsigned long long), c->stream));
+            E.prof_unit = c->d_pf_unit.p;
+            E.prof_event = c->d_pf_event.p;
+            E.prof_pos = c->d_pf_pos.p;
+            E.prof_score = c->d_pf_score.p;
+            E.nprof = c->d_pf_n.p;
+            E.prof_cap = c->pf_cap;
+        }
         hipLaunchKernelGGL(emulate_kernel, dim3(2), dim3(64), ring_lds ? ring_bytes : 0, c->stream, E);
         HIPCHK(hipGetLastError());
         uint32_t nemu = 0, err = 0;
@@ -1207,6 +1234,13 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
             fprintf(stderr, "unipeak_hip: exact replay: positions out of order\n");
             return UP_E_ARG;
         }
+        if (err & 16u) {  // the -w capture is full
+            unsigned long long used = 0;
+            HIPCHK(hipMemcpy(&used, c->d_pf_n.p, sizeof used, hipMemcpyDeviceToHost));
+            c->pf_cap = std::max<uint64_t>(c->pf_cap * 4, used + used / 4);
+            --attempt;  // growth only: the capture has no upper bound of its own
+            continue;
+        }
         if (err & 11u) {  // 1: a region longer than reg_cap positions, 2: more than out_cap
                           // regions, 8: the region-score slab is full
             if (err & 1u) c->emu_reg_cap *= 4;
@@ -1217,6 +1251,32 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
                 c->emu_scores_cap = std::max<uint64_t>(c->emu_scores_cap * 4, used + used / 4);
             }
             continue;
+        }
+        c->h_resync = resync;
+        if (c->prof_capture) {  // the captured retirements, grouped by unit (emission order kept)
+            unsigned long long np = 0;
+            HIPCHK(hipMemcpy(&np, c->d_pf_n.p, sizeof np, hipMemcpyDeviceToHost));
+            std::vector<uint32_t> pu(np), pe(np), pp(np);
+            std::vector<double> ps_(np);
+            if (np) {
+                HIPCHK(hipMemcpy(pu.data(), c->d_pf_unit.p, np * 4, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(pe.data(), c->d_pf_event.p, np * 4, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(pp.data(), c->d_pf_pos.p, np * 4, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(ps_.data(), c->d_pf_score.p, np * 8, hipMemcpyDeviceToHost));
+            }
+            c->h_pf_off.assign(nu + 1, 0);
+            for (uint64_t i = 0; i < np; ++i) ++c->h_pf_off[pu[i] + 1];
+            for (uint32_t u = 0; u < nu; ++u) c->h_pf_off[u + 1] += c->h_pf_off[u];
+            std::vector<uint64_t> fill(c->h_pf_off.begin(), c->h_pf_off.end() - 1);
+            c->h_pf_event.resize(np);
+            c->h_pf_pos.resize(np);
+            c->h_pf_score.resize(np);
+            for (uint64_t i = 0; i < np; ++i) {  // one buffer's entries are in slot order
+                const uint64_t k = fill[pu[i]]++;
+                c->h_pf_event[k] = pe[i];
+                c->h_pf_pos[k] = pp[i];
+                c->h_pf_score[k] = ps_[i];
+            }
         }
         emu.resize(nemu);
         ecnt.resize((size_t)nemu * S);
@@ -1265,6 +1325,8 @@ static int replay_head_hits(up_ctx *c, int slot) {
     const uint32_t *head = c->hp_head[slot].p;
     bool any = false;
     for (uint32_t i = 0; i < nu; ++i) any |= head[i] != 0;
+    c->h_resync.assign(nu, 0);  // no unit replayed (yet)
+    c->h_pf_off.assign(nu + 1, 0);
     if (!any) return UP_OK;
     // the head flags are a function of the (unchanged) tracks, so d_head of
     // a later pass still describes this one
@@ -1723,6 +1785,8 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
     int r = sync_units(c);
     if (r) return r;
     const uint32_t nu = (uint32_t)c->units.size();
+    c->h_resync.assign(nu, 0);
+    c->h_pf_off.assign(nu + 1, 0);
     up_ctx::Pass ps;
     ps.target = c->target;
     ps.target_hostp = c->target_hostp;
@@ -2023,3 +2087,30 @@ int up_hbm_copy_gbps(up_ctx *c, uint64_t bytes, int reps, double *gbps) {
     return UP_OK;
 }
 
+
+int up_set_profile_capture(up_ctx *c, int on) {
+    if (!c) return UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;
+    c->prof_capture = on != 0;
+    return UP_OK;
+}
+
+int up_unit_replay_profile(up_ctx *c, uint32_t unit, uint32_t *resync, uint64_t *n, uint32_t *event,
+                           uint32_t *pos, double *score, uint64_t cap) {
+    if (!c || !resync || !n) return UP_E_ARG;
+    if (!c->ran) return UP_E_STATE;
+    if (unit >= c->units.size()) return UP_E_ARG;
+    *resync = unit < c->h_resync.size() ? c->h_resync[unit] : 0u;
+    if (*resync != 0 && !c->prof_capture) return UP_E_STATE;  // replayed without the capture on
+    const uint64_t lo = unit + 1 < c->h_pf_off.size() ? c->h_pf_off[unit] : 0;
+    const uint64_t hi = unit + 1 < c->h_pf_off.size() ? c->h_pf_off[unit + 1] : 0;
+    *n = hi - lo;
+    if (!event && !pos && !score) return UP_OK;  // size query
+    if (cap < hi - lo || !event || !pos || !score) return UP_E_ARG;
+    for (uint64_t i = lo; i < hi; ++i) {
+        event[i - lo] = c->h_pf_event[i];
+        pos[i - lo] = c->h_pf_pos[i];
+        score[i - lo] = c->h_pf_score[i];
+    }
+    return UP_OK;
+}

@@ -63,7 +63,17 @@ struct EmuParams {
     uint64_t *out_score_off;     // [out_cap], ~0 when the slab was full
     unsigned long long *nscores;
     uint64_t scores_cap;
+    // -w (density profile) of replayed units: every processPosition with a
+    // nonzero score (peakcall.cpp:80-83) as (unit, event, pos, score), in
+    // emission order per buffer; event = index of the unit's add() whose
+    // retirement loop wrote it, or kFlushEvent for its flushContig()
+    uint32_t *prof_unit, *prof_event, *prof_pos;  // null: not captured
+    double *prof_score;
+    unsigned long long *nprof;
+    uint64_t prof_cap;
 };
+
+constexpr uint32_t kFlushEvent = 0xFFFFFFFFu;
 
 struct EmuState {
     // window: deque[j] = cell (head + j) % W
@@ -80,6 +90,7 @@ struct EmuState {
     uint32_t nhits;
     uint32_t cur_unit;
     uint32_t close_pos;   // position of the add being processed, 0 during a flush
+    uint32_t ev;          // index of that add within the unit (kFlushEvent: the flush)
     bool aligned;
     uint64_t horizon;     // positions <= horizon may hold misaligned leftovers
     bool resynced;
@@ -221,6 +232,17 @@ __device__ static void emu_process(const EmuParams &P, EmuState &E, uint32_t pos
         if (E.left != 0) emu_region(P, E);
         if (score >= P.region_thr) emu_addpos(P, E, hc, f, r);
     }
+    if (P.prof_score && score != 0.0) {  // profileOut_->write(PosScore(...)), peakcall.cpp:80-83
+        const unsigned long long k = atomicAdd(P.nprof, 1ull);
+        if (k < P.prof_cap) {
+            P.prof_unit[k] = E.cur_unit;
+            P.prof_event[k] = E.ev;
+            P.prof_pos[k] = pos;
+            P.prof_score[k] = score;
+        } else {
+            atomicOr(P.err, 16u);
+        }
+    }
     E.last_pos = pos;
     // resync: aligned, leftovers retired, nothing open
     if (!P.replay_all && E.aligned && (uint64_t)pos > E.horizon && E.n == 0) E.resynced = true;
@@ -318,6 +340,7 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
             }
             in_chain = true;
         }
+        uint32_t nadd = 0;  // add() calls of this unit so far (lane 0)
         if (lane == 0) {
             E.cur_unit = u;  // contig switch relabels the open region (peakcall.cpp:164-168)
             E.aligned = false;
@@ -350,6 +373,7 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
                         uint32_t counts[256];
                         for (int s = 0; s < S; ++s) counts[s] = count_at(U, S, nstr == 2 ? st : 0, s, pos);
                         E.close_pos = pos;
+                        E.ev = nadd++;
                         const bool first_aligned = !E.aligned && pos > (uint32_t)P.bw;
                         emu_add(P, E, counts, pos, nstr == 2 ? st == 0 : P.unit_buffer[u] == 0);
                         if (first_aligned) {
@@ -368,6 +392,7 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
             } else {
                 // explicit flushContig() at the end of the unit's pass
                 E.close_pos = 0;
+                E.ev = kFlushEvent;
                 emu_add(P, E, nullptr, E.buffer_pos + E.W, true);
                 E.buffer_pos = 0;
                 E.last_pos = 0;

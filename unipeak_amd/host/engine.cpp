@@ -409,6 +409,7 @@ void run_units(const EngineParams &ep, PassResult &out) {
         p.coeffs = ep.coeffs.empty() ? nullptr : ep.coeffs.data();
         p.n_coeffs = (uint32_t)ep.coeffs.size();
         if ((rc = up_set_params(job.ctx, &p))) return fail(rc, "up_set_params");
+        if (ep.profile && (rc = up_set_profile_capture(job.ctx, 1))) return fail(rc, "up_set_profile_capture");
         std::vector<uint32_t> tp, tc;
         for (uint32_t gi : job.units) {
             const UnitBuild &u = out.units[gi];
@@ -601,35 +602,77 @@ void write_profile(const PassResult &pr, uint16_t bw, ProfileSink &sink) {
     std::vector<std::pair<up_ctx *, uint32_t>> where(pr.units.size(), {nullptr, 0});
     for (const DeviceJob &j : g_jobs)
         for (size_t k = 0; k < j.dev_unit.size(); ++k) where[j.dev_unit[k]] = {j.ctx, (uint32_t)k};
-    for (const UnitBuild &u : pr.units)
-        if (u.head_hit)
-            fatal("-w with tags within the first bandwidth positions of a contig (quirk Q1) is not "
-                  "supported on the GPU path yet");
-    // retirement events: add() at p after q retires q-bw .. q-bw+min(W,p-q)-1
-    // (peakcall.cpp:171-184); flushContig() retires q-bw .. q+bw
-    struct Ev { uint64_t t; uint32_t unit; int64_t lo, hi; };
+    // Units the exact replay produced (quirk Q1 heads, -r <= 0, bw > 255)
+    // hand over their retirements as the state machine wrote them: every
+    // nonzero (pos, score) with the add() -- or flush -- whose retirement loop
+    // wrote it.  Positions at or after a resync point follow the dense KDE.
+    struct Replayed { uint32_t resync = 0; std::vector<uint32_t> event, pos; std::vector<double> score; };
+    std::vector<Replayed> rep(pr.units.size());
+    for (uint32_t k = 0; k < pr.units.size(); ++k) {
+        Replayed &r = rep[k];
+        uint64_t n = 0;
+        int rc = up_unit_replay_profile(where[k].first, where[k].second, &r.resync, &n, nullptr, nullptr,
+                                        nullptr, 0);
+        if (rc != UP_OK) fatal(std::string("up_unit_replay_profile: ") + up_strerror(rc));
+        r.event.resize(n);
+        r.pos.resize(n);
+        r.score.resize(n);
+        if (n && (rc = up_unit_replay_profile(where[k].first, where[k].second, &r.resync, &n, r.event.data(),
+                                              r.pos.data(), r.score.data(), n)) != UP_OK)
+            fatal(std::string("up_unit_replay_profile: ") + up_strerror(rc));
+    }
+    // retirement events in the driver's call order: add() at p after q retires
+    // q-bw .. q-bw+min(W,p-q)-1 (peakcall.cpp:171-184); flushContig()
+    // retires q-bw .. q+bw.  A replayed unit's entries go out at the event
+    // that wrote them, before the dense positions of the same event.
+    struct Ev { uint64_t t; uint32_t unit; int kind; int64_t lo, hi; };  // kind 0: replayed [lo, hi) entries
     std::vector<Ev> ev;
     const int64_t W = 2 * (int64_t)bw + 1;
     for (uint32_t k = 0; k < pr.units.size(); ++k) {
         const UnitBuild &u = pr.units[k];
+        const Replayed &r = rep[k];
+        for (size_t i = 0; i < r.event.size();) {  // runs of one event
+            size_t j = i;
+            while (j < r.event.size() && r.event[j] == r.event[i]) ++j;
+            const uint32_t e = r.event[i];
+            uint64_t t;
+            if (e == UP_FLUSH_EVENT) t = u.flush_time;
+            else if (e < u.add_time.size()) t = u.add_time[e];
+            else fatal("-w: the replay's add index exceeds the unit's adds");
+            ev.push_back({t, k, 0, (int64_t)i, (int64_t)j});
+            i = j;
+        }
+        if (r.resync == UP_FLUSH_EVENT) continue;  // replayed to the end
+        const int64_t x0 = r.resync ? (int64_t)r.resync : 1;  // dense from the resync point on
         int64_t q = 0;
         for (size_t i = 0; i < u.add_pos.size(); ++i) {
             const int64_t p = u.add_pos[i];
             if (q != 0 && p > q) {
                 const int64_t n = std::min<int64_t>(W, p - q);
-                ev.push_back({u.add_time[i], k, std::max<int64_t>(1, q - bw), q - bw + n - 1});
+                const int64_t lo = std::max<int64_t>({1, q - bw, x0}), hi = q - bw + n - 1;
+                if (lo <= hi) ev.push_back({u.add_time[i], k, 1, lo, hi});
             }
             q = p;
         }
-        if (q != 0) ev.push_back({u.flush_time, k, std::max<int64_t>(1, q - bw), q + bw});
+        if (q != 0) {
+            const int64_t lo = std::max<int64_t>({1, q - bw, x0}), hi = q + bw;
+            if (lo <= hi) ev.push_back({u.flush_time, k, 1, lo, hi});
+        }
     }
-    std::sort(ev.begin(), ev.end(), [](const Ev &a, const Ev &b) { return a.t < b.t; });
+    std::stable_sort(ev.begin(), ev.end(), [](const Ev &a, const Ev &b) {
+        return a.t != b.t ? a.t < b.t : a.kind < b.kind;
+    });
     // per-unit cache of one chunk of the device profile
     constexpr uint32_t kChunkPos = 1u << 22;
     struct Cache { int64_t first = -1; std::vector<double> f, r; };
     std::vector<Cache> cache(pr.units.size());
     for (const Ev &e : ev) {
         const UnitBuild &u = pr.units[e.unit];
+        if (e.kind == 0) {
+            const Replayed &r = rep[e.unit];
+            for (int64_t i = e.lo; i < e.hi; ++i) sink.write(u.buffer == 0, u.contig, r.pos[i], r.score[i]);
+            continue;
+        }
         Cache &c = cache[e.unit];
         for (int64_t x = e.lo; x <= e.hi; ++x) {
             if (c.first < 0 || x < c.first || x >= c.first + (int64_t)kChunkPos) {

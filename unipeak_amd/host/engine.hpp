@@ -53,6 +53,7 @@ struct EngineParams {
     std::vector<uint8_t> control;
     std::vector<double> coeffs;
     int ngpus = 0;           // 0: all visible devices
+    bool profile = false;    // -w: capture the exact replay's retirements too
 };
 
 // replay the merge loop; directional = two buffers and two passes

@@ -220,6 +220,7 @@ int main(int argc, char **argv) {
     ep.control = control;
     ep.coeffs = coeffs;
     ep.ngpus = env_gpus();
+    ep.profile = prof.fp != nullptr;
     run_units(ep, pr);
     timer.mark("gpu");
     if (prof.fp) {
