@@ -95,7 +95,7 @@ def load_table(names):
 def pmc_traffic(bytes_per_launch):
     """HBM bytes per K1a launch from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.py) when they were taken on this exact workload."""
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", rnd, "k1a_pmc_traffic.json")
         try:
             d = json.load(open(p))
@@ -158,8 +158,9 @@ def main():
         raise SystemExit("UNIPEAK_SIM_WORLD is for single-process runs")
     units, owner, mine_all = shard.plan(lens, nondir=nondir, world=sim_world or world, n_samples=S)
     mine = mine_all[sim_rank if sim_world > 1 else rank]
-    # resident track bytes: 4-bit counts, two positions per byte
-    need = sum(lens[units[k][0]] * nstr * S for k in mine) / 2
+    # resident track bytes: TB-bit counts
+    TB = capi.track_bits()
+    need = sum(lens[units[k][0]] * nstr * S for k in mine) * TB / 8
     if need > 250e9:
         raise SystemExit(f"workload {args.workload} needs {need / 1e9:.0f} GB of tracks per GPU at "
                          f"N={world}; run it on more GPUs")
@@ -193,9 +194,9 @@ def main():
                     local_tags += g2.tag_total(u, st, smp)
         g2.close()
     gen_s = time.time() - t_gen
-    # K1a algorithmic bytes: one 4-bit count per bp per strand per non-control
-    # sample
-    alg_bytes = sum(lens[units[k][0]] * nstr * s_nc for k in mine) // 2
+    # K1a algorithmic bytes: one TB-bit count per bp per strand per
+    # non-control sample
+    alg_bytes = sum(lens[units[k][0]] * nstr * s_nc for k in mine) * TB // 8
     copy_gbps = g.hbm_copy_gbps(1 << 30, 5)
 
     phase = {"allreduce": 0.0, "launch": 0.0, "wait": 0.0, "gather_merge": 0.0}
@@ -477,7 +478,7 @@ def main():
                          "kernel": "scan_kernel<..., kModeScreen> (K1a: stream + integer screen)",
                          "kernel_ms": round(k1a_ms, 4), "kernel_ms_max_rank": round(k1a_max, 4),
                          "bytes_per_launch": int(alg_bytes),
-                         "bytes_rule": "0.5 B (4-bit count) per bp per strand per non-control sample",
+                         "bytes_rule": f"{TB / 8} B ({TB}-bit count) per bp per strand per non-control sample",
                          "kernel_note": "mean K1a duration over the timed passes (HIP events on the pass "
                                         "stream); passes overlap, so K1a shares the GPU with earlier "
                                         "passes' K1b/K2/K3",
@@ -491,7 +492,7 @@ def main():
         }
         # SURVEY §8(d)'s pricing: one uint32 count per bp per strand per
         # non-control sample (8 * S_nc B/bp over both strands), beside the
-        # 4-bit layout's algorithmic bytes the kernel actually reads
+        # layout's algorithmic bytes the kernel actually reads
         survey_bytes = sum(lens[units[k][0]] * nstr * s_nc for k in mine_all[0]) * 4 if world == 1 else None
         rf = res["roofline"]
         rf["frac_step"] = round(alg_bytes / dt / 1e9 / HBM_PEAK_GBS, 4)  # whole pass at the step rate
@@ -502,7 +503,7 @@ def main():
             rf["bytes_per_launch_survey"] = int(survey_bytes)
             rf["frac_survey_rule"] = round(survey_bytes / (k1a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             rf["survey_rule_note"] = ("above 1: the kernel does not read SURVEY's uint32 bytes -- the tracks are "
-                                      "4-bit counts with an exact overflow table (DESIGN.md §3)")
+                                      f"{TB}-bit counts with an exact overflow table (DESIGN.md §3)")
         if world == 1 and not args.no_cpu_baseline and args.workload == "hg19-dir1":
             res["cpu_baseline"] = cpu_baseline(contigs, args, value, bg_set[0], last[1])
         print(json.dumps(res), flush=True)
@@ -620,7 +621,8 @@ def shift_pipeline(args, W):
         ka.append(ga.timings()[0])
         kb.append(gb.timings()[0])
     dt = (time.perf_counter() - t0) / args.steps
-    alg = genome  # K1a of each pass: both strands x 0.5 B per bp
+    TB = capi.track_bits()
+    alg = genome * 2 * TB // 8  # K1a of each pass: both strands x TB/8 B per bp
     k1a = float(np.mean(ka + kb))
     res = {
         "metric": METRIC, "value": round(genome / dt / 1e9, 3), "unit": "Gbp/s", "n_gpus": 1,
@@ -635,7 +637,7 @@ def shift_pipeline(args, W):
                      "unit": "GB/s", "frac": round(alg / (k1a * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": None, "kernel": "scan_kernel<..., kModeScreen> (K1a), both passes",
                      "kernel_ms": round(k1a, 4), "bytes_per_launch": int(alg),
-                     "bytes_rule": "0.5 B (4-bit count) per bp per strand, both strands"},
+                     "bytes_rule": f"{TB / 8} B ({TB}-bit count) per bp per strand, both strands"},
     }
     print(json.dumps(res), flush=True)
     for g, _ in ctx:

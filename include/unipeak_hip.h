@@ -95,6 +95,9 @@ typedef struct {
 
 /* library / device */
 int up_version(void);
+/* bits per stored count in a device track: the K1a stream
+ * reads bits/8 bytes per position per strand per non-control sample */
+int up_track_bits(void);
 const char *up_strerror(int code);
 int up_device_count(int *n);
 
@@ -109,9 +112,9 @@ int up_set_params(up_ctx *ctx, const up_params *p);
  * reverse buffer) over one contig pass; units of one buffer must be added in
  * the order the buffer sees them.  nstrands is 1 (directional) or 2
  * (nondirectional: strand 0 forward, 1 reverse).  Tracks start zeroed and
- * cover positions 1..contig_len; in device memory they are 4-bit counts (two
- * positions per byte) with the escape nibble 15 and an exact per-unit
- * overflow table for counts >= 15, so any uint32 count can
+ * cover positions 1..contig_len; in device memory they are up_track_bits()-bit
+ * counts (2: four positions per byte) whose largest value is an escape into
+ * an exact per-unit overflow table, so any uint32 count can
  * be written.
  * Quirk Q1 (misc/peakcall.cpp:177-183): a unit with pooled tags at a position
  * <= bw is replayed by the exact state machine; if all of its adds sit at
@@ -238,6 +241,60 @@ int up_unit_replay_profile(up_ctx *ctx, uint32_t unit, uint32_t *resync, uint64_
  * NULL for directional units */
 int up_unit_profile_range(up_ctx *ctx, uint32_t unit, uint64_t first, uint32_t count,
                           double *out_f, double *out_r);
+
+/* ---- tags_in_regions (src/tags_in_regions.cpp:131-199) on the GPU ---------
+ * A stream is one sample's alignment records in the order the reference's
+ * readAlign() returns them (ParseAlignStream / NondirParseAlignStream,
+ * misc/format.cpp:503-565, 873-895): key[i] = contig << 32 | firstPos,
+ * count[i] (> 0), forward[i].  The reference walks one cursor per stream
+ * through the regions (skip to the region's strand at (contig, left), then
+ * count every record on the contig at firstPos <= right, any strand: quirk
+ * Q12).  up_tir_query answers every (region, stream) pair as if that
+ * stream's cursor started at its first record: first = the record the skip
+ * loop stops at, end = the record the count loop stops at (n: exhausted),
+ * hits = sum of counts in [first, end) (uint32, wrapping like HitCount).
+ * That is the reference's answer whenever the real cursor has not passed
+ * `first` (nothing in between qualifies); the caller walks the other regions
+ * itself (bin/tags_in_regions does).  UP_TIR_HOST in first/end:
+ * the query crossed more unsorted runs of the stream than the device walks
+ * (an unsorted stream); the caller walks that pair. */
+#define UP_TIR_HOST 0xFFFFFFFFu
+typedef struct up_tir up_tir;
+int up_tir_open(int hip_device, up_tir **out);
+void up_tir_close(up_tir *h);
+/* upload stream `stream` (0..4095) and build its prefix sums and skip tables
+ * on the device (blocking; the host arrays may be freed afterwards) */
+int up_tir_set_stream(up_tir *h, uint32_t stream, uint64_t n, const uint64_t *key,
+                      const uint32_t *count, const uint8_t *forward);
+/* regions r = 0..n_regions-1 against streams 0..n_streams-1; outputs are
+ * [n_regions][n_streams] */
+int up_tir_query(up_tir *h, uint32_t n_streams, uint64_t n_regions, const uint32_t *contig,
+                 const uint32_t *left, const uint32_t *right, const uint8_t *forward,
+                 uint32_t *first, uint32_t *end, uint32_t *hits);
+/* device time in ms: [0] the last up_tir_set_stream's table build (after the
+ * upload), [1] the last up_tir_query's kernel */
+int up_tir_timings(up_tir *h, double *ms, int n);
+
+/* ---- convert_align's CountMap (misc/data.cpp:263-314, 321-596) on the GPU --
+ * Per (strand, contig) position -> count, as dense uint32 tracks in HBM
+ * (2 x the table's total length x 4 B).  up_cm_add = CountMap::add for n
+ * alignments (contig < n_contigs, 1 <= pos <= its length, else UP_E_ARG;
+ * count NULL = 1 each; per-position counts wrap at 2^32 like HitCount).
+ * up_cm_collect = the nonzero entries in the order convert_align writes
+ * them: nondir 0 -- CountMap::ConstIterator, forward strand then reverse,
+ * contigs in table order, positions ascending; nondir 1 --
+ * ConstNondirIterator, both strands merged by position with their counts
+ * added (forward[] = 1).  With every output NULL only *n is set; cap is the
+ * output arrays' length. */
+typedef struct up_cm up_cm;
+int up_cm_open(int hip_device, uint32_t n_contigs, const uint32_t *contig_len, up_cm **out);
+void up_cm_close(up_cm *h);
+int up_cm_add(up_cm *h, uint64_t n, const uint32_t *contig, const uint32_t *pos,
+              const uint8_t *forward, const uint32_t *count);
+int up_cm_collect(up_cm *h, int nondir, uint64_t *n, uint32_t *contig, uint32_t *pos,
+                  uint32_t *count, uint8_t *forward, uint64_t cap);
+/* device time in ms: [0] every up_cm_add kernel so far, [1] the last collect */
+int up_cm_timings(up_cm *h, double *ms, int n);
 
 #ifdef __cplusplus
 }

@@ -2,8 +2,8 @@
 reference CLIs: byte-identical region tables, strand_shift reports and
 tags_in_regions tables on seeded synthetic wiggle inputs.
 
-bin/regions and bin/strand_shift need the GPU (gpu marker);
-bin/tags_in_regions is host-only and runs on CPU."""
+Every CLI needs the GPU (gpu marker); bin/tags_in_regions is tested in
+tests/test_gpu_tir.py."""
 import os
 import zlib
 import subprocess
@@ -195,35 +195,6 @@ def test_strand_shift_cli_matches_oracle(orc_bin, gpu_lib, tmp_path, seed):
                        ["-c", ct, "-x", "100", "-n", "10", "-u", "0", "-g", "50", "-m", "20000000"]
                        + files)
     assert "# best_shift=" in out
-
-
-def test_tags_in_regions_cli_matches_oracle(orc_bin, tmp_path):
-    """host-only: build a region table with the oracle, then count 2 extra samples."""
-    ct, files = make_inputs(tmp_path, 5, HG_LIKE, 3)
-    regions = tmp_path / "regions.txt"
-    run([orc_bin, "regions", "-q", "-f", "-c", ct, "-o", str(regions), files[0]], tmp_path)
-    for extra in (["-e", "30"], []):
-        compare_tool(orc_bin, tmp_path, "tags_in_regions",
-                     ["-c", ct, "-f", str(regions)] + extra + files[1:])
-    # nondirectional input table
-    nd = tmp_path / "nd.txt"
-    run([orc_bin, "regions", "-q", "-D", "-c", ct, "-o", str(nd), files[0]], tmp_path)
-    compare_tool(orc_bin, tmp_path, "tags_in_regions", ["-D", "-c", ct, "-f", str(nd)] + files[1:],
-                 outname="nd_out.txt")
-
-
-def test_tags_in_regions_q12_reverse_mislabel(orc_bin, tmp_path):
-    """Q12: a forward-labelled reverse region counts 0 (no strand check in the
-    count loop; survey probe `chrA:5011-5162 55 0`)."""
-    write_contigs(tmp_path / "ct.txt", [("chrA", 20000)])
-    write_wig(tmp_path / "a.wig", "a", {}, {"chrA": [(5100, 30), (8000, 30)]})
-    (tmp_path / "r.txt").write_text("# x\n\tkurtosis\ta\nchrA:5011-5162\t1.00\t30\n"
-                                    "chrA:8060-7940\t1.00\t30\n")
-    out = compare_tool(orc_bin, tmp_path, "tags_in_regions",
-                       ["-c", "ct.txt", "-f", "r.txt", "a.wig"])
-    rows = [l.split("\t") for l in out.strip().split("\n") if not l.startswith(("#", "\t"))]
-    # the forward-labelled region skips (and so consumes) the reverse tags
-    assert rows[0][-1] == "0" and rows[1][-1] == "0"
 
 
 def test_cli_usage_errors(tmp_path):

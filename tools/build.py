@@ -1,7 +1,8 @@
 """Build every native artefact in-tree (used by __graft_entry__.build()).
 
   unipeak_amd/lib/libunipeak_hip.so   HIP kernels + C-ABI (gfx950)
-  bin/regions, bin/strand_shift, bin/tags_in_regions   C++ host CLIs
+  bin/regions, bin/strand_shift, bin/tags_in_regions, bin/convert_align
+                                      C++ host CLIs
   oracle/_build/liboracle.so, oracle/_build/orc        CPU restatement
                                                        (test infrastructure)
 Rebuilds only what is older than its sources.
@@ -29,9 +30,10 @@ def _run(cmd, cwd=ROOT):
 
 
 def compile_lib(out, extra=(), jobs=None):
-    """libunipeak_hip.so from five translation units compiled in parallel:
-    api.hip (C-ABI, non-templated kernels) and nh_tu.hip once per window
-    width NH = 1..4 (the templated K1/K3/K4 kernels)."""
+    """libunipeak_hip.so from six translation units compiled in parallel:
+    api.hip (C-ABI, non-templated kernels), tir.hip (tags_in_regions) and
+    nh_tu.hip once per window width NH = 1..4 (the templated K1/K3/K4
+    kernels)."""
     from concurrent.futures import ThreadPoolExecutor
     csrc = os.path.join(ROOT, "unipeak_amd", "csrc")
     objdir = os.path.join(ROOT, "build", "obj_" + os.path.basename(out).replace(".so", ""))
@@ -39,14 +41,16 @@ def compile_lib(out, extra=(), jobs=None):
     os.makedirs(os.path.dirname(out), exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
              "-I", os.path.join(ROOT, "include")] + list(extra)
-    units = [("api", os.path.join(csrc, "api.hip"), [])] + [
+    units = [("api", os.path.join(csrc, "api.hip"), []),
+             ("tir", os.path.join(csrc, "tir.hip"), []),
+             ("countmap", os.path.join(csrc, "countmap.hip"), [])] + [
         (f"nh{k}", os.path.join(csrc, "nh_tu.hip"), [f"-DUPK_NH_TU={k}"]) for k in (1, 2, 3, 4)]
     def one(u):
         name, src, defs = u
         obj = os.path.join(objdir, name + ".o")
         _run([HIPCC] + flags + defs + ["-c", "-o", obj, src])
         return obj
-    with ThreadPoolExecutor(jobs or min(5, os.cpu_count() or 1)) as ex:
+    with ThreadPoolExecutor(jobs or min(7, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(one, units))
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
     return out
@@ -79,7 +83,7 @@ def build_cli(force=False):
             _run(["g++", "-O2", "-std=c++17", "-Wall", "-ffp-contract=off", "-fno-fast-math",
                   "-I", os.path.join(ROOT, "include"), "-o", out, m] + common +
                  ["-L", lib, "-lunipeak_hip", "-Wl,-rpath,$ORIGIN/../unipeak_amd/lib",
-                  "-lpthread"])
+                  "-lpthread", "-lz"])
         outs.append(out)
     return outs
 

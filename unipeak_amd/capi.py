@@ -65,14 +65,16 @@ assert REGION_DTYPE.itemsize == ctypes.sizeof(Region)
 _lib = None
 
 EXPORTS = [
-    "up_version", "up_strerror", "up_device_count", "up_kernel_weights", "up_open",
+    "up_version", "up_track_bits", "up_strerror", "up_device_count", "up_kernel_weights", "up_open",
     "up_close", "up_set_params", "up_add_unit", "up_unit_count", "up_unit_pack",
     "up_unit_scatter", "up_unit_synth", "up_unit_synth_offset", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
     "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan", "up_shift_best",
     "up_timings", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
     "up_host_register", "up_unit_profile_range", "up_run_async", "up_run_wait", "up_set_timing",
     "up_set_profile_capture", "up_unit_replay_profile",
+    "up_tir_open", "up_tir_close", "up_tir_set_stream", "up_tir_query", "up_tir_timings",
 ]
+TIR_HOST = 0xFFFFFFFF  # UP_TIR_HOST
 
 
 def load_library(path=LIB_PATH):
@@ -87,6 +89,7 @@ def load_library(path=LIB_PATH):
     vp, u32p = c.c_void_p, c.POINTER(c.c_uint32)
     sig = {
         "up_version": (c.c_int, []),
+        "up_track_bits": (c.c_int, []),
         "up_strerror": (c.c_char_p, [c.c_int]),
         "up_device_count": (c.c_int, [c.POINTER(c.c_int)]),
         "up_kernel_weights": (c.c_int, [c.c_uint16, c.c_double, vp]),
@@ -123,6 +126,11 @@ def load_library(path=LIB_PATH):
         "up_set_profile_capture": (c.c_int, [vp, c.c_int]),
         "up_unit_replay_profile": (c.c_int, [vp, c.c_uint32, u32p, c.POINTER(c.c_uint64), vp, vp, vp,
                                              c.c_uint64]),
+        "up_tir_open": (c.c_int, [c.c_int, c.POINTER(vp)]),
+        "up_tir_close": (None, [vp]),
+        "up_tir_set_stream": (c.c_int, [vp, c.c_uint32, c.c_uint64, vp, vp, vp]),
+        "up_tir_query": (c.c_int, [vp, c.c_uint32, c.c_uint64, vp, vp, vp, vp, vp, vp, vp]),
+        "up_tir_timings": (c.c_int, [vp, vp, c.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -142,6 +150,11 @@ def kernel_weights(bw, total=1.0):
     w = np.zeros(2 * bw + 1, np.float64)
     _ck(L.up_kernel_weights(bw, total, w.ctypes.data))
     return w
+
+
+def track_bits():
+    """bits per stored count in a device track (up_track_bits)"""
+    return load_library().up_track_bits()
 
 
 def device_count():
@@ -332,3 +345,50 @@ class Lib:
             _ck(self.L.up_unit_replay_profile(self.ctx, unit, ctypes.byref(rs), ctypes.byref(n),
                                               ev.ctypes.data, pos.ctypes.data, sc.ctypes.data, n.value))
         return rs.value, ev, pos, sc
+
+
+class Tir:
+    """One up_tir handle: tags_in_regions' streams and queries on one GPU."""
+
+    def __init__(self, device=0):
+        self.L = load_library()
+        self.h = ctypes.c_void_p()
+        _ck(self.L.up_tir_open(device, ctypes.byref(self.h)))
+        self.n = 0
+
+    def close(self):
+        if self.h:
+            self.L.up_tir_close(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_stream(self, idx, contig, first, count, forward):
+        key = (np.asarray(contig, np.uint64) << np.uint64(32)) | np.asarray(first, np.uint64)
+        cnt = np.ascontiguousarray(count, np.uint32)
+        fwd = np.ascontiguousarray(forward, np.uint8)
+        _ck(self.L.up_tir_set_stream(self.h, idx, len(key), key.ctypes.data, cnt.ctypes.data,
+                                     fwd.ctypes.data))
+        self.n = max(self.n, idx + 1)
+
+    def query(self, contig, left, right, forward, n_streams=None):
+        """(first, end, hits), each [R][n_streams] uint32"""
+        S = n_streams or self.n
+        rc = np.ascontiguousarray(contig, np.uint32)
+        rl = np.ascontiguousarray(left, np.uint32)
+        rr = np.ascontiguousarray(right, np.uint32)
+        rf = np.ascontiguousarray(forward, np.uint8)
+        R = len(rc)
+        out = [np.zeros((R, S), np.uint32) for _ in range(3)]
+        _ck(self.L.up_tir_query(self.h, S, R, rc.ctypes.data, rl.ctypes.data, rr.ctypes.data,
+                                rf.ctypes.data, *(o.ctypes.data for o in out)))
+        return tuple(out)
+
+    def timings(self):
+        t = np.zeros(2, np.float64)
+        _ck(self.L.up_tir_timings(self.h, t.ctypes.data, 2))
+        return t

@@ -326,6 +326,7 @@ static void sync_all(up_ctx *c) {
 // include/unipeak_hip.h
 
 int up_version(void) { return 10000; }
+int up_track_bits(void) { return kTB; }
 
 const char *up_strerror(int code) {
     switch (code) {
