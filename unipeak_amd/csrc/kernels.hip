@@ -100,8 +100,15 @@ __device__ __forceinline__ uint32_t fsum32(uint32_t x, uint32_t acc) {
     if constexpr (kTB == 4) {
         return __builtin_amdgcn_udot8(x, 0x11111111u, acc, false);  // v_dot8_u32_u4 x all-ones
     } else {
-        return acc + (uint32_t)__builtin_popcount(x & 0x55555555u) +
-               2u * (uint32_t)__builtin_popcount(x & 0xAAAAAAAAu);
+        // a field's value = its low bit + 2 x its high bit = (both bits) +
+        // (the high bit again): two accumulating v_bcnt and one v_and
+        // (the low/high split took six VALU per dword)
+        // (written as asm: the compiler turns the sum into two plain v_bcnt
+        // and a v_add3, four VALU)
+        uint32_t r;
+        asm volatile("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+        asm volatile("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x & 0xAAAAAAAAu), "v"(r));
+        return r;
     }
 }
 
@@ -800,10 +807,11 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                         const uint32_t d[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
                         for (int i = 0; i < CPL; ++i) {
-                            uint32_t a = 0;
+                            // unweighted: the sum accumulates straight into cs
+                            uint32_t a = POOL == 2 ? 0u : cs[CPL * q + i];
 #pragma unroll
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
-                            cs[CPL * q + i] += POOL == 2 ? a * w : a;
+                            cs[CPL * q + i] = POOL == 2 ? cs[CPL * q + i] + a * w : a;
                         }
                         anybig |= fbig32(d[0]) | fbig32(d[1]) | fbig32(d[2]) | fbig32(d[3]);
                     }
@@ -811,10 +819,10 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                         const uint32_t d[4] = {hv.x, hv.y, hv.z, hv.w};
 #pragma unroll
                         for (int i = 0; i < CPL; ++i) {
-                            uint32_t a = 0;
+                            uint32_t a = POOL == 2 ? 0u : hs[i];
 #pragma unroll
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
-                            hs[i] += POOL == 2 ? a * w : a;
+                            hs[i] = POOL == 2 ? hs[i] + a * w : a;
                         }
                         anybig |= fbig32(d[0]) | fbig32(d[1]) | fbig32(d[2]) | fbig32(d[3]);
                     }
