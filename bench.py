@@ -442,7 +442,7 @@ def main():
         value = genome / dt / 1e9
         if sim_world > 1:  # not a headline line: one rank's shard of an N-GPU plan
             print(json.dumps({"sim_world": sim_world, "sim_rank": sim_rank, "ms_per_step": round(dt * 1e3, 4),
-                              "shard_bp": int(2 * alg_bytes // max(s_nc, 1)), "k1a_ms": round(k1a_ms, 4),
+                              "shard_bp": int(alg_bytes * 8 // TB // max(s_nc, 1)), "k1a_ms": round(k1a_ms, 4),
                               "k1_ms": round(k1_ms, 4), "warmup_timings_ms": [round(x, 4) for x in warm], "phases_ms": {k: round(v / args.steps * 1e3, 4)
                                                                       for k, v in phase.items()}}), flush=True)
             g.set_record_target(0, 0)
