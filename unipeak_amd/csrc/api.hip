@@ -82,6 +82,8 @@ struct Unit {
     std::vector<std::map<uint32_t, uint32_t>> ovf;
     uint64_t *d_ovf = nullptr;     // uploaded entries, sorted by (track, pos)
     uint32_t *d_ovf_off = nullptr; // [ntracks + 1]
+    uint32_t *d_ovf_tidx = nullptr;  // [ntracks][nblk] escape tile per block (kNoTile: none)
+    uint8_t *d_ovf_tiles = nullptr;  // [ntiles][kOvfBlk]
     bool ovf_dirty = false;
     uint32_t ovf_max = 0;          // largest escaped count of any track
 };
@@ -148,6 +150,7 @@ struct up_ctx {
     // rounds: K1a alone 0.35 vs 0.44 ms at 2, bench 4,395 vs 4,265 Gbp/s)
     int k1a_per_cu = 3;
     int k1b_per_cu = 0;              // K1b workgroups per CU (UNIPEAK_K1B_PER_CU; 0 = resident)
+    int k3_per_cu = 0;               // K3 workgroups per CU (UNIPEAK_K3_PER_CU; 0 = resident)
     bool use_graphs = true;          // passes as hipGraphs (UNIPEAK_GRAPHS=0: plain launches)
     // streams of the passes (with the context stream: four, HIP's default
     // hardware queues per process, so no two share a queue): every K1a on one
@@ -378,6 +381,7 @@ int up_open(int hip_device, up_ctx **out) {
     if (const char *e = getenv("UNIPEAK_K1A_PER_CU")) c->k1a_per_cu = atoi(e);
     if (const char *e = getenv("UNIPEAK_GRAPHS")) c->use_graphs = e[0] != '0';
     if (const char *e = getenv("UNIPEAK_K1B_PER_CU")) c->k1b_per_cu = atoi(e);
+    if (const char *e = getenv("UNIPEAK_K3_PER_CU")) c->k3_per_cu = atoi(e);
     if (const char *e = getenv("UNIPEAK_LAUNCHER")) c->use_launcher = e[0] != '0';
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     {
@@ -405,6 +409,8 @@ static void free_units(up_ctx *c) {
         if (u.dptr) (void)hipFree(u.dptr);
         if (u.d_ovf) (void)hipFree(u.d_ovf);
         if (u.d_ovf_off) (void)hipFree(u.d_ovf_off);
+        if (u.d_ovf_tidx) (void)hipFree(u.d_ovf_tidx);
+        if (u.d_ovf_tiles) (void)hipFree(u.d_ovf_tiles);
     }
     c->units.clear();
     c->units_dirty = true;
@@ -905,13 +911,21 @@ static int sync_units(up_ctx *c) {
         if (u.ovf_dirty) {
             if (u.d_ovf) (void)hipFree(u.d_ovf);
             if (u.d_ovf_off) (void)hipFree(u.d_ovf_off);
+            if (u.d_ovf_tidx) (void)hipFree(u.d_ovf_tidx);
+            if (u.d_ovf_tiles) (void)hipFree(u.d_ovf_tiles);
             u.d_ovf = nullptr;
             u.d_ovf_off = nullptr;
+            u.d_ovf_tidx = nullptr;
+            u.d_ovf_tiles = nullptr;
             // entries sorted by (track, position), indexed per kOvfBlk positions
             std::vector<uint64_t> e;
             u.ovf_max = 0;
             const uint32_t nb = ovf_nblk(u.len);
             std::vector<uint32_t> off(u.ovf.size() * (size_t)(nb + 1), 0);
+            // escape tiles: every block holding an escape gets kOvfBlk bytes
+            // of min(count, 255) (ovf_lookup)
+            std::vector<uint32_t> tidx(u.ovf.size() * (size_t)nb, kNoTile);
+            std::vector<uint8_t> tiles;
             for (size_t t = 0; t < u.ovf.size(); ++t) {
                 uint32_t *o = off.data() + t * (size_t)(nb + 1);
                 uint32_t b = 0;
@@ -920,19 +934,31 @@ static int sync_units(up_ctx *c) {
                     while (b <= kb) o[b++] = (uint32_t)e.size();
                     e.push_back(((uint64_t)kv.first << 32) | kv.second);
                     u.ovf_max = std::max(u.ovf_max, kv.second);
+                    uint32_t &ti = tidx[t * (size_t)nb + kb];
+                    if (ti == kNoTile) {
+                        ti = (uint32_t)(tiles.size() / kOvfBlk);
+                        tiles.resize(tiles.size() + kOvfBlk, 0);
+                    }
+                    tiles[(size_t)ti * kOvfBlk + ((kv.first - 1) & (kOvfBlk - 1))] =
+                        (uint8_t)std::min<uint32_t>(kv.second, 255u);
                 }
                 while (b <= nb) o[b++] = (uint32_t)e.size();
             }
             if (!e.empty()) {
                 HIPCHK(hipMalloc(&u.d_ovf, e.size() * sizeof(uint64_t)));
                 HIPCHK(hipMalloc(&u.d_ovf_off, off.size() * sizeof(uint32_t)));
+                HIPCHK(hipMalloc(&u.d_ovf_tidx, tidx.size() * sizeof(uint32_t)));
+                HIPCHK(hipMalloc(&u.d_ovf_tiles, tiles.size()));
                 HIPCHK(hipMemcpy(u.d_ovf, e.data(), e.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
                 HIPCHK(hipMemcpy(u.d_ovf_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(u.d_ovf_tidx, tidx.data(), tidx.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(u.d_ovf_tiles, tiles.data(), tiles.size(), hipMemcpyHostToDevice));
             }
             u.ovf_dirty = false;
         }
         d[i] = UnitDesc{(uint64_t)(uintptr_t)u.dptr, u.stride, u.len, u.strip0, u.nstrips, u.nstrands,
-                        (uint64_t)(uintptr_t)u.d_ovf, (uint64_t)(uintptr_t)u.d_ovf_off};
+                        (uint64_t)(uintptr_t)u.d_ovf, (uint64_t)(uintptr_t)u.d_ovf_off,
+                        (uint64_t)(uintptr_t)u.d_ovf_tidx, (uint64_t)(uintptr_t)u.d_ovf_tiles};
     }
     c->nstrips = strip;
     c->ovf_max_all = 0;
@@ -1068,7 +1094,9 @@ static StatParams stat_params(up_ctx *c, up_ctx::Pass &ps) {
 static void dispatch_stats(up_ctx *c, hipStream_t st, const StatParams &P, uint64_t nreg) {
     const size_t lds = kStatLds;
     const void *k = stats_kernel_for(P.bw, pool_mode(c), c->p.nondir != 0);
-    const uint64_t blocks = std::min<uint64_t>((nreg + 3) / 4, resident_blocks(c, k, lds));
+    uint64_t cap = resident_blocks(c, k, lds);
+    if (c->k3_per_cu > 0) cap = std::min<uint64_t>(cap, (uint64_t)c->k3_per_cu * (uint64_t)(c->ncu > 0 ? c->ncu : 256));
+    const uint64_t blocks = std::min<uint64_t>((nreg + 3) / 4, cap);
     if (blocks == 0) return;
     StatParams Q = P;
     void *args[] = {&Q};

@@ -72,7 +72,11 @@ struct UnitDesc {
     uint64_t ovf_off;   // uint32[ntracks][nblk + 1], nblk = ceil(len / kOvfBlk): index of
                         // the track's first entry at or after block b's first position
                         // (b = nblk: the track's end), or 0
+    uint64_t ovf_tidx;  // uint32[ntracks][nblk]: escape tile of block b (kNoTile: none)
+    uint64_t ovf_tiles; // uint8[ntiles][kOvfBlk]: min(count, 255) of every escaped position
+                        // of the tile's block (255: the entries hold it)
 };
+constexpr uint32_t kNoTile = 0xFFFFFFFFu;
 
 // packed per-strip summary written by the scan kernel (uint64):
 //   bits  0-15 interior run starts, 16-31 interior run ends,

@@ -119,11 +119,21 @@ __device__ __forceinline__ uint32_t fbig32(uint32_t x) {
     else return x & (x >> 1) & 0x55555555u;
 }
 
-// escaped count (>= 15): binary search of the entries of the position's
-// block (UnitDesc::ovf_off indexes them per kOvfBlk positions)
+// escaped count (>= kEsc): two dependent loads -- the block's escape tile
+// index, then the tile's byte -- and, for a count >= 255 only, a binary
+// search of the entries of the position's block (UnitDesc::ovf_off indexes
+// them per kOvfBlk positions).  With 2-bit tracks every peak position holding
+// three or more tags is an escape; the search alone (about six dependent
+// loads) was a fifth of K1b with 8 pooled samples.
 // (inline: a call needs a stack frame, i.e. scratch, in every kernel using it)
 __device__ __forceinline__ uint32_t ovf_lookup(const UnitDesc &U, uint32_t track, uint32_t pos) {
     if (!U.ovf || pos - 1u >= U.len) return kEsc;
+    const uint32_t nblk = ovf_nblk(U.len);
+    const uint32_t ti = ((const uint32_t *)U.ovf_tidx)[(size_t)track * nblk + ((pos - 1u) >> kOvfBlkShift)];
+    if (ti != kNoTile) {
+        const uint32_t v = ((const uint8_t *)U.ovf_tiles)[(size_t)ti * kOvfBlk + ((pos - 1u) & (kOvfBlk - 1u))];
+        if (v != 255u) return v;
+    }
     const uint32_t *off = (const uint32_t *)U.ovf_off + (size_t)track * (ovf_nblk(U.len) + 1) +
                           ((pos - 1u) >> kOvfBlkShift);
     const uint64_t *e = (const uint64_t *)U.ovf;
@@ -259,17 +269,24 @@ __device__ __forceinline__ void next_hits(uint64_t &m, T v, int (&b)[kHB], doubl
 // Same as load_words, but the N*kWordBytes bytes of each track are fetched
 // with 16-byte lane loads (one 1 KiB wave load per 1024/kWordBytes words) and
 // turned into the lane = position layout through this wave's LDS stage
-// (N*kWordBytes <= 1024 bytes).  x0 - 1 must be a multiple of 64 (the bytes
-// are then 16-byte aligned).
+// (kStageBytes per strand).  x0 - 1 must be a multiple of 64 (the bytes are
+// then 16-byte aligned).  Several pooled samples are fetched in batches: the
+// lanes of one set of wave loads cover up to kStageBytes / (N*kWordBytes)
+// tracks at once (lane l -> track l / NL, piece l % NL), so a batch costs one
+// memory round trip instead of one per sample (hg19, 8 samples + 1 control:
+// K1b load phase was 48 % of its clocks with one trip per sample).
+constexpr int kStageBytes = 4096;
 template <int N, int POOL>
 __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const UnitDesc &U, int S, int strand,
                                                   int64_t x0, int lane, int nnc, const int32_t *nc,
                                                   const double *coef, uint8_t *stage) {
     constexpr int NL = N * kWordBytes / 16;    // 16-byte lane loads per track
-    constexpr int NV = (NL + 63) / 64;           // wave loads per track
-    uint32_t c[N];
-    auto fetch = [&](int k) {
-        gu32x4 *t = (gu32x4 *)(track_u8(U, S, strand, nc[k]) + fbyte(kPadPos + x0 - 1));
+    static_assert(NL * 16 <= kStageBytes, "one track's window fits the stage");
+    const uint32_t sh = fshift(lane);
+    const int64_t b0 = fbyte(kPadPos + x0 - 1);
+    if constexpr (POOL == 0) {
+        constexpr int NV = (NL + 63) / 64;           // wave loads per track
+        gu32x4 *t = (gu32x4 *)(track_u8(U, S, strand, nc[0]) + b0);
         u32x4 v[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q)
@@ -281,34 +298,55 @@ __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const Uni
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t sh = fshift(lane);
+        uint32_t c[N];
 #pragma unroll
         for (int w = 0; w < N; ++w) c[w] = ((uint32_t)stage[kWordBytes * w + fbyte(lane)] >> sh) & kTMask;
-        resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[k]), x0, lane);
-    };
-    if constexpr (POOL == 0) {
-        fetch(0);
+        resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[0]), x0, lane);
 #pragma unroll
         for (int w = 0; w < N; ++w) cs[w] = c[w];
     } else {
+        // tracks per batch: two wave loads' worth (more held the K1b
+        // register budget: 14 tracks in flight spilled)
+        constexpr int NQ = 2;
+        constexpr int KB = (NQ * 64 / NL) < (kStageBytes / (NL * 16)) ? NQ * 64 / NL : kStageBytes / (NL * 16);
 #pragma unroll
         for (int w = 0; w < N; ++w) cs[w] = 0.0;
-        for (int k = 0; k < nnc; ++k) {
-            fetch(k);
-            if constexpr (POOL == 1) {
+        // POOL 2: the coefficient-weighted loop, then the unweighted one (Q5)
+        for (int pass = 0; pass < (POOL == 2 ? 2 : 1); ++pass) {
+            for (int k0 = 0; k0 < nnc; k0 += KB) {
+                const int kb = nnc - k0 < KB ? nnc - k0 : KB;
+                u32x4 v[NQ];
 #pragma unroll
-                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w];
-            } else {
-                const double q = coef[k];
+                for (int q = 0; q < NQ; ++q) {
+                    const int l = 64 * q + lane;
+                    if (l < kb * NL) {
+                        const int k = k0 + l / NL;
+                        v[q] = ((gu32x4 *)(track_u8(U, S, strand, nc[k]) + b0))[l % NL];
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();  // earlier readers of the stage are done
 #pragma unroll
-                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w] * q;
-            }
-        }
-        if constexpr (POOL == 2) {
-            for (int k = 0; k < nnc; ++k) {
-                fetch(k);
+                for (int q = 0; q < NQ; ++q)
+                    if (64 * q + lane < kb * NL) *(u32x4 *)(stage + 16 * (64 * q + lane)) = v[q];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int k = 0; k < kb; ++k) {  // sample order: the reference's summation order
+                    uint32_t c[N];
 #pragma unroll
-                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w];
+                    for (int w = 0; w < N; ++w)
+                        c[w] = ((uint32_t)stage[NL * 16 * k + kWordBytes * w + fbyte(lane)] >> sh) & kTMask;
+                    resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[k0 + k]), x0, lane);
+                    if (POOL == 2 && pass == 0) {
+                        const double q = coef[k0 + k];
+#pragma unroll
+                        for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w] * q;
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w];
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();  // stage free for the next batch
             }
         }
     }
@@ -565,6 +603,7 @@ constexpr size_t kScanLds = kKTab * sizeof(double) + kScreenLds + 4 * kStepWords
 #endif
 constexpr int kXFront = UPK_XFRONT;  // K1b work items with >= this many exact blocks go first
 constexpr size_t kExactLds = kKTab * sizeof(double) + 4 * kStepWords * kWave * sizeof(double);
+static_assert(2 * kStageBytes <= kStepWords * kWave * sizeof(double), "both strands' stages fit a wave's score area");
 
 // chunks 16l .. 16l+15 of lane l that can hold a position with score >= thr.
 // rd = this lane's row of the padded chunk-sum area (index 16l + j, j =
@@ -1026,7 +1065,8 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             uint64_t hf[NWIN], hr[NONDIR ? NWIN : 1];
             load_words_staged<NWIN, POOL>(wf, U, S, 0, x0, lane, P.nnc, P.nc, P.coef, (uint8_t *)scs);
             if constexpr (NONDIR)
-                load_words_staged<NWIN, POOL>(wr, U, S, 1, x0, lane, P.nnc, P.nc, P.coef, (uint8_t *)scs + 2048);
+                load_words_staged<NWIN, POOL>(wr, U, S, 1, x0, lane, P.nnc, P.nc, P.coef,
+                                              (uint8_t *)scs + kStageBytes);
 #pragma unroll
             for (int w = 0; w < NWIN; ++w) {
                 hf[w] = __ballot(nz(wf[w]));
