@@ -128,12 +128,14 @@ __device__ __forceinline__ uint32_t fbig32(uint32_t x) {
 // (inline: a call needs a stack frame, i.e. scratch, in every kernel using it)
 __device__ __forceinline__ uint32_t ovf_lookup(const UnitDesc &U, uint32_t track, uint32_t pos) {
     if (!U.ovf || pos - 1u >= U.len) return kEsc;
+#ifndef UPK_NO_TILES  // A/B: the binary search alone
     const uint32_t nblk = ovf_nblk(U.len);
     const uint32_t ti = ((const uint32_t *)U.ovf_tidx)[(size_t)track * nblk + ((pos - 1u) >> kOvfBlkShift)];
     if (ti != kNoTile) {
         const uint32_t v = ((const uint8_t *)U.ovf_tiles)[(size_t)ti * kOvfBlk + ((pos - 1u) & (kOvfBlk - 1u))];
         if (v != 255u) return v;
     }
+#endif
     const uint32_t *off = (const uint32_t *)U.ovf_off + (size_t)track * (ovf_nblk(U.len) + 1) +
                           ((pos - 1u) >> kOvfBlkShift);
     const uint64_t *e = (const uint64_t *)U.ovf;
