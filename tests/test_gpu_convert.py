@@ -304,3 +304,40 @@ def test_convert_align_fails_loudly_without_gpu(tmp_path):
     r = subprocess.run([BIN, "-q", "-c", "ct.txt", "-o", "o.wig", "k.bed"], cwd=tmp_path,
                        capture_output=True, text=True)
     assert r.returncode == 1 and "no HIP device" in r.stderr
+
+
+@pytest.mark.gpu
+def test_count_map_device_order(gpu_lib):
+    """up_cm_* through the C-ABI against dictionaries: per-position sums with
+    uint32 wrap, both iterators' orders, contig edges, an invalid add"""
+    rng = np.random.default_rng(7)
+    lens = [1, 70_000, 8_191, 8_193, 100]
+    n = 200_000
+    c = rng.integers(0, len(lens), n).astype(np.uint32)
+    p = np.array([int(rng.integers(1, lens[k] + 1)) for k in c], np.uint32)
+    f = (rng.random(n) < 0.5).astype(np.uint8)
+    k = rng.integers(1, 5, n).astype(np.uint32)
+    k[:3] = 0xFFFFFFFF
+    with gpu_lib.CountMap(lens) as cm:
+        cm.add(c, p, f, k)
+        cm.add(c[:1000], p[:1000], f[:1000])  # count NULL: 1 each
+        with pytest.raises(gpu_lib.UpError):
+            cm.add([1], [lens[1] + 1], [1])
+        d_dir = cm.collect(False)
+        d_nd = cm.collect(True)
+    want = {}
+    for i in range(n):
+        key = (int(f[i] == 0), int(c[i]), int(p[i]))
+        want[key] = (want.get(key, 0) + int(k[i])) & 0xFFFFFFFF
+    for i in range(1000):
+        key = (int(f[i] == 0), int(c[i]), int(p[i]))
+        want[key] = (want.get(key, 0) + 1) & 0xFFFFFFFF
+    exp = sorted((s, cc, pp, v) for (s, cc, pp), v in want.items() if v)
+    got = [(int(1 - ff), int(cc), int(pp), int(v)) for cc, pp, v, ff in zip(*d_dir)]
+    assert got == exp
+    nd = {}
+    for (s, cc, pp), v in want.items():
+        nd[(cc, pp)] = (nd.get((cc, pp), 0) + v) & 0xFFFFFFFF
+    exp_nd = sorted((cc, pp, v) for (cc, pp), v in nd.items() if v)
+    assert [(int(cc), int(pp), int(v)) for cc, pp, v, _ in zip(*d_nd)] == exp_nd
+    assert d_nd[3].all()

@@ -73,6 +73,7 @@ EXPORTS = [
     "up_host_register", "up_unit_profile_range", "up_run_async", "up_run_wait", "up_set_timing",
     "up_set_profile_capture", "up_unit_replay_profile",
     "up_tir_open", "up_tir_close", "up_tir_set_stream", "up_tir_query", "up_tir_timings",
+    "up_cm_open", "up_cm_close", "up_cm_add", "up_cm_collect", "up_cm_timings",
 ]
 TIR_HOST = 0xFFFFFFFF  # UP_TIR_HOST
 
@@ -131,6 +132,11 @@ def load_library(path=LIB_PATH):
         "up_tir_set_stream": (c.c_int, [vp, c.c_uint32, c.c_uint64, vp, vp, vp]),
         "up_tir_query": (c.c_int, [vp, c.c_uint32, c.c_uint64, vp, vp, vp, vp, vp, vp, vp]),
         "up_tir_timings": (c.c_int, [vp, vp, c.c_int]),
+        "up_cm_open": (c.c_int, [c.c_int, c.c_uint32, vp, c.POINTER(vp)]),
+        "up_cm_close": (None, [vp]),
+        "up_cm_add": (c.c_int, [vp, c.c_uint64, vp, vp, vp, vp]),
+        "up_cm_collect": (c.c_int, [vp, c.c_int, c.POINTER(c.c_uint64), vp, vp, vp, vp, c.c_uint64]),
+        "up_cm_timings": (c.c_int, [vp, vp, c.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -392,3 +398,42 @@ class Tir:
         t = np.zeros(2, np.float64)
         _ck(self.L.up_tir_timings(self.h, t.ctypes.data, 2))
         return t
+
+
+class CountMap:
+    """One up_cm handle: convert_align's CountMap as dense HBM tracks."""
+
+    def __init__(self, contig_lens, device=0):
+        self.L = load_library()
+        self.h = ctypes.c_void_p()
+        lens = np.ascontiguousarray(contig_lens, np.uint32)
+        _ck(self.L.up_cm_open(device, len(lens), lens.ctypes.data, ctypes.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            self.L.up_cm_close(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def add(self, contig, pos, forward, count=None):
+        c = np.ascontiguousarray(contig, np.uint32)
+        p = np.ascontiguousarray(pos, np.uint32)
+        f = np.ascontiguousarray(forward, np.uint8)
+        k = None if count is None else np.ascontiguousarray(count, np.uint32)
+        _ck(self.L.up_cm_add(self.h, len(p), c.ctypes.data, p.ctypes.data, f.ctypes.data,
+                             None if k is None else k.ctypes.data))
+
+    def collect(self, nondir=False):
+        """(contig, pos, count, forward) in the iterators' order"""
+        n = ctypes.c_uint64()
+        _ck(self.L.up_cm_collect(self.h, int(nondir), ctypes.byref(n), None, None, None, None, 0))
+        out = [np.zeros(n.value, np.uint32) for _ in range(3)] + [np.zeros(n.value, np.uint8)]
+        if n.value:
+            _ck(self.L.up_cm_collect(self.h, int(nondir), ctypes.byref(n), *(o.ctypes.data for o in out),
+                                     n.value))
+        return tuple(out)

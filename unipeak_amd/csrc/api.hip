@@ -158,7 +158,8 @@ struct up_ctx {
     // up the dispatcher serves it first), the rest of a pass on one of two
     // chain streams, alternating, so two passes' K1x..K3 may overlap
     hipStream_t k1a_stream = nullptr;
-    hipStream_t chain[2] = {};
+    hipStream_t chain[4] = {};
+    int n_chain = 2;                 // chain streams in use (UNIPEAK_CHAINS, 1..4)
     uint64_t nlaunch = 0;
     hipStream_t stream = nullptr;
     bool have_params = false;
@@ -312,7 +313,8 @@ static bool busy(const up_ctx *c) { return c && c->seq_launched != c->seq_done; 
 static void sync_all(up_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->k1a_stream);
-    for (auto st : c->chain) (void)hipStreamSynchronize(st);
+    for (auto st : c->chain)
+        if (st) (void)hipStreamSynchronize(st);
 }
 
 #define HIPCHK(x)                                                                   \
@@ -382,6 +384,7 @@ int up_open(int hip_device, up_ctx **out) {
     if (const char *e = getenv("UNIPEAK_GRAPHS")) c->use_graphs = e[0] != '0';
     if (const char *e = getenv("UNIPEAK_K1B_PER_CU")) c->k1b_per_cu = atoi(e);
     if (const char *e = getenv("UNIPEAK_K3_PER_CU")) c->k3_per_cu = atoi(e);
+    if (const char *e = getenv("UNIPEAK_CHAINS")) c->n_chain = std::min(4, std::max(1, atoi(e)));
     if (const char *e = getenv("UNIPEAK_LAUNCHER")) c->use_launcher = e[0] != '0';
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     {
@@ -390,7 +393,7 @@ int up_open(int hip_device, up_ctx **out) {
         const char *e = getenv("UNIPEAK_K1A_PRIO");  // A/B: 0 = normal priority
         HIPCHK(hipStreamCreateWithPriority(&c->k1a_stream, hipStreamNonBlocking,
                                            (e && e[0] == '0') ? least : greatest));
-        for (auto &st : c->chain) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        for (int i = 0; i < c->n_chain; ++i) HIPCHK(hipStreamCreateWithFlags(&c->chain[i], hipStreamNonBlocking));
     }
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     for (auto &ps : c->pass) {
@@ -450,7 +453,8 @@ void up_close(up_ctx *c) {
         c->pass[k].release();
     }
     (void)hipStreamDestroy(c->k1a_stream);
-    for (auto st : c->chain) (void)hipStreamDestroy(st);
+    for (auto st : c->chain)
+        if (st) (void)hipStreamDestroy(st);
     (void)hipEventDestroy(c->host_work);
     for (auto &e : c->scat_ev) (void)hipEventSynchronize(e);
     c->hp_scat[0].release(); c->hp_scat[1].release();
@@ -1517,7 +1521,7 @@ static int launch_pass(up_ctx *c, int slot) {
     // (stream order serialises the K1a's; a slot is reused only after the
     // host saw its previous pass done)
     hipStream_t s1 = c->k1a_stream;
-    ps.stream = c->chain[c->nlaunch++ & 1];
+    ps.stream = c->chain[c->nlaunch++ % (uint64_t)c->n_chain];
     // (nothing to follow once the context stream has drained: two API
     // calls per pass fewer, ~5 us of host time, which bounds 8-GPU steps)
     if (hipStreamQuery(c->stream) != hipSuccess) {
