@@ -582,9 +582,20 @@ def shift_pipeline(args, W):
         # strand_shift.cpp:205-228: per region the first shift of the largest
         # correlation above -1 (K4 + a device reduction), then the first
         # n_test qualifying regions
-        best, bcorr = ga.shift_best(elig, max_shift)
+        # (in chunks, as bin/strand_shift: the reference's loop stops at the
+        # n_test-th qualifying region, so only the regions it reaches are
+        # correlated)
+        best_l, done, tested = [], 0, 0
+        while tested < n_test and done < len(elig):
+            m = min(n_test + n_test // 4 + 16 if done == 0 else 2 * (n_test - tested) + 16, len(elig) - done)
+            b_, c_ = ga.shift_best(elig[done:done + m], max_shift)
+            q = np.flatnonzero(c_ >= u_thr)[:n_test - tested]
+            best_l.append(b_[q])
+            tested += len(q)
+            done += m
         t3 = time.perf_counter()
-        ok = np.flatnonzero(bcorr >= u_thr)[:n_test]
+        best = np.concatenate(best_l) if best_l else np.zeros(0, np.int64)
+        ok = np.arange(len(best))
         freq = np.bincount(best[ok], minlength=max_shift + 1).astype(np.float64)
         # strand_shift.cpp:241-248: dens[i - 5 + j] += freq[i] * k5[j]; every
         # dens[k] receives its terms in ascending i, as in the reference loop
@@ -606,7 +617,8 @@ def shift_pipeline(args, W):
         if timed:
             for k, v in zip(ph, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, tr - t0, t4c - t4b)):
                 ph[k] += v
-        info.update(shift_candidates=int(n), eligible=int(len(elig)), tested=int(len(ok)), best_shift=bs,
+        info.update(shift_candidates=int(n), eligible=int(len(elig)), correlated=int(done), tested=int(len(ok)),
+                    best_shift=bs,
                     regions_candidates=int(nb), regions_accepted=acc)
 
     for g, _ in ctx:

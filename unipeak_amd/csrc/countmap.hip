@@ -127,22 +127,22 @@ __global__ void __launch_bounds__(kThreads) cm_emit(const uint32_t *__restrict__
         __syncthreads();
         if (nz) {
             uint64_t o = out + before + wex;
-            // contig of the first nonzero: binary search of the offsets
-            const bool rev = !nondir && v >= genome;
-            const uint64_t g = rev ? v - genome : v;
-            uint32_t lo = 0, hi = n_contigs;  // last contig with off <= g
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (off[mid] <= g) lo = mid;
-                else hi = mid;
-            }
             for (int j = 0; j < 4; ++j) {
                 if (!val[j]) continue;
-                const uint64_t gj = g + j;
-                uint32_t c = lo;
-                while (c + 1 < n_contigs && off[c + 1] <= gj) ++c;
-                o_contig[o] = c;
-                o_pos[o] = (uint32_t)(gj - off[c] + 1);
+                // strand and contig of view position v + j (a group of four
+                // may straddle the forward/reverse boundary: the genome
+                // length need not be a multiple of 4)
+                const uint64_t vj = v + j;
+                const bool rev = !nondir && vj >= genome;
+                const uint64_t g = rev ? vj - genome : vj;
+                uint32_t lo = 0, hi = n_contigs;  // last contig with off <= g
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (off[mid] <= g) lo = mid;
+                    else hi = mid;
+                }
+                o_contig[o] = lo;
+                o_pos[o] = (uint32_t)(g - off[lo] + 1);
                 o_cnt[o] = val[j];
                 o_fwd[o] = rev ? 0 : 1;
                 ++o;

@@ -107,21 +107,30 @@ int main(int argc, char **argv) {
     for (const Candidate *c : regs)
         if ((uint64_t)(c->r.right - c->r.left + 1) > (unsigned)(2 * max_shift + 3)) elig.push_back(c);
     // per region the first shift with the largest correlation (:209-217),
-    // reduced on the GPU
-    std::vector<uint16_t> bshift;
-    std::vector<double> bcorr;
-    shift_best(ep, pr, elig, max_shift, bshift, bcorr);
-
+    // reduced on the GPU -- for the regions the reference's loop reaches:
+    // it stops at the n_test-th qualifying one, so the sorted regions go to
+    // the device in chunks (the first n_test + n_test/4, then twice what is
+    // still missing) until enough qualify or none are left
     uint16_t tested = 0;
     uint64_t tags_in = 0;
     std::vector<uint64_t> freq((size_t)max_shift + 1, 0);
     const size_t W = (size_t)max_shift + 1;
-    for (size_t k = 0; tested < n_test && k < elig.size(); ++k) {
-        if (bcorr[k] >= corr_thr) {
-            ++freq[bshift[k]];
-            tags_in += elig[k]->r.sum;
-            ++tested;
+    size_t done = 0;
+    while (tested < n_test && done < elig.size()) {
+        const size_t want = done == 0 ? (size_t)n_test + n_test / 4 + 16 : 2 * (size_t)(n_test - tested) + 16;
+        const size_t m = std::min(want, elig.size() - done);
+        std::vector<const Candidate *> chunk(elig.begin() + done, elig.begin() + done + m);
+        std::vector<uint16_t> bshift;
+        std::vector<double> bcorr;
+        shift_best(ep, pr, chunk, max_shift, bshift, bcorr);
+        for (size_t k = 0; tested < n_test && k < m; ++k) {
+            if (bcorr[k] >= corr_thr) {
+                ++freq[bshift[k]];
+                tags_in += chunk[k]->r.sum;
+                ++tested;
+            }
         }
+        done += m;
     }
     if (tested == 0) { std::cerr << "error: no regions qualified with given settings" << std::endl << std::endl; exit_now(1); }
     if (tested < n_test) std::cerr << "warning: too few regions qualified with given settings" << std::endl;
