@@ -152,14 +152,17 @@ struct up_ctx {
     int k1b_per_cu = 0;              // K1b workgroups per CU (UNIPEAK_K1B_PER_CU; 0 = resident)
     int k3_per_cu = 0;               // K3 workgroups per CU (UNIPEAK_K3_PER_CU; 0 = resident)
     bool use_graphs = true;          // passes as hipGraphs (UNIPEAK_GRAPHS=0: plain launches)
-    // streams of the passes (with the context stream: four, HIP's default
-    // hardware queues per process, so no two share a queue): every K1a on one
-    // high-priority stream (stream order serialises them; as resources free
-    // up the dispatcher serves it first), the rest of a pass on one of two
-    // chain streams, alternating, so two passes' K1x..K3 may overlap
+    // streams of the passes: every K1a on one high-priority stream (stream
+    // order serialises them; as resources free up the dispatcher serves it
+    // first), the rest of a pass on one of n_chain chain streams in turn, so
+    // that many passes' K1x..K3 may overlap (bench.py raises
+    // GPU_MAX_HW_QUEUES so no two of them share a hardware queue)
     hipStream_t k1a_stream = nullptr;
     hipStream_t chain[4] = {};
-    int n_chain = 2;                 // chain streams in use (UNIPEAK_CHAINS, 1..4)
+    // chain streams in use (UNIPEAK_CHAINS, 1..4): three -- hg19 configs[1],
+    // same box, two alternating rounds: 4,832 / 4,755 Gbp/s vs 4,652 / 4,487
+    // with two and 4,636 / 4,604 with four
+    int n_chain = 3;
     uint64_t nlaunch = 0;
     hipStream_t stream = nullptr;
     bool have_params = false;

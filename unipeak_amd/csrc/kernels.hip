@@ -128,14 +128,12 @@ __device__ __forceinline__ uint32_t fbig32(uint32_t x) {
 // (inline: a call needs a stack frame, i.e. scratch, in every kernel using it)
 __device__ __forceinline__ uint32_t ovf_lookup(const UnitDesc &U, uint32_t track, uint32_t pos) {
     if (!U.ovf || pos - 1u >= U.len) return kEsc;
-#ifndef UPK_NO_TILES  // A/B: the binary search alone
     const uint32_t nblk = ovf_nblk(U.len);
     const uint32_t ti = ((const uint32_t *)U.ovf_tidx)[(size_t)track * nblk + ((pos - 1u) >> kOvfBlkShift)];
     if (ti != kNoTile) {
         const uint32_t v = ((const uint8_t *)U.ovf_tiles)[(size_t)ti * kOvfBlk + ((pos - 1u) & (kOvfBlk - 1u))];
         if (v != 255u) return v;
     }
-#endif
     const uint32_t *off = (const uint32_t *)U.ovf_off + (size_t)track * (ovf_nblk(U.len) + 1) +
                           ((pos - 1u) >> kOvfBlkShift);
     const uint64_t *e = (const uint64_t *)U.ovf;
@@ -281,8 +279,7 @@ constexpr int kStageBytes = 4096;
 template <int N, int POOL>
 __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const UnitDesc &U, int S, int strand,
                                                   int64_t x0, int lane, int nnc, const int32_t *nc,
-                                                  const double *coef, uint8_t *stage,
-                                                  const u32x4 *pre = nullptr) {
+                                                  const double *coef, uint8_t *stage) {
     constexpr int NL = N * kWordBytes / 16;    // 16-byte lane loads per track
     static_assert(NL * 16 <= kStageBytes, "one track's window fits the stage");
     const uint32_t sh = fshift(lane);
@@ -293,7 +290,7 @@ __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const Uni
         u32x4 v[NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q)
-            if (64 * q + lane < NL) v[q] = (pre && q == 0) ? *pre : t[64 * q + lane];
+            if (64 * q + lane < NL) v[q] = t[64 * q + lane];
         __builtin_amdgcn_wave_barrier();  // earlier readers of the stage are done
 #pragma unroll
         for (int q = 0; q < NV; ++q)
@@ -776,18 +773,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     if constexpr (MODE == kModeScreen && !PROF && kPf) {
         if (it0 < it_end) pf_issue(it0, find_unit(units, P.nunits, it0), 0, 0);
     }
-    // K1b with one directional sample: the window bytes of the next exact
-    // block -- the next one of this strip, else the first of this wave's
-    // next work item -- are loaded while the current block is computed
-    // (UPK_NO_K1B_PF for A/B)
-#ifdef UPK_NO_K1B_PF
-    constexpr bool kBpf = false;
-#else
-    constexpr bool kBpf = MODE == kModeExact && POOL == 0 && !NONDIR && !PROF;
-#endif
-    u32x4 bpf_v = {0u, 0u, 0u, 0u};
-    int64_t bpf_x0 = INT64_MIN;  // window position the prefetched bytes belong to
-    uint32_t bpf_unit = 0xFFFFFFFFu;
     for (uint32_t it = it0; it < it_end; it += istep) {
         const uint32_t item = it;
 #ifdef UPK_DEBUG_TIMES
@@ -1078,38 +1063,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 #endif
             T wf[NWIN], wr[NONDIR ? NWIN : 1];
             uint64_t hf[NWIN], hr[NONDIR ? NWIN : 1];
-            if constexpr (kBpf) {
-                constexpr int NL = NWIN * kWordBytes / 16;
-                const bool hit = bpf_x0 == x0 && bpf_unit == cur;
-                const u32x4 here = bpf_v;
-                // the next exact block's window: later in this strip, or the
-                // first exact block of this wave's next item
-                int64_t nx0 = INT64_MIN;
-                uint32_t nunit = cur;
-                const uint32_t later = exact_blocks & ~((2u << j) - 1u);
-                if (later) {
-                    nx0 = p0 + 64 * ((int64_t)__builtin_ctz(later) * SW - NH);
-                } else if (it + istep < it_end) {
-                    const uint32_t ein = cptr(P.xref)[it + istep];
-                    const auto *esn = cptr(P.xlist + (uint64_t)ein * kXEntry);
-                    const uint32_t e1n = esn[1];
-                    nunit = e1n >> 16;
-                    if (nunit != 0xFFFFu && (e1n & 0xFFFFu)) {
-                        const uint32_t lstrip = esn[0] - units[nunit].strip0;
-                        nx0 = 1 + (int64_t)lstrip * kStrip + 64 * ((int64_t)__builtin_ctz(e1n & 0xFFFFu) * SW - NH);
-                    }
-                }
-                if (nx0 != INT64_MIN && lane < NL) {
-                    const UnitDesc &Un = units[nunit];
-                    bpf_v = ((gu32x4 *)(track_u8(Un, S, 0, ncs[0]) + fbyte(kPadPos + nx0 - 1)))[lane];
-                }
-                bpf_x0 = nx0;
-                bpf_unit = nunit;
-                load_words_staged<NWIN, POOL>(wf, U, S, 0, x0, lane, P.nnc, P.nc, P.coef, (uint8_t *)scs,
-                                              hit ? &here : nullptr);
-            } else {
-                load_words_staged<NWIN, POOL>(wf, U, S, 0, x0, lane, P.nnc, P.nc, P.coef, (uint8_t *)scs);
-            }
+            load_words_staged<NWIN, POOL>(wf, U, S, 0, x0, lane, P.nnc, P.nc, P.coef, (uint8_t *)scs);
             if constexpr (NONDIR)
                 load_words_staged<NWIN, POOL>(wr, U, S, 1, x0, lane, P.nnc, P.nc, P.coef,
                                               (uint8_t *)scs + kStageBytes);
