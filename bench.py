@@ -40,10 +40,11 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# the library's four streams (context, K1a, two chains) plus torch's and
+# the library's five streams (context, K1a, three chains) plus torch's and
 # RCCL's: more hardware queues than HIP's default 4, so no stream of a pass
-# shares an in-order queue with a collective (read at HIP initialisation)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# shares an in-order queue with another (read at HIP initialisation)
+# (the configs[2] pipeline holds two contexts: twice the streams)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "12" if "hg19-shift" in sys.argv else "8")
 
 from unipeak_amd import capi, shard  # noqa: E402
 
