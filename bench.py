@@ -576,9 +576,21 @@ def shift_pipeline(args, W):
         tr = time.perf_counter()
         regs, _ = ga.regions_view()
         t1 = time.perf_counter()
-        order = np.argsort(-regs["sum"].astype(np.int64), kind="stable")
-        span = (regs["right"].astype(np.int64) - regs["left"] + 1)[order]
-        elig = order[span > 2 * max_shift + 3]
+        # the regions long enough to be tested, in the order of a stable sort
+        # by sum descending -- only as far as the loop below reaches: the
+        # top m by (sum desc, index asc) are selected in O(n) and sorted, and
+        # the selection widens if more are needed (same order as a full
+        # stable argsort)
+        long_ = np.flatnonzero((regs["right"].astype(np.int64) - regs["left"] + 1) > 2 * max_shift + 3)
+        key = (regs["sum"][long_].astype(np.uint64) << np.uint64(32)) | \
+            (np.uint64(0xFFFFFFFF) - long_.astype(np.uint64))
+
+        def top(m):
+            if m >= len(key):
+                return long_[np.argsort(key)[::-1]]
+            part = np.argpartition(key, len(key) - m)[len(key) - m:]
+            return long_[part[np.argsort(key[part])[::-1]]]
+        elig = top(min(len(key), n_test + n_test // 4 + 16))
         t2 = time.perf_counter()
         # strand_shift.cpp:205-228: per region the first shift of the largest
         # correlation above -1 (K4 + a device reduction), then the first
@@ -587,8 +599,10 @@ def shift_pipeline(args, W):
         # n_test-th qualifying region, so only the regions it reaches are
         # correlated)
         best_l, done, tested = [], 0, 0
-        while tested < n_test and done < len(elig):
-            m = min(n_test + n_test // 4 + 16 if done == 0 else 2 * (n_test - tested) + 16, len(elig) - done)
+        while tested < n_test and done < len(key):
+            m = min(n_test + n_test // 4 + 16 if done == 0 else 2 * (n_test - tested) + 16, len(key) - done)
+            if done + m > len(elig):
+                elig = top(min(len(key), max(done + m, 2 * len(elig))))
             b_, c_ = ga.shift_best(elig[done:done + m], max_shift)
             q = np.flatnonzero(c_ >= u_thr)[:n_test - tested]
             best_l.append(b_[q])
@@ -618,7 +632,7 @@ def shift_pipeline(args, W):
         if timed:
             for k, v in zip(ph, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, tr - t0, t4c - t4b)):
                 ph[k] += v
-        info.update(shift_candidates=int(n), eligible=int(len(elig)), correlated=int(done), tested=int(len(ok)),
+        info.update(shift_candidates=int(n), eligible=int(len(key)), correlated=int(done), tested=int(len(ok)),
                     best_shift=bs,
                     regions_candidates=int(nb), regions_accepted=acc)
 
