@@ -118,6 +118,20 @@ __device__ __forceinline__ uint32_t fbig32(uint32_t x) {
     if constexpr (kTB == 4) return x & 0x88888888u;
     else return x & (x >> 1) & 0x55555555u;
 }
+// the same bits before the field mask, OR-accumulated into acc (one shift
+// and one v_and_or_b32 per dword); mask the accumulator once with kBigMask
+__device__ __forceinline__ uint32_t fbig_acc(uint32_t x, uint32_t acc) {
+    if constexpr (kTB == 4) {
+        return x | acc;
+    } else {
+        // (x & (x >> 1)) | acc in one v_bitop3 (LUT 0xEA); the compiler
+        // splits it into v_and + half a v_or3
+        uint32_t r;
+        asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(r) : "v"(x), "v"(x >> 1), "v"(acc));
+        return r;
+    }
+}
+constexpr uint32_t kBigMask = kTB == 4 ? 0x88888888u : 0x55555555u;
 
 // escaped count (>= kEsc): two dependent loads -- the block's escape tile
 // index, then the tile's byte -- and, for a count >= 255 only, a binary
@@ -852,7 +866,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
                             cs[CPL * q + i] = POOL == 2 ? cs[CPL * q + i] + a * w : a;
                         }
-                        anybig |= fbig32(d[0]) | fbig32(d[1]) | fbig32(d[2]) | fbig32(d[3]);
+                        anybig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], anybig))));
                     }
                     {
                         const uint32_t d[4] = {hv.x, hv.y, hv.z, hv.w};
@@ -863,7 +877,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
                             hs[i] = POOL == 2 ? hs[i] + a * w : a;
                         }
-                        anybig |= fbig32(d[0]) | fbig32(d[1]) | fbig32(d[2]) | fbig32(d[3]);
+                        anybig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], anybig))));
                     }
                 }
             }
@@ -878,7 +892,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 #ifndef UPK_NO_K1A_DPP
             if constexpr (MODE == kModeScreen) {
                 const int D = (R + CPL - 1) / CPL;
-                if (D <= 2 && __ballot(anybig != 0u) == 0) {
+                if (D <= 2 && __ballot((anybig & kBigMask) != 0u) == 0) {
                     uint32_t T[kLoads];
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
@@ -928,7 +942,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             // escape among them), whose true count the screen does not know,
             // goes exact (kBig).  Rare: the strip is re-read (L2) for the
             // per-chunk bits only when some lane saw such a field.
-            if (__ballot(anybig != 0u) != 0) {
+            if (__ballot((anybig & kBigMask) != 0u) != 0) {
                 for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
                     for (int k = 0; k < P.nnc; ++k) {
                         gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, ncs[k]) + fbyte(kPadPos + p0 - 1));
