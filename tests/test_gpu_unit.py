@@ -86,6 +86,25 @@ def test_multi_sample_with_control(gpu_lib, oracle, seed):
     compare(ref, ref_sums, regs, gcnt)
 
 
+@pytest.mark.parametrize("big", [(1_400_000_000, 1_300_000_000, 1_200_000_000),
+                                 (3_000_000_000, 2_000_000_000, 7)], ids=["u32", "over"])
+def test_multi_sample_huge_counts(gpu_lib, oracle, big):
+    """several pooled samples sum in uint32 window words (kernels.hip WinT)
+    only while no position's sum can reach 2^32: 'u32' sums 3.9e9 at one
+    position on that path, 'over' (5e9 possible) takes the FP64 pooling with
+    zero coefficients (api.hip pool_mode); the reference's double countSum
+    (peakcall.cpp:186-200) is exact in both"""
+    rng = np.random.default_rng(250)
+    length, bw, bg, S = 120_000, 50, 0.004, 3
+    pos, cnt = random_unit(rng, length, bw, S=S)
+    i = pos.size // 2
+    cnt[i] = big
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, hit_thr=30.0)
+    regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt, hit_thr=30.0)
+    assert (regs["peak"] == pos[i]).any()
+    compare(ref, ref_sums, regs, gcnt)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_coefficients_q5(gpu_lib, oracle, seed):
     rng = np.random.default_rng(300 + seed)

@@ -509,9 +509,11 @@ int up_set_params(up_ctx *c, const up_params *p) {
             HIPCHK(hipMemcpy(c->d_nc.p, c->nc.data(), c->nc.size() * sizeof(int32_t), hipMemcpyHostToDevice));
         HIPCHK(c->d_ctl.ensure(S));
         HIPCHK(hipMemcpy(c->d_ctl.p, c->ctl.data(), S, hipMemcpyHostToDevice));
-        HIPCHK(c->d_coef.ensure(c->coef.size() + 1));
-        if (!c->coef.empty())
-            HIPCHK(hipMemcpy(c->d_coef.p, c->coef.data(), c->coef.size() * sizeof(double), hipMemcpyHostToDevice));
+        // without coefficients: zeros, so the FP64 pooling (POOL 2) of
+        // pool_mode's fallback sums 0 * c + c = c (the reference's countSum)
+        std::vector<double> dc = c->coef.empty() ? std::vector<double>(c->nc.size() + 1, 0.0) : c->coef;
+        HIPCHK(c->d_coef.ensure(dc.size() + 1));
+        HIPCHK(hipMemcpy(c->d_coef.p, dc.data(), dc.size() * sizeof(double), hipMemcpyHostToDevice));
     }
     // K1 screen: integer weight per non-control sample bounding its share of
     // |countSum| (1, or ceil(|coef| + 1) with coefficients, quirk Q5), and the
@@ -977,9 +979,14 @@ static int sync_units(up_ctx *c) {
     return UP_OK;
 }
 
+// 0: one non-control sample; 1: several, summed in uint32 window words
+// (kernels.hip WinT) -- only while no position's sum can reach 2^32, else
+// 2 with zero coefficients (d_coef), the FP64 pooling of -z (quirk Q5)
 static int pool_mode(const up_ctx *c) {
     if (!c->coef.empty()) return 2;
-    return c->nc.size() == 1 ? 0 : 1;
+    if (c->nc.size() == 1) return 0;
+    const double cmax = (double)std::max<uint32_t>(kEsc - 1, c->ovf_max_all) * (double)c->nc.size();
+    return cmax < 4294967296.0 ? 1 : 2;
 }
 
 static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps, uint32_t ovf_cap) {

@@ -68,10 +68,13 @@ __device__ __forceinline__ const UPK_CONST T *cptr(const T *p) {
     return (const UPK_CONST T *)p;
 }
 
-// window word storage: raw counts when the pooled count is the single
-// non-control sample's count, otherwise the FP64 pooled count
+// window word storage: integer pooled counts (one non-control sample's
+// count, or several samples' unscaled sum -- exact in uint32: the host runs
+// POOL 1 only when the largest possible sum is below 2^32, and the reference's
+// double countSum of integers is that same integer), otherwise the FP64
+// pooled count (coefficients, Q5)
 template <int POOL>
-using WinT = typename std::conditional<POOL == 0, uint32_t, double>::type;
+using WinT = typename std::conditional<POOL == 2, double, uint32_t>::type;
 
 __device__ __forceinline__ double rl_cs(uint32_t v, int l) { return (double)rl_u(v, l); }
 __device__ __forceinline__ double rl_cs(double v, int l) { return rl_d(v, l); }
@@ -212,12 +215,12 @@ __device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], const UnitDesc &
         for (int w = 0; w < N; ++w) cs[w] = c[w];
     } else {
 #pragma unroll
-        for (int w = 0; w < N; ++w) cs[w] = 0.0;
+        for (int w = 0; w < N; ++w) cs[w] = 0;
         for (int k = 0; k < nnc; ++k) {
             fetch(k);
             if constexpr (POOL == 1) {
 #pragma unroll
-                for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w];
+                for (int w = 0; w < N; ++w) cs[w] += c[w];
             } else {
                 const double q = coef[k];
 #pragma unroll
@@ -321,10 +324,13 @@ __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const Uni
     } else {
         // tracks per batch: two wave loads' worth (more held the K1b
         // register budget: 14 tracks in flight spilled)
-        constexpr int NQ = 2;
+#ifndef UPK_K1B_NQ
+#define UPK_K1B_NQ 2
+#endif
+        constexpr int NQ = UPK_K1B_NQ;
         constexpr int KB = (NQ * 64 / NL) < (kStageBytes / (NL * 16)) ? NQ * 64 / NL : kStageBytes / (NL * 16);
 #pragma unroll
-        for (int w = 0; w < N; ++w) cs[w] = 0.0;
+        for (int w = 0; w < N; ++w) cs[w] = 0;
         // POOL 2: the coefficient-weighted loop, then the unweighted one (Q5)
         for (int pass = 0; pass < (POOL == 2 ? 2 : 1); ++pass) {
             for (int k0 = 0; k0 < nnc; k0 += KB) {
@@ -351,7 +357,10 @@ __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const Uni
                     for (int w = 0; w < N; ++w)
                         c[w] = ((uint32_t)stage[NL * 16 * k + kWordBytes * w + fbyte(lane)] >> sh) & kTMask;
                     resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[k0 + k]), x0, lane);
-                    if (POOL == 2 && pass == 0) {
+                    if constexpr (POOL == 1) {
+#pragma unroll
+                        for (int w = 0; w < N; ++w) cs[w] += c[w];
+                    } else if (pass == 0) {
                         const double q = coef[k0 + k];
 #pragma unroll
                         for (int w = 0; w < N; ++w) cs[w] = cs[w] + (double)c[w] * q;
@@ -686,9 +695,14 @@ __device__ __forceinline__ uint32_t screen_any(int R, const uint32_t *rd, uint32
 #ifndef UPK_K1B_WPE
 #define UPK_K1B_WPE 3
 #endif
+#ifndef UPK_K1B_WPE_ND
+#define UPK_K1B_WPE_ND UPK_K1B_WPE
+#endif
 #ifndef UPK_SCAN_ATTR
-#define UPK_SCAN_ATTR \
-    __attribute__((amdgpu_waves_per_eu(MODE == kModeExact ? UPK_K1B_WPE : MODE == kModeScreen ? UPK_K1A_WPE : 1)))
+#define UPK_SCAN_ATTR                                                                                   \
+    __attribute__((amdgpu_waves_per_eu(MODE == kModeExact ? (NONDIR ? UPK_K1B_WPE_ND : UPK_K1B_WPE) \
+                                       : MODE == kModeScreen ? UPK_K1A_WPE                           \
+                                                             : 1)))
 #endif
 template <int NH, int POOL, bool NONDIR, bool PROF, int MODE>
 __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, uint32_t strip_begin,
