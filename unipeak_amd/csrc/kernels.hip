@@ -1778,6 +1778,74 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 counted = true;
             }
         }
+        if constexpr (POOL != 2) {
+            // several samples (and at most 32 (strand, sample) tracks): each
+            // 64-position block's bytes of every track come with one wave
+            // load (lane l: track l/2, 16-byte piece l%2 of the 32 bytes
+            // covering the block), staged through this wave's terms area and
+            // read back as lane = position; the next block's load is in
+            // flight meanwhile.  (Per sample, pooled fetch then count_at, the
+            // block cost S + nnc dependent round trips.)
+            constexpr int NSTR = NONDIR ? 2 : 1;
+            if (kn && !counted && S > 1 && S * NSTR <= 32) {
+                best = kval;
+                best_x = kpos;
+                const int jt = lane >> 1;
+                const bool tl = jt < S * NSTR;
+                gu8 *tb = track_u8(U, S, tl ? jt / S : 0, tl ? jt % S : 0);
+                auto bload = [&](int64_t x0) -> u32x4 {
+                    u32x4 r = {0u, 0u, 0u, 0u};
+                    if (tl) r = ((gu32x4 *)(tb + (fbyte(kPadPos + x0 - 1) & ~(int64_t)15)))[lane & 1];
+                    return r;
+                };
+                uint8_t *stg = (uint8_t *)terms;
+                u32x4 nv = bload(left);
+                for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64, ++blk) {
+                    const int64_t x = x0 + lane;
+                    const bool valid = x <= (int64_t)right;
+                    const u32x4 cv = nv;
+                    if (x0 + 64 <= (int64_t)right) nv = bload(x0 + 64);
+                    __builtin_amdgcn_wave_barrier();  // the previous block's reads are done
+                    *(u32x4 *)(stg + 16 * lane) = cv;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    const int64_t n0 = kPadPos + x - 1;
+                    const uint32_t off = (uint32_t)(fbyte(n0) - (fbyte(kPadPos + x0 - 1) & ~(int64_t)15));
+                    const uint32_t sh = fshift(n0);
+                    auto fld = [&](int j) -> uint32_t {  // track j = strand * S + sample
+                        const uint32_t f = ((uint32_t)stg[32 * j + off] >> sh) & kTMask;
+                        return (f == kEsc && valid) ? ovf_lookup(U, (uint32_t)j, (uint32_t)x) : f;
+                    };
+                    uint32_t pf = 0, pr = 0;  // pooled counts (their sum is exact: host bound)
+                    for (int k = 0; k < P.nnc; ++k) {
+                        pf += fld(P.nc[k]);
+                        if constexpr (NONDIR) pr += fld(S + P.nc[k]);
+                    }
+                    const bool h0 = valid && pf != 0u;
+                    const bool h1 = NONDIR && valid && pr != 0u;
+                    uint32_t pc = 0;
+                    for (int s = 0; s < S; ++s) {
+                        uint32_t c = h0 ? fld(s) : 0u;
+                        if constexpr (NONDIR) c += h1 ? fld(S + s) : 0u;
+                        pc += c;
+                        const uint32_t t = wave_sum_u32(c);
+                        if (lane == (s & 63)) {
+                            const int slot = s >> 6;
+                            esum[0] += slot == 0 ? t : 0u;
+                            esum[1] += slot == 1 ? t : 0u;
+                            esum[2] += slot == 2 ? t : 0u;
+                            esum[3] += slot == 3 ? t : 0u;
+                        }
+                    }
+                    if (blk < kStatCache) pcache[64 * blk + lane] = pc;
+                    cnt_acc += pc;
+                    sum_acc += pc * (uint32_t)(uint16_t)(x - left);
+                }
+                __builtin_amdgcn_wave_barrier();  // terms reused below
+                counted = true;
+            }
+        }
         if (kn && !counted) {
             best = kval;
             best_x = kpos;
