@@ -118,6 +118,35 @@ def test_coefficients_q5(gpu_lib, oracle, seed):
     assert prof.tobytes() == f.tobytes()
 
 
+@pytest.mark.parametrize("S,nondir,bw", [(9, False, 50), (9, False, 100), (36, False, 50),
+                                          (3, True, 50), (12, True, 90)],
+                         ids=["8s1c", "8s1c_bw100", "35s_seq", "3s_nondir", "11s_nondir_bw90"])
+def test_pooled_samples(gpu_lib, oracle, S, nondir, bw):
+    """several pooled samples (POOL 1, uint32 window sums) and a control:
+    K3's batched per-block fetch while the (strand, sample) tracks fit one
+    wave load (32), the per-sample path beyond ('35s_seq'), both strands
+    without the correlation ('*_nondir'), NH 2 windows"""
+    rng = np.random.default_rng(500 + S + bw)
+    length, bg = 160_000, 0.004
+    control = [0] * (S - 1) + [1]
+    pos_f, cnt_f = random_unit(rng, length, bw, S=S)
+    if not nondir:
+        ref, ref_sums = oracle.run_unit(bw, bg, pos_f, cnt_f, control=control, hit_thr=30.0)
+        regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos_f, cnt_f, control=control, hit_thr=30.0)
+    else:
+        pos_r, cnt_r = random_unit(rng, length, bw, S=S)
+        allp = np.union1d(pos_f, pos_r).astype(np.uint32)
+        cf = np.zeros((allp.size, S), np.uint32)
+        cr = np.zeros((allp.size, S), np.uint32)
+        cf[np.searchsorted(allp, pos_f)] = cnt_f
+        cr[np.searchsorted(allp, pos_r)] = cnt_r
+        ref, ref_sums = oracle.run_unit(bw, bg, allp, cf, cr, nondir=True, control=control, hit_thr=30.0)
+        regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, allp, cf, cr, nondir=True, control=control,
+                                 hit_thr=30.0)
+    assert len(regs) > 5
+    compare(ref, ref_sums, regs, gcnt)
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_nondirectional_with_corr(gpu_lib, oracle, seed):
     rng = np.random.default_rng(400 + seed)
