@@ -4,7 +4,7 @@
 Default workload (BASELINE.json configs[1], the metric's config): hg19 full
 genome (25 contigs, 3,095,693,983 bp), one directional sample (3SEQ-style),
 default parameters (bw 50, -r 25, -k 50, -t 10), synthetic hg19-shaped tag
-counts generated on the device, packed to 4-bit tracks and
+counts generated on the device, packed to 2-bit tracks and
 resident in HBM before timing.  Other BASELINE configs are available with
 --workload for our own measurements (the default line is the headline):
 
@@ -12,7 +12,11 @@ resident in HBM before timing.  Other BASELINE configs are available with
   hg19-nondir1 configs[2]  regions pass of C3: -D -y, 1 sample, both strands
   hg19-shift   configs[2]  the whole C3 pipeline: strand_shift, then regions -D -y -s <best>
   hg19-8s1c    configs[3]  8 samples + 1 negative control (-e 9), directional
-  hg19mm9-32s  configs[4]  hg19+mm9, 32 samples, -D -k 50 -u 0.3 -y (8 GPUs)
+  hg19mm9-32s  configs[4]  hg19+mm9, 32 samples, -D -k 50 -u 0.3 -y (8 GPUs): the survey's
+                           generator (independent peak centres per sample: no region
+                           reaches -r 25 once 32 samples are pooled)
+  hg19mm9-32rep configs[4] the same table and flags on 32 replicates (shared peak
+                           centres), read with -s 75: the filters decide
 
 One step = the whole hot path over the genome: RCCL all-reduce of the tag
 totals -> background -> up_run_async (K1a stream+screen on a high-priority
@@ -73,6 +77,14 @@ WORKLOADS = {
                         corr=0.3, want_corr=True, baseline="configs[4]",
                         desc="hg19+mm9 (names prefixed), 32 nondirectional samples, -D -k 50 -u 0.3 -y, "
                              "bw 50 (BASELINE configs[4])"),
+    # configs[4] as a ChIP experiment of 32 replicates: shared peak centres
+    # (per-sample heights and jitter; artifact, spike and weak peaks the
+    # filters reject), read with -s 75 as strand_shift finds it
+    "hg19mm9-32rep": dict(tables=["hg19", "mm9"], nondir=True, samples=32, controls=0, kurt=50.0,
+                          corr=0.3, want_corr=True, baseline="configs[4]", peak_seed=7, shift=75,
+                          desc="hg19+mm9 (names prefixed), 32 nondirectional replicate samples "
+                               "(shared peak centres), -D -k 50 -u 0.3 -y -s 75, bw 50 "
+                               "(BASELINE configs[4])"),
 }
 
 
@@ -170,6 +182,11 @@ def main():
     g = capi.Lib(dev)
     g.set_params(args.bw, S, 0.0029, nondir=nondir, control=control)  # background set per step
     t_gen = time.time()
+    pseed, shift = W.get("peak_seed", 0), W.get("shift", 0)
+
+    def offset(synth_strand):  # -s: forward +s, reverse -s (misc/format.cpp:693-705)
+        return shift if synth_strand == 0 else -shift
+
     for k in mine:  # ascending global order: records come back unit-major
         ci, buf = units[k]
         u = g.add_unit(lens[ci], buffer_id=buf)
@@ -177,7 +194,8 @@ def main():
             synth_strand = st if nondir else buf
             for smp in range(S):
                 seed = args.seed + smp if smp < s_nc else 2000 + (smp - s_nc)
-                g.synth(u, st, smp, seed, ci, synth_strand, nondir=nondir, peaks=smp < s_nc)
+                g.synth(u, st, smp, seed, ci, synth_strand, nondir=nondir, peaks=smp < s_nc,
+                        offset=offset(synth_strand), peak_seed=pseed)
     local_tags = sum(g.tag_total(i, st, smp) for i in range(len(mine)) for st in range(nstr)
                      for smp in range(s_nc))
     if sim_world > 1:  # the background needs the genome-wide total: generate the other units too
@@ -191,7 +209,9 @@ def main():
             u = g2.add_unit(lens[ci], buffer_id=buf)
             for st in range(nstr):
                 for smp in range(s_nc):
-                    g2.synth(u, st, smp, args.seed + smp, ci, st if nondir else buf, nondir=nondir, peaks=True)
+                    sst = st if nondir else buf
+                    g2.synth(u, st, smp, args.seed + smp, ci, sst, nondir=nondir, peaks=True,
+                             offset=offset(sst), peak_seed=pseed)
                     local_tags += g2.tag_total(u, st, smp)
         g2.close()
     gen_s = time.time() - t_gen

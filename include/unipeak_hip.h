@@ -143,6 +143,13 @@ int up_unit_synth(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
 int up_unit_synth_offset(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
                          uint64_t seed, uint32_t contig_index, int32_t synth_strand,
                          int32_t nondir, int32_t with_peaks, int32_t offset);
+/* the same with peak_seed != 0: replicate samples -- peak
+ * centres drawn from peak_seed and shared by every sample generated with it,
+ * per-sample heights, centre jitter (-20..+20) and tag offsets from `seed`;
+ * peak_seed 0 is up_unit_synth_offset */
+int up_unit_synth_ex(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
+                     uint64_t seed, uint32_t contig_index, int32_t synth_strand,
+                     int32_t nondir, int32_t with_peaks, int32_t offset, uint64_t peak_seed);
 /* total tags of one track (sum of its counts, uint64) */
 int up_unit_tag_total(up_ctx *ctx, uint32_t unit, int32_t strand, uint16_t sample,
                       uint64_t *total);

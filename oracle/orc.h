@@ -120,6 +120,22 @@ int orc_tags_in_regions_main(int argc, char **argv);
 size_t orc_synth_track(uint64_t seed, uint32_t contig, int strand, int nondir,
                        uint32_t len, uint16_t bw, int with_peaks,
                        uint32_t *pos, uint32_t *cnt, size_t cap);
+/* the same track moved by `offset` (the wiggle reader's -s) and, with
+ * peak_seed != 0, in replicate mode (shared peak centres) */
+size_t orc_synth_track_ex(uint64_t seed, uint32_t contig, int strand, int nondir,
+                          uint32_t len, uint16_t bw, int with_peaks, int32_t offset,
+                          uint64_t peak_seed, uint32_t *pos, uint32_t *cnt, size_t cap);
+/* one unit of a synthetic genome run entirely inside the oracle: the
+ * (strand, sample) tracks are generated (orc_synth_track_ex; seeds[s],
+ * with_peaks[s], offset[strand]), merged by position and fed to one
+ * ProfileBuffer in the reference's order (forward add before reverse add at
+ * a position, as orc_run_unit), then flushed.  Output as orc_run_unit. */
+int64_t orc_genome_unit(const double *kernel, uint32_t kernel_size, double region_thr,
+                        double kurt_thr, double corr_thr, double hit_thr, int buffer_forward,
+                        int nondir, uint16_t n_expt, const uint8_t *control,
+                        const uint64_t *seeds, const uint8_t *with_peaks, uint64_t peak_seed,
+                        const int32_t *offset, uint32_t contig, uint32_t len, uint16_t bw,
+                        orc_unit_region *out, uint32_t *out_sums, size_t cap);
 /* the Poisson thresholds used by the background draw (6 entries) */
 void orc_synth_thresholds(double lambda, uint64_t *thr6);
 

@@ -497,6 +497,79 @@ int64_t orc_run_unit(const double *kernel, uint32_t kernel_size,
     return (int64_t)u.n;
 }
 
+/* a synthetic unit generated and run inside the oracle (bench.py's genome
+ * workloads at full size without host count matrices; see orc.h) */
+int64_t orc_genome_unit(const double *kernel, uint32_t kernel_size, double region_thr,
+                        double kurt_thr, double corr_thr, double hit_thr, int buffer_forward,
+                        int nondir, uint16_t n_expt, const uint8_t *control,
+                        const uint64_t *seeds, const uint8_t *with_peaks, uint64_t peak_seed,
+                        const int32_t *offset, uint32_t contig, uint32_t len, uint16_t bw,
+                        orc_unit_region *out, uint32_t *out_sums, size_t cap) {
+    const int nstr = nondir ? 2 : 1;
+    const size_t ntr = (size_t)nstr * n_expt;
+    uint32_t **tp = (uint32_t **)xmalloc(ntr * sizeof(uint32_t *));
+    uint32_t **tc = (uint32_t **)xmalloc(ntr * sizeof(uint32_t *));
+    size_t *tn = (size_t *)xmalloc(ntr * sizeof(size_t));
+    size_t *cur = (size_t *)calloc(ntr, sizeof(size_t));
+    /* positions holding a tag of any track, as a bitmap over 1..len */
+    uint64_t *bits = (uint64_t *)calloc((size_t)len / 64 + 2, sizeof(uint64_t));
+    for (int k = 0; k < nstr; ++k) {
+        const int strand = nondir ? k : (buffer_forward ? 0 : 1);
+        for (uint16_t s = 0; s < n_expt; ++s) {
+            const size_t t = (size_t)k * n_expt + s;
+            const size_t need = orc_synth_track_ex(seeds[s], contig, strand, nondir, len, bw,
+                                                   with_peaks[s], offset[strand], peak_seed, NULL,
+                                                   NULL, 0);
+            tp[t] = (uint32_t *)xmalloc((need + 1) * sizeof(uint32_t));
+            tc[t] = (uint32_t *)xmalloc((need + 1) * sizeof(uint32_t));
+            tn[t] = orc_synth_track_ex(seeds[s], contig, strand, nondir, len, bw, with_peaks[s],
+                                       offset[strand], peak_seed, tp[t], tc[t], need);
+            for (size_t i = 0; i < tn[t]; ++i) bits[tp[t][i] >> 6] |= 1ull << (tp[t][i] & 63);
+        }
+    }
+    unit_sink u = {out, out_sums, cap, 0, n_expt};
+    orc_buf *b = orc_buf_new(kernel, kernel_size, region_thr, kurt_thr, corr_thr, hit_thr,
+                             buffer_forward, n_expt, control, NULL, 0, unit_cb, &u, NULL, NULL);
+    b->rej_cb = unit_rej_cb;
+    b->contig = contig;
+    b->region->contig = contig;
+    uint32_t *cv = (uint32_t *)xmalloc((size_t)nstr * n_expt * sizeof(uint32_t));
+    for (size_t w = 0; w <= (size_t)len / 64 + 1; ++w) {
+        uint64_t m = bits[w];
+        while (m) {
+            const uint32_t x = (uint32_t)(w * 64 + (size_t)__builtin_ctzll(m));
+            m &= m - 1;
+            for (int k = 0; k < nstr; ++k) {
+                int any = 0;
+                for (uint16_t s = 0; s < n_expt; ++s) {
+                    const size_t t = (size_t)k * n_expt + s;
+                    uint32_t c = 0;
+                    if (cur[t] < tn[t] && tp[t][cur[t]] == x) c = tc[t][cur[t]++];
+                    cv[(size_t)k * n_expt + s] = c;
+                    any |= c != 0;
+                }
+                /* orc_run_unit's order: forward add, then reverse add */
+                if (any)
+                    orc_buf_add(b, cv + (size_t)k * n_expt, contig, x,
+                                nondir ? k == 0 : buffer_forward);
+            }
+        }
+    }
+    orc_buf_flush(b);
+    orc_buf_free(b);
+    for (size_t t = 0; t < ntr; ++t) {
+        free(tp[t]);
+        free(tc[t]);
+    }
+    free(tp);
+    free(tc);
+    free(tn);
+    free(cur);
+    free(bits);
+    free(cv);
+    return (int64_t)u.n;
+}
+
 typedef struct {
     double *score;
     uint32_t len;

@@ -46,10 +46,23 @@ static int cmp_u32(const void *a, const void *b) {
 size_t orc_synth_track(uint64_t seed, uint32_t contig, int strand, int nondir,
                        uint32_t len, uint16_t bw, int with_peaks,
                        uint32_t *pos, uint32_t *cnt, size_t cap) {
+    return orc_synth_track_ex(seed, contig, strand, nondir, len, bw, with_peaks, 0, 0, pos, cnt,
+                              cap);
+}
+
+/* offset: the track moved as the wiggle reader's -s moves it (forward +s,
+ * reverse -s, misc/format.cpp:693-705), counts leaving [1, len] dropped.
+ * peak_seed != 0: replicate samples -- centres from peak_seed's keys, shared
+ * by every sample; per-sample height and a -20..+20 centre jitter from the
+ * sample's own seed (device: up_unit_synth_ex). */
+size_t orc_synth_track_ex(uint64_t seed, uint32_t contig, int strand, int nondir,
+                          uint32_t len, uint16_t bw, int with_peaks, int32_t offset,
+                          uint64_t peak_seed, uint32_t *pos, uint32_t *cnt, size_t cap) {
     const uint64_t skey = mix64(seed);
     const uint64_t ckey = mix64(skey ^ (uint64_t)(contig + 1));
     const uint64_t tkey = mix64(ckey ^ (uint64_t)(0x100 + strand));
-    const uint64_t pkey = mix64(ckey ^ (uint64_t)(0x200 + (nondir ? 0 : strand)));
+    const uint64_t pckey = peak_seed ? mix64(mix64(peak_seed) ^ (uint64_t)(contig + 1)) : ckey;
+    const uint64_t pkey = mix64(pckey ^ (uint64_t)(0x200 + (nondir ? 0 : strand)));
     const int64_t lo = 2 * (int64_t)bw + 2, hi = (int64_t)len - 2 * (int64_t)bw - 1;
     uint64_t thr[6];
     orc_synth_thresholds(SYN_LAMBDA, thr);
@@ -66,16 +79,27 @@ size_t orc_synth_track(uint64_t seed, uint32_t contig, int strand, int nondir,
         const int64_t shift = (nondir && strand == 1) ? 150 : 0;
         for (uint32_t j = 0; chi >= clo && j < npk; ++j) {
             const uint64_t h = mix64(pkey ^ mix64(0x7065616B00000000ull + j));
-            const int64_t centre = clo + (int64_t)(h % (uint64_t)(chi - clo + 1));
-            const uint32_t n = 20u + (uint32_t)(mix64(h) % 180u);
+            int64_t centre = clo + (int64_t)(h % (uint64_t)(chi - clo + 1));
+            uint32_t n = 20u + (uint32_t)(mix64(h) % 180u);
+            // replicate mode: the shared hash also picks the peak's kind --
+            // 0/1 an artifact on strand 0/1 only, 2 a spike (every tag of every
+            // sample at the shared centre), 3 a weak peak (2..11 tags per sample), else normal
+            const uint32_t kind = peak_seed ? (uint32_t)(h >> 56) & 15u : 4u;
+            if (peak_seed) {
+                const uint64_t hs = mix64(h ^ skey);
+                n = 20u + (uint32_t)(hs % 180u);
+                if (kind != 2) centre += (int64_t)((hs >> 32) % 41u) - 20;
+                if (kind == 3) n = 2u + (uint32_t)(hs % 10u);
+                if (kind <= 1 && (uint32_t)strand != kind) n = 0;
+            }
             for (uint32_t i = 0; i < n; ++i) {
                 int64_t s = 0;
                 const uint64_t base = mix64(tkey ^ h ^ mix64(0x74616700000000ull + i));
                 for (int m = 0; m < 12; ++m) s += (int64_t)(mix64(base + (uint64_t)m) >> 32);
                 const int64_t num = 60 * (s - 6 * 4294967296ll);
-                const int64_t off = (num + 2147483648ll) >> 32; /* floor */
+                const int64_t off = kind == 2 ? 0 : (num + 2147483648ll) >> 32; /* floor */
                 const int64_t p = centre + shift + off;
-                if (p < lo || p > hi) continue;
+                if (p < lo || p > hi || p + offset < 1 || p + offset > (int64_t)len) continue;
                 if (ntags == tcap) {
                     tcap = tcap ? 2 * tcap : 1024;
                     tags = (uint32_t *)realloc(tags, tcap * sizeof(uint32_t));
@@ -83,17 +107,59 @@ size_t orc_synth_track(uint64_t seed, uint32_t contig, int strand, int nondir,
                 tags[ntags++] = (uint32_t)p;
             }
         }
-        qsort(tags, ntags, sizeof(uint32_t), cmp_u32);
     }
-
     size_t out = 0, ti = 0;
+    if (peak_seed) {
+        /* replicate mode's background: chunks of 2^16 positions, each with
+         * n ~ Poisson(lambda * 2^16) tags at uniform positions (n = #{k :
+         * tab[k] <= u0}); device: synth_bgc_kernel */
+        uint64_t tab[1024];
+        const double mu = SYN_LAMBDA * 65536.0;
+        double pr = exp(-mu), cdf = pr;
+        for (int k = 0; k < 1024; ++k) {
+            tab[k] = cdf >= 1.0 ? ~0ull : (uint64_t)(cdf * 18446744073709551616.0);
+            pr *= mu / (double)(k + 1);
+            cdf += pr;
+        }
+        const uint64_t nch = hi >= lo ? ((uint64_t)(hi - lo + 1) + 65535) >> 16 : 0;
+        for (uint64_t ch = 0; ch < nch; ++ch) {
+            const uint64_t u0 = mix64(tkey ^ mix64(0x6267000000000000ull + ch));
+            uint32_t a = 0, b = 1024;
+            while (a < b) {
+                const uint32_t m = (a + b) >> 1;
+                if (tab[m] <= u0) a = m + 1;
+                else b = m;
+            }
+            const int64_t base = lo + (int64_t)(ch << 16);
+            for (uint32_t i = 0; i < a; ++i) {
+                const int64_t x = base + (int64_t)(mix64(u0 ^ mix64((uint64_t)i + 1)) >> 48);
+                if (x > hi || x + offset < 1 || x + offset > (int64_t)len) continue;
+                if (ntags == tcap) {
+                    tcap = tcap ? 2 * tcap : 1024;
+                    tags = (uint32_t *)realloc(tags, tcap * sizeof(uint32_t));
+                }
+                tags[ntags++] = (uint32_t)x;
+            }
+        }
+        qsort(tags, ntags, sizeof(uint32_t), cmp_u32);
+        while (ti < ntags) {
+            const uint32_t x = tags[ti];
+            uint32_t c = 0;
+            while (ti < ntags && tags[ti] == x) { ++c; ++ti; }
+            if (out < cap) { pos[out] = (uint32_t)((int64_t)x + offset); cnt[out] = c; }
+            ++out;
+        }
+        free(tags);
+        return out;
+    }
+    if (ntags) qsort(tags, ntags, sizeof(uint32_t), cmp_u32);
     for (int64_t x = lo; x <= hi; ++x) {
         const uint64_t u = mix64(tkey ^ mix64((uint64_t)x));
         uint32_t c = 0;
         while (c < 6 && u >= thr[c]) ++c;
         while (ti < ntags && tags[ti] == (uint32_t)x) { ++c; ++ti; }
-        if (c) {
-            if (out < cap) { pos[out] = (uint32_t)x; cnt[out] = c; }
+        if (c && x + offset >= 1 && x + offset <= (int64_t)len) {
+            if (out < cap) { pos[out] = (uint32_t)(x + offset); cnt[out] = c; }
             ++out;
         }
     }

@@ -43,6 +43,15 @@ class Oracle:
         L.orc_synth_track.restype = c.c_size_t
         L.orc_synth_track.argtypes = [c.c_uint64, c.c_uint32, c.c_int, c.c_int, c.c_uint32,
                                       c.c_uint16, c.c_int, vp, vp, c.c_size_t]
+        L.orc_synth_track_ex.restype = c.c_size_t
+        L.orc_synth_track_ex.argtypes = [c.c_uint64, c.c_uint32, c.c_int, c.c_int, c.c_uint32,
+                                         c.c_uint16, c.c_int, c.c_int32, c.c_uint64, vp, vp,
+                                         c.c_size_t]
+        L.orc_genome_unit.restype = c.c_int64
+        L.orc_genome_unit.argtypes = [vp, c.c_uint32, c.c_double, c.c_double, c.c_double,
+                                      c.c_double, c.c_int, c.c_int, c.c_uint16, vp, vp, vp,
+                                      c.c_uint64, vp, c.c_uint32, c.c_uint32, c.c_uint16, vp, vp,
+                                      c.c_size_t]
         L.orc_baseline_run.restype = c.c_int
         L.orc_baseline_run.argtypes = [c.c_uint32, vp, c.c_uint64, c.c_uint16, c.c_double,
                                        c.c_double, c.c_double, c.c_double, vp, vp, vp]
@@ -110,6 +119,37 @@ class Oracle:
                                    pos.ctypes.data, cnt.ctypes.data, cap)
         assert n <= cap
         return pos[:n].copy(), cnt[:n].copy()
+
+    def synth_track_ex(self, seed, contig, strand, nondir, length, bw, peaks=True, offset=0,
+                       peak_seed=0):
+        n = self.L.orc_synth_track_ex(seed, contig, strand, int(nondir), length, bw, int(peaks),
+                                      offset, peak_seed, None, None, 0)
+        pos = np.zeros(n + 1, np.uint32)
+        cnt = np.zeros(n + 1, np.uint32)
+        m = self.L.orc_synth_track_ex(seed, contig, strand, int(nondir), length, bw, int(peaks),
+                                      offset, peak_seed, pos.ctypes.data, cnt.ctypes.data, n + 1)
+        assert m == n
+        return pos[:n].copy(), cnt[:n].copy()
+
+    def genome_unit(self, bw, background, contig, length, seeds, with_peaks, *, region_thr=25.0,
+                    kurt_thr=50.0, corr_thr=-1.0, hit_thr=10.0, buffer_forward=True,
+                    nondir=False, control=None, peak_seed=0, offset=(0, 0), cap=1 << 20):
+        """All candidate regions of one synthetic unit, generated and run
+        inside the oracle (orc_genome_unit): no host count matrices."""
+        k = self.kernel(bw, 1.0 / background)
+        S = len(seeds)
+        sd = np.ascontiguousarray(seeds, np.uint64)
+        wp = np.ascontiguousarray(with_peaks, np.uint8)
+        ctl = np.zeros(S, np.uint8) if control is None else np.asarray(control, np.uint8)
+        off = np.ascontiguousarray(offset, np.int32)
+        out = np.zeros(cap, UNIT_DTYPE)
+        sums = np.zeros((cap, S), np.uint32)
+        n = self.L.orc_genome_unit(k.ctypes.data, k.size, region_thr, kurt_thr, corr_thr, hit_thr,
+                                   int(buffer_forward), int(nondir), S, ctl.ctypes.data,
+                                   sd.ctypes.data, wp.ctypes.data, peak_seed, off.ctypes.data,
+                                   contig, length, bw, out.ctypes.data, sums.ctypes.data, cap)
+        assert n <= cap
+        return out[:n], sums[:n]
 
     def baseline(self, lens, seed, bw, region_thr, kurt_thr, hit_thr, background):
         lens = np.ascontiguousarray(lens, np.uint32)

@@ -10,9 +10,10 @@ checked against the oracle on the same seeded data.
     configs[2]  hg19, 1 nondirectional sample, -D -y           (25 units)
     configs[3]  hg19, 8 pooled samples + 1 control             (50 units)
     configs[4]  hg19+mm9 (prefixed), 32 nondirectional samples, -D -k 50
-                -u 0.3 -y, on a documented contig subset (hg19_chr21,
-                mm9_chrY, mm9_chrM: one rank's worth of 32-sample work
-                would need ~25 GB of oracle count matrices)
+                -u 0.3 -y: all 47 contigs on the replicate generator
+                (shared peak centres, -s 75) with the oracle generating
+                each unit itself (orc_genome_unit); plus the survey-spec
+                generator on a contig subset at -r 1 -u -0.95
 * CLI level (byte-identical output files, bin/ vs the oracle's restatement
   of the reference CLIs, on synthetic wiggle files):
     configs[0]  chr21-only table, -m 3095693983, 1 directional sample
@@ -75,7 +76,7 @@ def seeds(S, n_ctl, base=1000):
 
 
 def gpu_genome(capi, contigs, sel, S, n_ctl, nondir, kurt, corr, want_corr, background=None,
-               region_thr=25.0):
+               region_thr=25.0, peak_seed=0, shift=0):
     """every unit of the selected contigs through one context, exactly as
     bench.py sets it up -> (units, regions, counts, background)"""
     lens = [L for _, L in contigs]
@@ -91,8 +92,9 @@ def gpu_genome(capi, contigs, sel, S, n_ctl, nondir, kurt, corr, want_corr, back
             assert u == k
             for st in range(nstr):
                 for smp in range(S):
-                    g.synth(u, st, smp, sd[smp][0], ci, st if nondir else buf, nondir=nondir,
-                            peaks=sd[smp][1])
+                    sst = st if nondir else buf
+                    g.synth(u, st, smp, sd[smp][0], ci, sst, nondir=nondir, peaks=sd[smp][1],
+                            offset=shift if sst == 0 else -shift, peak_seed=peak_seed)
         if background is None:  # regions.cpp:205-213 with the uint32 genome size (Q10)
             tags = sum(g.tag_total(k, st, smp) for k in range(len(units)) for st in range(nstr)
                        for smp in range(s_nc))
@@ -132,18 +134,37 @@ def oracle_unit(oracle, contigs, unit, S, n_ctl, nondir, kurt, corr, background,
                            cap=1 << 20)
 
 
+def oracle_genome_unit(oracle, contigs, unit, S, n_ctl, nondir, kurt, corr, background,
+                       region_thr=25.0, peak_seed=0, shift=0):
+    """the same unit generated and run inside the oracle (orc_genome_unit):
+    no host count matrices, so a 32-sample hg19+mm9 genome fits"""
+    ci, buf = unit
+    sd = seeds(S, n_ctl)
+    s_nc = S - n_ctl
+    return oracle.genome_unit(BW, background, ci, contigs[ci][1], [a for a, _ in sd],
+                              [int(b) for _, b in sd], region_thr=region_thr, kurt_thr=kurt,
+                              corr_thr=corr, hit_thr=10.0 * s_nc, buffer_forward=buf == 0,
+                              nondir=nondir, control=[0] * s_nc + [1] * n_ctl,
+                              peak_seed=peak_seed, offset=(shift, -shift))
+
+
 def check_genome(capi, oracle, contigs, sel, S, n_ctl, nondir, kurt, corr, want_corr,
-                 background=None, min_regions=1, region_thr=25.0):
+                 background=None, min_regions=1, region_thr=25.0, peak_seed=0, shift=0,
+                 in_oracle=False):
     units, regs, cnt, bg = gpu_genome(capi, contigs, sel, S, n_ctl, nondir, kurt, corr,
-                                      want_corr, background, region_thr)
+                                      want_corr, background, region_thr, peak_seed, shift)
     assert len(regs) >= min_regions
     # unit-major records: one slice per unit
     bounds = np.searchsorted(regs["unit"], np.arange(len(units) + 1))
     assert np.all(np.diff(regs["unit"].astype(np.int64)) >= 0)
     order = sorted(range(len(units)), key=lambda k: -contigs[units[k][0]][1])  # longest first
     with ThreadPoolExecutor(WORKERS) as ex:
-        futs = {k: ex.submit(oracle_unit, oracle, contigs, units[k], S, n_ctl, nondir, kurt, corr,
-                             bg, region_thr) for k in order}
+        if in_oracle or peak_seed or shift:
+            futs = {k: ex.submit(oracle_genome_unit, oracle, contigs, units[k], S, n_ctl, nondir,
+                                 kurt, corr, bg, region_thr, peak_seed, shift) for k in order}
+        else:
+            futs = {k: ex.submit(oracle_unit, oracle, contigs, units[k], S, n_ctl, nondir, kurt,
+                                 corr, bg, region_thr) for k in order}
         total = accepted = 0
         for k in range(len(units)):
             ref, ref_sums = futs[k].result()
@@ -210,6 +231,34 @@ def test_configs4_hg19mm9_32_samples_subset(gpu_lib, oracle):
     total, acc = check_genome(gpu_lib, oracle, contigs, sel, 32, 0, True, 50.0, -0.95, True,
                               background=bg, min_regions=100, region_thr=1.0)
     assert 0 < acc < total
+
+
+def test_configs4_hg19mm9_32_replicates_full(gpu_lib, oracle):
+    """BASELINE configs[4] at its stated size and flags: all 47 contigs of the
+    prefixed hg19+mm9 table, 32 nondirectional samples, -D -k 50 -u 0.3 -y,
+    -r 25, -t 10 (x 32), bw 50 -- on the replicate generator (bench.py's
+    hg19mm9-32rep: shared peak centres, read with -s 75 as strand_shift
+    finds it), whose pooled peaks cross -r 25 and whose
+    artifact / spike peaks the correlation and kurtosis filters reject.  The
+    background is the one bench.py computes (the tag totals over the uint32
+    genome size, Q10).  Every candidate of every unit against the oracle,
+    which generates and runs each unit itself (orc_genome_unit).  The -s
+    shift moves reverse tags to positions <= bw, so every unit also takes
+    the quirk-Q1 head replay."""
+    contigs = load_tables(["hg19", "mm9"])
+    assert len(contigs) == 47 and sum(L for _, L in contigs) == 5_750_605_500
+    total, acc = check_genome(gpu_lib, oracle, contigs, range(len(contigs)), 32, 0, True, 50.0,
+                              0.3, True, min_regions=30_000, peak_seed=7, shift=75)
+    assert 0.8 * total < acc < total  # every filter family decides somewhere
+
+
+def test_configs1_hg19_in_oracle_generation(gpu_lib, oracle):
+    """configs[1] once more with the oracle generating each unit itself
+    (orc_genome_unit) -- the same answer as the matrix path above"""
+    contigs = load_tables(["hg19"])
+    total, acc = check_genome(gpu_lib, oracle, contigs, range(len(contigs)), 1, 0, False, 50.0,
+                              -1.0, False, min_regions=40_000, in_oracle=True)
+    assert total == 41_450 and acc == 41_087
 
 
 # ---- CLI level ------------------------------------------------------------

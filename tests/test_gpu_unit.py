@@ -259,6 +259,27 @@ def test_synthetic_track_offset(gpu_lib, oracle, offset, strand):
     assert ref.tobytes() == f.tobytes()
 
 
+@pytest.mark.parametrize("peak_seed,offset,strand,sample_seed",
+                         [(7, 75, 0, 1000), (7, -75, 1, 1031), (99, 0, 0, 1005), (7, -300, 1, 1002)])
+def test_synthetic_track_replicate_mode(gpu_lib, oracle, peak_seed, offset, strand, sample_seed):
+    """up_unit_synth_ex (replicate mode: shared centres, per-sample heights
+    and jitter, peak kinds, chunked Poisson background) == the oracle's
+    orc_synth_track_ex, tag totals and dense profile bit for bit"""
+    length, bw = 700_000, 50  # > 10 background chunks of 2^16 positions, a ragged last one
+    pos, cnt = oracle.synth_track_ex(sample_seed, 3, strand, True, length, bw, True, offset,
+                                     peak_seed)
+    with gpu_lib.Lib(0) as g:
+        g.set_params(bw, 1, 0.003)
+        u = g.add_unit(length)
+        g.synth(u, 0, 0, sample_seed, 3, strand, nondir=True, peaks=True, offset=offset,
+                peak_seed=peak_seed)
+        assert g.tag_total(u, 0, 0) == int(cnt.sum())
+        g.run()
+        f, _ = g.profile(u, length)
+    ref = oracle.profile(bw, 0.003, length, pos, cnt.reshape(-1, 1))
+    assert ref.tobytes() == f.tobytes()
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_shift_best_is_first_maximum_of_table(gpu_lib, seed):
     """up_shift_best == strand_shift.cpp:209-217 applied to up_shift_scan's

@@ -67,7 +67,7 @@ _lib = None
 EXPORTS = [
     "up_version", "up_track_bits", "up_strerror", "up_device_count", "up_kernel_weights", "up_open",
     "up_close", "up_set_params", "up_add_unit", "up_unit_count", "up_unit_pack",
-    "up_unit_scatter", "up_unit_synth", "up_unit_synth_offset", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
+    "up_unit_scatter", "up_unit_synth", "up_unit_synth_offset", "up_unit_synth_ex", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
     "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan", "up_shift_best",
     "up_timings", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
     "up_host_register", "up_unit_profile_range", "up_run_async", "up_run_wait", "up_set_timing",
@@ -105,6 +105,9 @@ def load_library(path=LIB_PATH):
                                     c.c_uint32, c.c_int32, c.c_int32, c.c_int32]),
         "up_unit_synth_offset": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.c_uint64,
                                            c.c_uint32, c.c_int32, c.c_int32, c.c_int32, c.c_int32]),
+        "up_unit_synth_ex": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16, c.c_uint64,
+                                       c.c_uint32, c.c_int32, c.c_int32, c.c_int32, c.c_int32,
+                                       c.c_uint64]),
         "up_unit_tag_total": (c.c_int, [vp, c.c_uint32, c.c_int32, c.c_uint16,
                                         c.POINTER(c.c_uint64)]),
         "up_unit_set_last_add": (c.c_int, [vp, c.c_uint32, c.c_uint32]),
@@ -227,8 +230,13 @@ class Lib:
                                    pos.ctypes.data, counts.ctypes.data))
 
     def synth(self, unit, strand, sample, seed, contig_index, synth_strand, nondir=False,
-              peaks=True, offset=0):
-        if offset:
+              peaks=True, offset=0, peak_seed=0):
+        """peak_seed != 0: replicate mode (shared peak centres)"""
+        if peak_seed:
+            _ck(self.L.up_unit_synth_ex(self.ctx, unit, strand, sample, seed, contig_index,
+                                        synth_strand, int(nondir), int(peaks), int(offset),
+                                        int(peak_seed)))
+        elif offset:
             _ck(self.L.up_unit_synth_offset(self.ctx, unit, strand, sample, seed, contig_index,
                                             synth_strand, int(nondir), int(peaks), int(offset)))
         else:

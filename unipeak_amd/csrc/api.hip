@@ -783,6 +783,17 @@ int up_unit_synth(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uin
 int up_unit_synth_offset(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uint64_t seed,
                          uint32_t contig_index, int32_t synth_strand, int32_t nondir,
                          int32_t with_peaks, int32_t offset) {
+    return up_unit_synth_ex(c, unit, strand, sample, seed, contig_index, synth_strand, nondir,
+                            with_peaks, offset, 0);
+}
+
+// peak_seed != 0: replicate mode -- the peak centres come from
+// peak_seed's keys, shared by every sample generated with it; each sample
+// draws its own height (tags per peak) and a centre jitter of -20..+20 bp
+// from its own seed, and its own tag offsets
+int up_unit_synth_ex(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, uint64_t seed,
+                     uint32_t contig_index, int32_t synth_strand, int32_t nondir,
+                     int32_t with_peaks, int32_t offset, uint64_t peak_seed) {
     if (offset < -32768 || offset > 32767) return UP_E_ARG;  // a short, like -s
     int r = check_track(c, unit, strand, sample);
     if (r) return r;
@@ -793,7 +804,8 @@ int up_unit_synth_offset(up_ctx *c, uint32_t unit, int32_t strand, uint16_t samp
     const uint64_t skey = hmix(seed);
     const uint64_t ckey = hmix(skey ^ (uint64_t)(contig_index + 1));
     const uint64_t tkey = hmix(ckey ^ (uint64_t)(0x100 + synth_strand));
-    const uint64_t pkey = hmix(ckey ^ (uint64_t)(0x200 + (nondir ? 0 : synth_strand)));
+    const uint64_t pckey = peak_seed ? hmix(hmix(peak_seed) ^ (uint64_t)(contig_index + 1)) : ckey;
+    const uint64_t pkey = hmix(pckey ^ (uint64_t)(0x200 + (nondir ? 0 : synth_strand)));
     const int64_t lo = 2 * (int64_t)bw + 2, hi = (int64_t)len - 2 * (int64_t)bw - 1;
     if (hi < lo) return UP_OK;
     SynthThr thr;
@@ -810,8 +822,26 @@ int up_unit_synth_offset(up_ctx *c, uint32_t unit, int32_t strand, uint16_t samp
     uint32_t *trk = c->d_stage.p;  // dense uint32 staging, packed below
     HIPCHK(hipMemsetAsync(trk, 0, (size_t)len * sizeof(uint32_t), c->stream));
     const uint64_t npos = (uint64_t)(hi - lo + 1);
-    hipLaunchKernelGGL(synth_bg_kernel, dim3((unsigned)((npos + 255) / 256)), dim3(256), 0,
-                       c->stream, trk, tkey, lo, hi, thr, (int64_t)offset, (int64_t)len);
+    uint64_t *d_tab = nullptr;
+    uint64_t tab[1024];  // host source of an async copy: lives until the sync below
+    if (!peak_seed) {
+        hipLaunchKernelGGL(synth_bg_kernel, dim3((unsigned)((npos + 255) / 256)), dim3(256), 0,
+                           c->stream, trk, tkey, lo, hi, thr, (int64_t)offset, (int64_t)len);
+    } else {
+        // replicate mode: chunked Poisson background (synth_bgc_kernel)
+        const double mu = 0.002925 * 65536.0;
+        double pr = std::exp(-mu), cdf = pr;
+        for (int k = 0; k < 1024; ++k) {
+            tab[k] = cdf >= 1.0 ? ~0ull : (uint64_t)(cdf * 18446744073709551616.0);
+            pr *= mu / (double)(k + 1);
+            cdf += pr;
+        }
+        HIPCHK(hipMalloc(&d_tab, sizeof tab));
+        HIPCHK(hipMemcpyAsync(d_tab, tab, sizeof tab, hipMemcpyHostToDevice, c->stream));
+        const uint32_t nch = (uint32_t)((npos + 65535) >> 16);
+        hipLaunchKernelGGL(synth_bgc_kernel, dim3((nch + 255) / 256), dim3(256), 0, c->stream, trk,
+                           tkey, lo, hi, d_tab, (int64_t)offset, (int64_t)len, nch);
+    }
     HIPCHK(hipGetLastError());
     if (with_peaks) {
         std::vector<uint32_t> tags;
@@ -823,13 +853,24 @@ int up_unit_synth_offset(up_ctx *c, uint32_t unit, int32_t strand, uint16_t samp
         const int64_t shift = (nondir && synth_strand == 1) ? 150 : 0;
         for (uint32_t j = 0; chi >= clo && j < npk; ++j) {
             const uint64_t h = hmix(pkey ^ hmix(0x7065616B00000000ull + j));
-            const int64_t centre = clo + (int64_t)(h % (uint64_t)(chi - clo + 1));
-            const uint32_t n = 20u + (uint32_t)(hmix(h) % 180u);
+            int64_t centre = clo + (int64_t)(h % (uint64_t)(chi - clo + 1));
+            uint32_t n = 20u + (uint32_t)(hmix(h) % 180u);
+            // replicate mode: the shared hash also picks the peak's kind --
+            // 0/1 an artifact on strand 0/1 only, 2 a spike (every tag of every
+            // sample at the shared centre), 3 a weak peak (2..11 tags per sample), else normal
+            const uint32_t kind = peak_seed ? (uint32_t)(h >> 56) & 15u : 4u;
+            if (peak_seed) {
+                const uint64_t hs = hmix(h ^ skey);
+                n = 20u + (uint32_t)(hs % 180u);
+                if (kind != 2) centre += (int64_t)((hs >> 32) % 41u) - 20;
+                if (kind == 3) n = 2u + (uint32_t)(hs % 10u);
+                if (kind <= 1 && (uint32_t)synth_strand != kind) n = 0;
+            }
             for (uint32_t i = 0; i < n; ++i) {
                 int64_t s = 0;
                 const uint64_t b = hmix(tkey ^ h ^ hmix(0x74616700000000ull + i));
                 for (int m = 0; m < 12; ++m) s += (int64_t)(hmix(b + (uint64_t)m) >> 32);
-                const int64_t off = (60 * (s - 6 * 4294967296ll) + 2147483648ll) >> 32;
+                const int64_t off = kind == 2 ? 0 : (60 * (s - 6 * 4294967296ll) + 2147483648ll) >> 32;
                 const int64_t p = centre + shift + off;
                 // generated on [lo, hi]; the -s offset then moves it, and the
                 // wiggle reader's bounds drop what leaves [1, len]
@@ -847,6 +888,10 @@ int up_unit_synth_offset(up_ctx *c, uint32_t unit, int32_t strand, uint16_t samp
             HIPCHK(hipStreamSynchronize(c->stream));
             HIPCHK(hipFree(d));
         }
+    }
+    if (d_tab) {
+        HIPCHK(hipStreamSynchronize(c->stream));  // the table is read by synth_bgc_kernel
+        HIPCHK(hipFree(d_tab));
     }
     if ((r = pack_track(c, unit, strand, sample, trk))) return r;
     c->ran = false;

@@ -2426,6 +2426,31 @@ __global__ void synth_bg_kernel(uint32_t *stage, uint64_t tkey, int64_t lo, int6
     stage[x + offset - 1] = c;
 }
 
+// replicate mode's background (peak_seed != 0): the same
+// Poisson(λ) per position, drawn sparsely -- chunk c = positions
+// [lo + c·2^16, lo + (c+1)·2^16) gets n ~ Poisson(λ·2^16) tags (n = #{k :
+// tab[k] <= u0}, tab the 1024 CDF thresholds) at uniform positions (the top 16
+// bits of a hash per tag); tags past hi are dropped.  One thread per chunk.
+__global__ void synth_bgc_kernel(uint32_t *stage, uint64_t tkey, int64_t lo, int64_t hi,
+                                 const uint64_t *__restrict__ tab, int64_t offset, int64_t len,
+                                 uint32_t nchunks) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
+    const uint64_t u0 = mix64(tkey ^ mix64(0x6267000000000000ull + c));
+    uint32_t a = 0, b = 1024;
+    while (a < b) {
+        const uint32_t m = (a + b) >> 1;
+        if (tab[m] <= u0) a = m + 1;
+        else b = m;
+    }
+    const int64_t base = lo + ((int64_t)c << 16);
+    for (uint32_t i = 0; i < a; ++i) {
+        const int64_t x = base + (int64_t)(mix64(u0 ^ mix64((uint64_t)i + 1)) >> 48);
+        if (x > hi || x + offset < 1 || x + offset > len) continue;
+        atomicAdd(&stage[x + offset - 1], 1u);
+    }
+}
+
 // sum of a track's counts, escapes excluded (their counts are added on the
 // host from the overflow table)
 __global__ void track_sum_kernel(const uint8_t *__restrict__ t, uint64_t n, unsigned long long *out) {
