@@ -164,6 +164,17 @@ __device__ __forceinline__ uint32_t ovf_lookup(const UnitDesc &U, uint32_t track
     return (lo < end && (uint32_t)(e[lo] >> 32) == pos) ? (uint32_t)e[lo] : kEsc;
 }
 
+// the K1a screen's bound of an escaped field at position pos: its count when
+// below 255 (the escape tile's byte: two dependent loads), else 255 (the
+// caller then treats the chunk as unbounded, kBig)
+__device__ __forceinline__ uint32_t esc_bound(const UnitDesc &U, uint32_t track, int64_t pos) {
+    if (!U.ovf_tidx || (uint64_t)(pos - 1) >= (uint64_t)U.len) return 255u;
+    const uint32_t ti = ((const uint32_t *)U.ovf_tidx)[(size_t)track * ovf_nblk(U.len) +
+                                                         ((uint32_t)(pos - 1) >> kOvfBlkShift)];
+    if (ti == kNoTile) return 255u;
+    return ((const uint8_t *)U.ovf_tiles)[(size_t)ti * kOvfBlk + ((uint32_t)(pos - 1) & (kOvfBlk - 1u))];
+}
+
 // escapes of N words (lane's position x0 + 64w + lane in word w): each lane
 // resolves its own escaped words, one lookup per round, so the rounds are the
 // most escapes any lane holds rather than the words with an escape anywhere
@@ -952,36 +963,57 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 mchunk = 0;
                 exact_blocks = 0;
             } else {
-            // A chunk holding an escaped field (4-bit: a count >= 8, the
-            // escape among them), whose true count the screen does not know,
-            // goes exact (kBig).  Rare: the strip is re-read (L2) for the
-            // per-chunk bits only when some lane saw such a field.
+            // A chunk holding an escaped field: with 2-bit tracks the field
+            // counted as kEsc in the chunk sum is replaced by the position's
+            // count from its escape tile (exact below 255; a count >= 255
+            // makes the chunk unbounded, kBig) -- with several pooled samples
+            // every sample's own peaks hold escapes, and sending all of them
+            // exact made K1b several times longer.  (4-bit tracks: any count
+            // >= 8 goes exact.)  Only strips where some lane saw an escape
+            // re-read their bytes (L2) for the per-field positions.
             if (__ballot((anybig & kBigMask) != 0u) != 0) {
                 for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
                     for (int k = 0; k < P.nnc; ++k) {
+                        const uint32_t trk = (uint32_t)(st * S + ncs[k]);
+                        const uint32_t w = POOL == 2 ? cptr(P.wscreen)[k] : 1u;
                         gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, ncs[k]) + fbyte(kPadPos + p0 - 1));
-#pragma unroll 2
+                        // field f of dword j of the 16 bytes at strip byte B:
+                        // position p0 + kPerByte * (B + 4 j) + f
+                        auto chunk_fix = [&](const uint32_t (&d)[4], int i, int64_t B, uint32_t &sum) -> uint32_t {
+                            uint32_t b = 0;
+#pragma unroll
+                            for (int j = 0; j < DPC; ++j) {
+                                if constexpr (kTB == 2) {
+                                    uint32_t e = fbig32(d[DPC * i + j]);
+                                    while (e) {
+                                        const int f = __builtin_ctz(e) >> 1;
+                                        e &= e - 1;
+                                        const uint32_t v =
+                                            esc_bound(U, trk, p0 + kPerByte * (B + 4 * (DPC * i + j)) + f);
+                                        if (v >= 255u) b = 1;
+                                        else sum += (v - kEsc) * w;
+                                    }
+                                } else {
+                                    b |= fbig32(d[DPC * i + j]);
+                                }
+                            }
+                            return b;
+                        };
+#pragma unroll 1
                         for (int q = 0; q < kLoads; ++q) {
                             const u32x4 x = t[64 * q + lane];
                             const uint32_t d[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-                            for (int i = 0; i < CPL; ++i) {
-                                uint32_t b = 0;
-#pragma unroll
-                                for (int j = 0; j < DPC; ++j) b |= fbig32(d[DPC * i + j]);
-                                big |= (b ? 1u : 0u) << (CPL * q + i);
-                            }
+                            for (int i = 0; i < CPL; ++i)
+                                big |= (chunk_fix(d, i, 16 * (64 * q + lane), cs[CPL * q + i]) ? 1u : 0u)
+                                       << (CPL * q + i);
                         }
                         if (lane < 2 * HL) {
-                            const u32x4 x = t[lane < HL ? lane - HL : kLoads * kWave + lane - HL];
+                            const int hl = lane < HL ? lane - HL : kLoads * kWave + lane - HL;
+                            const u32x4 x = t[hl];
                             const uint32_t d[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-                            for (int i = 0; i < CPL; ++i) {
-                                uint32_t b = 0;
-#pragma unroll
-                                for (int j = 0; j < DPC; ++j) b |= fbig32(d[DPC * i + j]);
-                                hbig |= (b ? 1u : 0u) << i;
-                            }
+                            for (int i = 0; i < CPL; ++i) hbig |= (chunk_fix(d, i, 16 * hl, hs[i]) ? 1u : 0u) << i;
                         }
                     }
                 }
