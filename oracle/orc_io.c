@@ -15,6 +15,7 @@
  * sets it), so the reference's first merge step is undefined behaviour.  We
  * restate the intended two-handle merge (as if `forward` started true).
  */
+#define _GNU_SOURCE 1 /* fopencookie */
 #include "orc.h"
 
 #include <ctype.h>
@@ -24,6 +25,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <zlib.h>
 
 /* ---------------------------------------------------------------------- */
 /* small utilities                                                         */
@@ -167,6 +169,41 @@ static uint32_t ctab_find(const ctab *t, const char *name, size_t len) {
     return t->n;
 }
 
+/* misc/filterstream.cpp:30-50, 86-104: a name ending in GZIP_SUFFIX ".gz"
+ * (misc/defaults.hpp:26) is read / written through boost's gzip filters --
+ * here zlib behind a stdio cookie; BZIP2_SUFFIX ".bz2" takes bzip2 filters,
+ * refused in this image (no libbz2 headers) with an error exit. */
+static int ends_with(const char *s, const char *suf) {
+    const size_t n = strlen(s), m = strlen(suf);
+    return n >= m && strcmp(s + n - m, suf) == 0;
+}
+static ssize_t gzc_read(void *c, char *buf, size_t n) {
+    const int r = gzread((gzFile)c, buf, (unsigned)(n < (1u << 30) ? n : (1u << 30)));
+    if (r < 0) fail("error: gzip stream error\n\n");
+    return r;
+}
+static ssize_t gzc_write(void *c, const char *buf, size_t n) {
+    size_t done = 0;
+    while (done < n) {
+        const size_t k = n - done < (1u << 30) ? n - done : (1u << 30);
+        const int w = gzwrite((gzFile)c, buf + done, (unsigned)k);
+        if (w <= 0) return done ? (ssize_t)done : -1;
+        done += (size_t)w;
+    }
+    return (ssize_t)done;
+}
+static int gzc_close(void *c) { return gzclose((gzFile)c) == Z_OK ? 0 : EOF; }
+static FILE *filter_open(const char *fname, int write) {
+    if (ends_with(fname, ".bz2"))
+        fail("error: could not %s %s: bzip2 (.bz2) streams are not supported by this build "
+             "(libbz2 headers absent)\n", write ? "write" : "read", fname);
+    if (!ends_with(fname, ".gz")) return fopen(fname, write ? "wb" : "rb");
+    gzFile g = gzopen(fname, write ? "wb" : "rb");
+    if (!g) return NULL;
+    cookie_io_functions_t io = {write ? NULL : gzc_read, write ? gzc_write : NULL, NULL, gzc_close};
+    return fopencookie(g, write ? "w" : "r", io);
+}
+
 /* line reader with std::getline/istream::good() semantics */
 typedef struct {
     FILE *fp;
@@ -183,7 +220,7 @@ static void in_open(instream *s, const char *fname) {
         s->fp = stdin;
         s->fname = xstrdup("standard input stream");
     } else {
-        s->fp = fopen(fname, "rb");
+        s->fp = filter_open(fname, 0);
         if (!s->fp) fail("error: could not read %s\n\n", fname);
         s->fname = xstrdup(fname);
     }
@@ -735,7 +772,7 @@ static void write_region(region_writer *w, const orc_region *g, uint16_t n_expt)
 
 static FILE *open_out(const char *fname) {
     if (strcmp(fname, "stdout") == 0) return stdout;
-    FILE *fp = fopen(fname, "wb");
+    FILE *fp = filter_open(fname, 1);
     if (!fp) fail("error: could not write %s\n\n", fname);
     return fp;
 }

@@ -16,6 +16,7 @@
 #include "cli.hpp"
 #include "unipeak_hip.h"
 #include "wigio.hpp"
+#include "gzio.hpp"
 
 using namespace unipeak;
 
@@ -196,7 +197,7 @@ int main(int argc, char **argv) {
             });
         for (auto &th : pool) th.join();
     }
-    FILE *out = out_name == "stdout" ? stdout : std::fopen(out_name.c_str(), "wb");
+    FILE *out = out_name == "stdout" ? stdout : open_output(out_name);
     if (!out) {
         std::cerr << "error: could not write " << out_name << std::endl << std::endl;
         return 1;

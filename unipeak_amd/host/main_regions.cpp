@@ -12,6 +12,7 @@
 #include "cli.hpp"
 #include "engine.hpp"
 #include "wigio.hpp"
+#include "gzio.hpp"
 
 using namespace unipeak;
 
@@ -180,7 +181,7 @@ int main(int argc, char **argv) {
     h << "# background=" << background << "\n";
     ProfileSink prof;
     if (!profile.empty()) {  // regions.cpp:276-284: header first, profile as positions retire
-        prof.fp = profile == "stdout" ? stdout : std::fopen(profile.c_str(), "wb");
+        prof.fp = profile == "stdout" ? stdout : open_output(profile);
         if (!prof.fp) { std::cerr << "error: could not write " << profile << std::endl << std::endl; exit_now(1); }
         std::setvbuf(prof.fp, nullptr, _IOFBF, 1 << 22);
         prof.ct = &ct;
@@ -257,7 +258,7 @@ int main(int argc, char **argv) {
         row += "\n";
         table += row;
     }
-    FILE *out = out_name == "stdout" ? stdout : std::fopen(out_name.c_str(), "wb");
+    FILE *out = out_name == "stdout" ? stdout : open_output(out_name);
     if (!out) { std::cerr << "error: could not write " << out_name << std::endl << std::endl; exit_now(1); }
     std::fwrite(table.data(), 1, table.size(), out);
     if (out != stdout) std::fclose(out); else std::fflush(stdout);

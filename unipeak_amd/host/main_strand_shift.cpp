@@ -12,6 +12,7 @@
 #include "cli.hpp"
 #include "engine.hpp"
 #include "wigio.hpp"
+#include "gzio.hpp"
 
 using namespace unipeak;
 
@@ -180,7 +181,7 @@ int main(int argc, char **argv) {
         o += "shift\tregions\n";
         for (size_t i = 0; i < W; ++i)
             if (freq[i]) o += fmt_lexical((double)i) + "\t" + fmt_lexical((double)freq[i]) + "\n";
-        FILE *out = out_name == "stdout" ? stdout : std::fopen(out_name.c_str(), "wb");
+        FILE *out = out_name == "stdout" ? stdout : open_output(out_name);
         if (!out) { std::cerr << "error: could not write " << out_name << std::endl << std::endl; exit_now(1); }
         std::fwrite(o.data(), 1, o.size(), out);
         if (out != stdout) std::fclose(out); else std::fflush(stdout);

@@ -22,6 +22,7 @@
 #include "cli.hpp"
 #include "unipeak_hip.h"
 #include "wigio.hpp"
+#include "gzio.hpp"
 
 using namespace unipeak;
 
@@ -327,7 +328,7 @@ int main(int argc, char **argv) {
         for (size_t i = 0; i < S; ++i) o += "\t" + fmt_lexical(hits[r * S + i]);
         o += "\n";
     }
-    FILE *out = out_name == "stdout" ? stdout : std::fopen(out_name.c_str(), "wb");
+    FILE *out = out_name == "stdout" ? stdout : open_output(out_name);
     if (!out) { std::cerr << "error: could not write " << out_name << std::endl << std::endl; return 1; }
     std::fwrite(o.data(), 1, o.size(), out);
     if (out != stdout) std::fclose(out); else std::fflush(stdout);

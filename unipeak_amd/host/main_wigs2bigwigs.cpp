@@ -256,6 +256,10 @@ std::string strip_re(const std::string &s, const std::string &suffix) {
 }
 
 bool read_lines(const std::string &path, std::vector<std::string> &out) {
+    // the Perl script pipes *.bz2 through bunzip2; libbz2 is not in this image
+    if (path.size() > 4 && path.compare(path.size() - 4, 4, ".bz2") == 0)
+        die("error: " + path + ": bzip2 (.bz2) input is not supported by this build; "
+            "decompress it first (bunzip2)\n");
     if (path.size() > 3 && path.compare(path.size() - 3, 3, ".gz") == 0) {
         gzFile g = gzopen(path.c_str(), "rb");
         if (!g) return false;

@@ -1,5 +1,6 @@
 // unipeak_amd/host/wigio.cpp -- see wigio.hpp.
 #include "wigio.hpp"
+#include "gzio.hpp"
 
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -144,11 +145,10 @@ static bool lex_data(const char *p, const char *e, uint32_t *pos, uint32_t *cnt)
 }
 
 LexedFile::~LexedFile() {
-    if (base_ && size_) munmap((void *)base_, size_);
+    if (base_ && size_ && base_ != inflated_.data()) munmap((void *)base_, size_);
 }
 
 void LexedFile::lex(const std::string &fname, int fd, uint64_t size) {
-    (void)fname;
     size_ = size;
     if (size_) {
         void *m = mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd, 0);
@@ -156,6 +156,10 @@ void LexedFile::lex(const std::string &fname, int fd, uint64_t size) {
         madvise(m, size_, MADV_SEQUENTIAL);
         base_ = (const char *)m;
     }
+    lex_bytes();
+}
+
+void LexedFile::lex_bytes() {
     // newline-aligned chunk boundaries
     const unsigned T = ingest_threads();
     uint64_t chunk_bytes = 1u << 20;  // UNIPEAK_LEX_CHUNK: tests force many small chunks
@@ -229,6 +233,16 @@ std::shared_ptr<const LexedFile> LexedFile::open(const std::string &fname) {
     static std::unordered_map<std::string, std::weak_ptr<const LexedFile>> cache;
     std::lock_guard<std::mutex> lock(mu);
     if (auto sp = cache[fname].lock()) return sp;
+    if (is_bz2(fname)) return nullptr;  // LineReader refuses it (gzio.cpp)
+    if (is_gz(fname)) {
+        std::shared_ptr<LexedFile> f(new LexedFile());
+        if (!inflate_file(fname, f->inflated_)) return nullptr;
+        f->size_ = f->inflated_.size();
+        f->base_ = f->inflated_.data();
+        f->lex_bytes();
+        cache[fname] = f;
+        return f;
+    }
     const int fd = ::open(fname.c_str(), O_RDONLY);
     if (fd < 0) return nullptr;
     struct stat st;
@@ -254,7 +268,7 @@ LineReader::LineReader(const std::string &fname, bool lexed) {
         const char *nl = std::getenv("UNIPEAK_NO_LEX");  // tests: the plain getline reader
         if (lexed && !(nl && *nl && *nl != '0')) lexed_ = LexedFile::open(fname);
         if (!lexed_) {
-            fp_ = std::fopen(fname.c_str(), "rb");
+            fp_ = open_input(fname);  // ".gz" through zlib, ".bz2" refused (gzio.hpp)
             if (!fp_) {
                 std::cerr << "error: could not read " << fname << std::endl << std::endl;
                 exit_now(1);

@@ -51,7 +51,8 @@ class ContigTable {
 // A file split into the lines std::getline would return -- count('\n') + 1
 // of them, the last one (possibly empty) reaching end-of-file -- and lexed
 // by a thread pool over newline-aligned chunks of the memory-mapped file
-// (SURVEY.md 8(f) #1).  Lines of the canonical data form
+// (a ".gz" file is inflated into memory first, gzio.hpp).
+// Lines of the canonical data form
 // "<digits>< |\t>[-]<digits>" with both values < 2^32 are stored as two
 // integers; every other line (track/variableStep headers, comments, anything
 // unusual) keeps its text for the exact serial parser, so the lexed path
@@ -76,8 +77,10 @@ class LexedFile {
   private:
     LexedFile() = default;
     void lex(const std::string &fname, int fd, uint64_t size);
+    void lex_bytes();
     const char *base_ = nullptr;
     uint64_t size_ = 0, lines_ = 0;
+    std::string inflated_;  // a ".gz" file's decompressed bytes (base_ points here)
     std::vector<Chunk> chunks_;
 };
 
