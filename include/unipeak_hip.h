@@ -160,10 +160,10 @@ int up_reset_units(up_ctx *ctx);
 
 /* Run K1..K3 over every unit (stream-ordered, blocking).  Configurations
  * the parallel scan does not represent -- region threshold <= 0 (the leap
- * branch of processPosition is live, quirk Q11) or bw > 127 -- run the exact
- * state machine over every unit instead (K0 replay, sequential per buffer:
- * exact, slow); up_run_async and up_unit_profile* refuse them
- * (UP_E_UNSUPPORTED).  up_shift_scan correlates a replayed region's stored
+ * branch of processPosition is live, quirk Q11) or bw > 255 (kMaxBw: K1's
+ * halo of NH <= 4 words) -- run the exact state machine over every unit
+ * instead (K0 replay, sequential per buffer: exact, slow); up_run_async and
+ * up_unit_profile* refuse them (UP_E_UNSUPPORTED).  up_shift_scan correlates a replayed region's stored
  * scores (Region::scores), as strandCorr does. */
 int up_run(up_ctx *ctx, uint64_t *n_regions);
 /* Pipelined form of up_run: up_run_async enqueues one pass and returns
@@ -221,7 +221,8 @@ int up_shift_best(up_ctx *ctx, const uint64_t *region_idx, size_t n,
 
 /* device-side timings of the last up_run in ms: [0]=K1 scan, [1]=K2
  * segment, [2]=K3 stats, [3]=whole up_run wall, [4]=K1 launches */
-/* achievable HBM rate: device-to-device copy of `bytes` (best of reps),
+/* achievable HBM rate: a float4 streaming copy kernel of `bytes` (a multiple
+ * of 16; best of reps),
  * GB/s counting read + write (the bench's copy-rate reference) */
 int up_hbm_copy_gbps(up_ctx *ctx, uint64_t bytes, int reps, double *gbps);
 int up_timings(up_ctx *ctx, double *ms, int n);

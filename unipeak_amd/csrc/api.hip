@@ -2150,7 +2150,7 @@ int up_unit_profile(up_ctx *c, uint32_t unit, double *out_f, double *out_r, uint
 // Achievable HBM rate on this device: device-to-device copy of `bytes`
 // (read + write), best of `reps`, reported as (2 * bytes) / time.
 int up_hbm_copy_gbps(up_ctx *c, uint64_t bytes, int reps, double *gbps) {
-    if (!c || !gbps || bytes == 0 || reps < 1) return UP_E_ARG;
+    if (!c || !gbps || bytes < 16 || bytes % 16 || reps < 1) return UP_E_ARG;
     HIPCHK(hipSetDevice(c->dev));
     void *a = nullptr, *b = nullptr;
     HIPCHK(hipMalloc(&a, bytes));
@@ -2162,7 +2162,8 @@ int up_hbm_copy_gbps(up_ctx *c, uint64_t bytes, int reps, double *gbps) {
     float best = 0;
     for (int i = 0; i <= reps; ++i) {
         HIPCHK(hipEventRecord(c->ev[5], c->stream));
-        HIPCHK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, c->stream));
+        hipLaunchKernelGGL(hbm_copy_kernel, dim3(256 * 16), dim3(256), 0, c->stream, (const u32x4 *)a,
+                           (u32x4 *)b, (uint64_t)(bytes / 16));
         HIPCHK(hipEventRecord(c->ev[6], c->stream));
         HIPCHK(hipEventSynchronize(c->ev[6]));
         float ms = 0;

@@ -53,7 +53,12 @@ __device__ __forceinline__ uint4 load4(const uint32_t *tracks, uint64_t genome, 
     if (v + 4 <= view_n && (v & 3) == 0) {
         a = *reinterpret_cast<const uint4 *>(tracks + v);
         if (nondir) {
-            const uint4 b = *reinterpret_cast<const uint4 *>(tracks + genome + v);
+            // the reverse half starts at `genome`: 16-byte aligned only when
+            // genome % 4 == 0, else four dword loads
+            const uint32_t *r = tracks + genome + v;
+            uint4 b;
+            if ((genome & 3) == 0) b = *reinterpret_cast<const uint4 *>(r);
+            else b = make_uint4(r[0], r[1], r[2], r[3]);
             a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
         }
     } else {

@@ -1810,7 +1810,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 counted = true;
             }
         }
-        if constexpr (POOL != 2) {
+        // (2-bit tracks only: a 64-position block spans at most 32 bytes
+        // from its 16-byte-aligned base only at 4 positions per byte; the
+        // 4-bit A/B build takes the per-sample path)
+        static_assert(kTB == 2 || kTB == 4, "track layout");
+        if constexpr (POOL != 2 && kTB == 2) {
             // several samples (and at most 32 (strand, sample) tracks): each
             // 64-position block's bytes of every track come with one wave
             // load (lane l: track l/2, 16-byte piece l%2 of the 32 bytes
@@ -2481,6 +2485,25 @@ __global__ void synth_bgc_kernel(uint32_t *stage, uint64_t tkey, int64_t lo, int
         if (x > hi || x + offset < 1 || x + offset > len) continue;
         atomicAdd(&stage[x + offset - 1], 1u);
     }
+}
+
+// the bench's achievable-HBM reference: a float4 (16 B per lane) streaming
+// copy, four loads in flight per lane before their stores (the guide's
+// measured ceiling is a float4 copy, ~6.3 TB/s)
+__global__ void __launch_bounds__(256) hbm_copy_kernel(const u32x4 *__restrict__ a, u32x4 *__restrict__ b,
+                                                       uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const u32x4 x0 = __builtin_nontemporal_load(a + i), x1 = __builtin_nontemporal_load(a + i + stride);
+        const u32x4 x2 = __builtin_nontemporal_load(a + i + 2 * stride);
+        const u32x4 x3 = __builtin_nontemporal_load(a + i + 3 * stride);
+        __builtin_nontemporal_store(x0, b + i);
+        __builtin_nontemporal_store(x1, b + i + stride);
+        __builtin_nontemporal_store(x2, b + i + 2 * stride);
+        __builtin_nontemporal_store(x3, b + i + 3 * stride);
+    }
+    for (; i < n; i += stride) b[i] = a[i];
 }
 
 // sum of a track's counts, escapes excluded (their counts are added on the

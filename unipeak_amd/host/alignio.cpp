@@ -36,15 +36,18 @@ double BinomPosterior::prob(uint16_t mismatches, const std::vector<uint32_t> &hi
 }
 
 // ---------------------------------------------------------------------------
-// BAM through BGZF (what misc/bamtools/BamReader.cpp:561-700 reads): the
-// whole file is inflated member by member, then records are cut from it
+// BAM through BGZF (what misc/bamtools/BamReader.cpp:561-700 reads): BGZF
+// blocks are gzip members, inflated one after another into a sliding window
+// that holds the current record (a few MB whatever the file size, as the
+// reference's BamReader holds one block at a time)
 // ---------------------------------------------------------------------------
 class BamFile {
   public:
+    ~BamFile();
     bool open(const std::string &fname);
     // next record; false at the end (or a truncated record)
     bool next();
-    // fields of the current record
+    // fields of the current record (valid until the next call)
     int32_t ref_id = 0, pos = 0, l_seq = 0;
     uint16_t flag = 0;
     uint8_t mapq = 0;
@@ -54,64 +57,97 @@ class BamFile {
     bool nm(uint32_t *out) const;  // BamAlignment::GetTag("NM", int32&)
 
   private:
+    bool need(size_t n);  // n inflated bytes at at_; false if the stream ends first
+    bool inflate_more();
+    FILE *fp_ = nullptr;
+    z_stream zs_;
+    bool zinit_ = false, zdone_ = false, raw_eof_ = false;
+    std::vector<uint8_t> raw_;
+    size_t raw_at_ = 0;
     std::vector<uint8_t> data_;
     size_t at_ = 0;
 };
 
 static uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
 
+BamFile::~BamFile() {
+    if (zinit_) inflateEnd(&zs_);
+    if (fp_) std::fclose(fp_);
+}
+
+// one inflate step of at most 1 MiB; false once nothing more will come (end
+// of input, a truncated member or bytes that are not gzip: what inflated
+// before stays readable, as the whole-file reader behaved)
+bool BamFile::inflate_more() {
+    if (zdone_) return false;
+    if (raw_at_ == raw_.size() && !raw_eof_) {
+        raw_.resize(1u << 20);
+        const size_t k = std::fread(raw_.data(), 1, raw_.size(), fp_);
+        raw_.resize(k);
+        raw_at_ = 0;
+        if (k == 0) raw_eof_ = true;
+    }
+    if (raw_at_ == raw_.size()) {  // input exhausted
+        zdone_ = true;
+        return false;
+    }
+    if (at_ > (8u << 20) && at_ * 2 > data_.size()) {  // slide the window
+        data_.erase(data_.begin(), data_.begin() + (std::ptrdiff_t)at_);
+        at_ = 0;
+    }
+    zs_.next_in = raw_.data() + raw_at_;
+    zs_.avail_in = (uInt)(raw_.size() - raw_at_);
+    const size_t old = data_.size(), room = 1u << 20;
+    data_.resize(old + room);
+    zs_.next_out = data_.data() + old;
+    zs_.avail_out = (uInt)room;
+    const int rc = inflate(&zs_, Z_NO_FLUSH);
+    data_.resize(old + room - zs_.avail_out);
+    raw_at_ = (size_t)(zs_.next_in - raw_.data());
+    if (rc == Z_STREAM_END) {
+        inflateReset(&zs_);  // the next BGZF block
+    } else if (rc == Z_BUF_ERROR || (rc == Z_OK && zs_.avail_in == 0)) {
+        if (raw_at_ == raw_.size() && raw_eof_) zdone_ = true;  // truncated member
+    } else if (rc != Z_OK) {
+        zdone_ = true;  // not gzip / corrupt
+    }
+    return true;
+}
+
+bool BamFile::need(size_t n) {
+    while (data_.size() - at_ < n)
+        if (!inflate_more() && data_.size() - at_ < n) return false;
+    return true;
+}
+
 bool BamFile::open(const std::string &fname) {
-    FILE *fp = std::fopen(fname.c_str(), "rb");
-    if (!fp) return false;
-    std::vector<uint8_t> raw;
-    uint8_t buf[1 << 16];
-    for (size_t k; (k = std::fread(buf, 1, sizeof buf, fp)) > 0;) raw.insert(raw.end(), buf, buf + k);
-    std::fclose(fp);
-    // every BGZF block is a gzip member
-    z_stream zs;
-    std::memset(&zs, 0, sizeof zs);
-    if (inflateInit2(&zs, 15 + 16) != Z_OK) return false;
-    size_t in = 0;
-    std::vector<uint8_t> out(1 << 20);
-    while (in < raw.size()) {
-        zs.next_in = raw.data() + in;
-        zs.avail_in = (uInt)std::min<size_t>(raw.size() - in, 1u << 30);
-        int rc;
-        do {
-            zs.next_out = out.data();
-            zs.avail_out = (uInt)out.size();
-            rc = inflate(&zs, Z_NO_FLUSH);
-            data_.insert(data_.end(), out.data(), out.data() + (out.size() - zs.avail_out));
-        } while (rc == Z_OK && zs.avail_in > 0);
-        in = (size_t)(zs.next_in - raw.data());
-        if (rc != Z_STREAM_END) break;  // truncated or not gzip: keep what inflated
-        inflateReset(&zs);
-    }
-    inflateEnd(&zs);
+    fp_ = std::fopen(fname.c_str(), "rb");
+    if (!fp_) return false;
+    std::memset(&zs_, 0, sizeof zs_);
+    if (inflateInit2(&zs_, 15 + 16) != Z_OK) return false;
+    zinit_ = true;
     // header: magic, text, references
-    if (data_.size() < 12 || std::memcmp(data_.data(), "BAM\1", 4) != 0) return false;
-    size_t p = 4;
-    const uint32_t l_text = le32(&data_[p]);
-    p += 4 + l_text;
-    if (p + 4 > data_.size()) return false;
-    const uint32_t n_ref = le32(&data_[p]);
-    p += 4;
+    if (!need(12) || std::memcmp(data_.data() + at_, "BAM\1", 4) != 0) return false;
+    at_ += 4;
+    const uint32_t l_text = le32(&data_[at_]);
+    if (!need(4 + (size_t)l_text + 4)) return false;
+    at_ += 4 + l_text;
+    const uint32_t n_ref = le32(&data_[at_]);
+    at_ += 4;
     for (uint32_t i = 0; i < n_ref; ++i) {
-        if (p + 4 > data_.size()) return false;
-        const uint32_t l_name = le32(&data_[p]);
-        p += 4;
-        if (p + l_name + 4 > data_.size()) return false;
-        ref_names.emplace_back((const char *)&data_[p], l_name ? l_name - 1 : 0);  // NUL-terminated
-        p += l_name + 4;
+        if (!need(4)) return false;
+        const uint32_t l_name = le32(&data_[at_]);
+        if (!need(4 + (size_t)l_name + 4)) return false;
+        ref_names.emplace_back((const char *)&data_[at_ + 4], l_name ? l_name - 1 : 0);  // NUL-terminated
+        at_ += 4 + l_name + 4;
     }
-    at_ = p;
     return true;
 }
 
 bool BamFile::next() {
-    if (at_ + 4 > data_.size()) return false;
+    if (!need(4)) return false;
     const uint32_t block = le32(&data_[at_]);
-    if (block == 0 || block < 32 || at_ + 4 + block > data_.size()) return false;
+    if (block == 0 || block < 32 || !need(4 + (size_t)block)) return false;
     const uint8_t *r = &data_[at_ + 4];
     ref_id = (int32_t)le32(r);
     pos = (int32_t)le32(r + 4);

@@ -223,6 +223,8 @@ int main(int argc, char **argv) {
     for (const Records &x : rec) all_complete = all_complete && x.complete;
     if (!row_error.empty() && all_complete) {  // no stream can fail before that row
         warm.join();
+        for (up_tir *h : dev)
+            if (h) up_tir_close(h);
         std::cerr << row_error;
         return 1;
     }
