@@ -428,6 +428,14 @@ def main():
     if comm is not None:
         comm.torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    dump = os.environ.get("UNIPEAK_BENCH_DUMP")
+    if final is not None and dump:  # rehearsals: the merged records of the last step
+        blocks, _, _ = border.blocks(final[1])
+        recs = [b.copy() for _, b, _ in blocks]
+        for (g, _, _), r in zip(blocks, recs):
+            r["unit"] = g  # rank-local unit id -> global unit id
+        np.savez(dump, recs=np.concatenate(recs) if recs else np.zeros(0, capi.REGION_DTYPE),
+                 counts=np.concatenate([c for _, _, c in blocks]) if blocks else np.zeros((0, S), np.uint32))
     if final is not None:  # the last step's records: accepted count (outside the timing)
         final = (final[0], sum(int(np.count_nonzero(r["accepted"])) for r, _ in final[1] if len(r)))
     last = (None, final if final is not None else (n0, 0), None)

@@ -9,6 +9,7 @@
 #include <iostream>
 
 #include "wigio.hpp"
+#include "unipeak_hip.h"
 
 namespace unipeak {
 
@@ -142,5 +143,21 @@ int env_gpus() {
     const char *e = std::getenv("UNIPEAK_GPUS");
     return e ? std::atoi(e) : 0;
 }
+
+static int env_share() {
+    const char *e = std::getenv("UNIPEAK_SHARE_DEVICE");
+    return e ? std::atoi(e) : 0;
+}
+
+int cli_device_count() {
+    int nd = 0;
+    up_device_count(&nd);
+    if (nd < 1) return nd;
+    if (env_share() > 0) return env_share();
+    const int g = env_gpus();
+    return g > 0 && g < nd ? g : nd;
+}
+
+int cli_physical_device(int d) { return env_share() > 0 ? 0 : d; }
 
 }  // namespace unipeak

@@ -40,6 +40,12 @@ class ArgParser {
 
 // GPU count for the engine: UNIPEAK_GPUS (0 or unset = every visible device)
 int env_gpus();
+// the devices the CLIs spread units (tags_in_regions: samples) over: every
+// visible HIP device, at most UNIPEAK_GPUS; UNIPEAK_SHARE_DEVICE=N instead
+// makes N logical devices that all live on HIP device 0, each with its own
+// context (the multi-device path exercised on a one-GPU box)
+int cli_device_count();
+int cli_physical_device(int logical);
 
 // UNIPEAK_TIMING=1: phase wall times on stderr ("[timing] <phase> <s>"),
 // so ingest and the GPU phase can be reported apart

@@ -325,13 +325,12 @@ static void join_prewarm() {
 
 void prewarm_devices(int ngpus) {
     g_exit_hook = join_prewarm;  // an input error must not exit mid-initialisation
-    g_prewarm = std::thread([ngpus] {
-        int nd = 0;
-        up_device_count(&nd);
-        if (ngpus > 0 && ngpus < nd) nd = ngpus;
+    (void)ngpus;  // cli_device_count() reads UNIPEAK_GPUS / UNIPEAK_SHARE_DEVICE
+    g_prewarm = std::thread([] {
+        const int nd = cli_device_count();
         std::vector<up_ctx *> pre(std::max(nd, 0), nullptr);
         for (int d = 0; d < nd; ++d)
-            if (up_open(d, &pre[d]) != UP_OK) pre[d] = nullptr;
+            if (up_open(cli_physical_device(d), &pre[d]) != UP_OK) pre[d] = nullptr;
         g_pre = std::move(pre);
         g_pre_ndev = nd;
     });
@@ -343,10 +342,9 @@ void run_units(const EngineParams &ep, PassResult &out) {
         g_prewarm.join();
         ndev = g_pre_ndev;
     } else {
-        up_device_count(&ndev);
+        ndev = cli_device_count();
     }
     if (ndev < 1) fatal("no HIP device available (the GPU path has no CPU fallback)");
-    if (ep.ngpus > 0 && ep.ngpus < ndev) ndev = ep.ngpus;
     const size_t S = ep.p.n_samples;
     // Quirk Q1: a unit whose adds all sit at positions <= bw leaves density
     // (and maybe an open region) in its buffer after flushContig(); the
@@ -400,7 +398,7 @@ void run_units(const EngineParams &ep, PassResult &out) {
         if (job.dev < (int)g_pre.size() && g_pre[job.dev]) {
             job.ctx = g_pre[job.dev];
             g_pre[job.dev] = nullptr;
-        } else if ((rc = up_open(job.dev, &job.ctx))) {
+        } else if ((rc = up_open(cli_physical_device(job.dev), &job.ctx))) {
             return fail(rc, "up_open");
         }
         tm.mark("  gpu: up_open");

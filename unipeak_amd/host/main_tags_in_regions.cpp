@@ -140,11 +140,10 @@ int main(int argc, char **argv) {
     int ndev = 0;
     std::vector<up_tir *> dev;
     std::thread warm([&] {
-        up_device_count(&ndev);
-        ndev = std::min<int>(ndev, (int)files.size());
+        ndev = std::min<int>(cli_device_count(), (int)files.size());
         dev.assign(std::max(ndev, 0), nullptr);
         for (int d = 0; d < ndev; ++d)
-            if (up_tir_open(d, &dev[d]) != UP_OK) dev[d] = nullptr;
+            if (up_tir_open(cli_physical_device(d), &dev[d]) != UP_OK) dev[d] = nullptr;
     });
     const size_t S = files.size();
     std::vector<Records> rec(S);
