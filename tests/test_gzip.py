@@ -93,7 +93,7 @@ def test_pipeline_on_gzipped_wiggles(orc_bin, gpu_lib, tmp_path):
     gz = [p + ".gz" for p in plain]
     rep = _same(orc_bin, tmp_path, "strand_shift", ["-x", "100", "-c", "ct.txt", gz[0]], "shift.txt.gz")
     best = [l for l in rep.splitlines() if l.startswith("# best_shift=")][0].split("=")[1]
-    args = ["-D", "-y", "-u", "-1", "-s", best, "-c", "ct.txt"]
+    args = ["-D", "-y", "-u", "-1", "-r", "5", "-s", best, "-c", "ct.txt"]
     _same(orc_bin, tmp_path, "regions", args + ["-w", "prof.wig.gz"] + gz, "regions.txt.gz")
     table = _same(orc_bin, tmp_path, "regions", args + gz, "r2.txt.gz")
     assert sum(1 for l in table.splitlines() if l.startswith("chr")) > 10
