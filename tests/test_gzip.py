@@ -108,10 +108,11 @@ def test_profile_output_gzipped(orc_bin, gpu_lib, tmp_path):
     """-w x.wig.gz: the density profile through the gzip filter"""
     plain = _inputs(tmp_path, n=1)
     for tool, who in ((orc_bin, "ref"), (os.path.join(BIN, "regions"), "got")):
+        (tmp_path / who).mkdir()  # same file names: the profile's track name is its file name's prefix
         cmd = [tool] + (["regions"] if tool == orc_bin else [])
-        run(cmd + ["-f", "-c", "ct.txt", "-w", f"{who}_p.wig.gz", "-o", f"{who}_t.txt"] + plain,
-            tmp_path)
-    a, b = ((tmp_path / f"{w}_p.wig.gz").read_bytes() for w in ("ref", "got"))
+        run(cmd + ["-f", "-c", "../ct.txt", "-w", "p.wig.gz", "-o", "t.txt", "../" + plain[0]],
+            tmp_path / who)
+    a, b = ((tmp_path / w / "p.wig.gz").read_bytes() for w in ("ref", "got"))
     assert b[:2] == b"\x1f\x8b"
     assert gzip.decompress(a) == gzip.decompress(b) and len(gzip.decompress(b)) > 1000
 
