@@ -146,7 +146,7 @@ def test_bin_refuses_bz2(gpu_lib, tmp_path, tool, where):
     (tmp_path / "reg.txt").write_text("chrA:1000-2000\t1\n")
     inp = "s0.wig.bz2" if where == "input" else plain[0]
     out = "o.txt" if where == "input" else "o.txt.bz2"
-    extra = ["-f", "reg.txt"] if tool == "tags_in_regions" else []
+    extra = {"tags_in_regions": ["-f", "reg.txt"], "strand_shift": ["-x", "20", "-u", "-1"]}.get(tool, [])
     quiet = ["-q"] if tool in ("regions", "convert_align") else []  # the CLIs that take -q
     r = subprocess.run([os.path.join(BIN, tool)] + quiet + ["-c", "ct.txt", "-o", out] + extra + [inp],
                        cwd=tmp_path, capture_output=True, text=True)
