@@ -143,7 +143,8 @@ def test_convert_align_writes_gzip(gpu_lib, tmp_path):
 def test_bin_refuses_bz2(gpu_lib, tmp_path, tool, where):
     plain = _inputs(tmp_path, n=1)
     (tmp_path / "s0.wig.bz2").write_bytes((tmp_path / plain[0]).read_bytes())
-    (tmp_path / "reg.txt").write_text("chrA:1000-2000\t1\n")
+    orc = os.path.join(ROOT, "oracle", "_build", "orc")
+    run([orc, "regions", "-q", "-c", "ct.txt", "-o", "reg.txt", plain[0]], tmp_path)
     inp = "s0.wig.bz2" if where == "input" else plain[0]
     out = "o.txt" if where == "input" else "o.txt.bz2"
     extra = {"tags_in_regions": ["-f", "reg.txt"], "strand_shift": ["-x", "20", "-u", "-1"]}.get(tool, [])
