@@ -349,9 +349,14 @@ void run_units(const EngineParams &ep, PassResult &out) {
     // Quirk Q1: a unit whose adds all sit at positions <= bw leaves density
     // (and maybe an open region) in its buffer after flushContig(); the
     // library replays such chains, so a chain's units share one device.
+    // With a region threshold <= 0 (quirk Q11 live) every unit's last region
+    // is still open after its flush and is closed -- relabelled -- in the
+    // buffer's next unit (peakcall.cpp:76-78, 164-168), so every unit of a
+    // buffer chains to the next one.
     // group[i] = first unit of the chain unit i belongs to.
     std::vector<uint32_t> group(out.units.size());
     {
+        const bool q11 = !(ep.p.region_thr > 0);
         int32_t open_prev[2] = {-1, -1};
         for (uint32_t i = 0; i < out.units.size(); ++i) {
             const UnitBuild &u = out.units[i];
@@ -360,7 +365,7 @@ void run_units(const EngineParams &ep, PassResult &out) {
             group[i] = linked ? group[open_prev[b]] : i;
             const bool in_chain = u.head_hit || linked;
             const bool leaks = !u.add_pos.empty() && u.add_pos.back() <= ep.p.bw;
-            open_prev[b] = (in_chain && leaks) ? (int32_t)i : -1;
+            open_prev[b] = (q11 || (in_chain && leaks)) ? (int32_t)i : -1;
         }
     }
     // LPT assignment of unit groups to devices by track bytes
