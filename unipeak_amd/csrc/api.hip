@@ -2162,8 +2162,8 @@ int up_hbm_copy_gbps(up_ctx *c, uint64_t bytes, int reps, double *gbps) {
     float best = 0;
     for (int i = 0; i <= reps; ++i) {
         HIPCHK(hipEventRecord(c->ev[5], c->stream));
-        hipLaunchKernelGGL(hbm_copy_kernel, dim3(256 * 16), dim3(256), 0, c->stream, (const u32x4 *)a,
-                           (u32x4 *)b, (uint64_t)(bytes / 16));
+        hipLaunchKernelGGL(hbm_copy_kernel, dim3((unsigned)((bytes / 16 + 255) / 256)), dim3(256), 0, c->stream,
+                           (const u32x4 *)a, (u32x4 *)b, (uint64_t)(bytes / 16));
         HIPCHK(hipEventRecord(c->ev[6], c->stream));
         HIPCHK(hipEventSynchronize(c->ev[6]));
         float ms = 0;

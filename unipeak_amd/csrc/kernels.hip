@@ -164,17 +164,6 @@ __device__ __forceinline__ uint32_t ovf_lookup(const UnitDesc &U, uint32_t track
     return (lo < end && (uint32_t)(e[lo] >> 32) == pos) ? (uint32_t)e[lo] : kEsc;
 }
 
-// the K1a screen's bound of an escaped field at position pos: its count when
-// below 255 (the escape tile's byte: two dependent loads), else 255 (the
-// caller then treats the chunk as unbounded, kBig)
-__device__ __forceinline__ uint32_t esc_bound(const UnitDesc &U, uint32_t track, int64_t pos) {
-    if (!U.ovf_tidx || (uint64_t)(pos - 1) >= (uint64_t)U.len) return 255u;
-    const uint32_t ti = ((const uint32_t *)U.ovf_tidx)[(size_t)track * ovf_nblk(U.len) +
-                                                         ((uint32_t)(pos - 1) >> kOvfBlkShift)];
-    if (ti == kNoTile) return 255u;
-    return ((const uint8_t *)U.ovf_tiles)[(size_t)ti * kOvfBlk + ((uint32_t)(pos - 1) & (kOvfBlk - 1u))];
-}
-
 // escapes of N words (lane's position x0 + 64w + lane in word w): each lane
 // resolves its own escaped words, one lookup per round, so the rounds are the
 // most escapes any lane holds rather than the words with an escape anywhere
@@ -854,6 +843,10 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             constexpr int HL = kScrHalo * kChunkBytes / 16;  // halo lane loads per side (kScrHalo chunks)
             uint32_t cs[CPL * kLoads];
             uint32_t big = 0, hs[CPL], hbig = 0, anybig = 0;
+            // tracks (strand * nnc + k < 64) whose bytes in this strip hold an
+            // escape; esc_far: one of the tracks beyond the first 64 does
+            uint64_t esc_tracks = 0;
+            bool esc_far = false;
 #pragma unroll
             for (int k = 0; k < CPL * kLoads; ++k) cs[k] = 0;
 #pragma unroll
@@ -880,6 +873,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                         pf_issue(it + istep, nc_, 0, 0);
                     }
                     const uint32_t w = POOL == 2 ? cptr(P.wscreen)[k] : 1u;
+                    uint32_t tbig = 0;  // this track's escape bits
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
                         const uint32_t d[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
@@ -891,7 +885,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
                             cs[CPL * q + i] = POOL == 2 ? cs[CPL * q + i] + a * w : a;
                         }
-                        anybig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], anybig))));
+                        tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
                     }
                     {
                         const uint32_t d[4] = {hv.x, hv.y, hv.z, hv.w};
@@ -902,8 +896,14 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
                             hs[i] = POOL == 2 ? hs[i] + a * w : a;
                         }
-                        anybig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], anybig))));
+                        tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
                     }
+                    if (__ballot((tbig & kBigMask) != 0u) != 0) {  // wave-uniform
+                        const int ti = st * P.nnc + k;
+                        if (ti < 64) esc_tracks |= 1ull << ti;
+                        else esc_far = true;
+                    }
+                    anybig |= tbig;
                 }
             }
             // Register pre-screen (no LDS): group g = lane l of load q holds
@@ -963,57 +963,107 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 mchunk = 0;
                 exact_blocks = 0;
             } else {
-            // A chunk holding an escaped field: with 2-bit tracks the field
-            // counted as kEsc in the chunk sum is replaced by the position's
-            // count from its escape tile (exact below 255; a count >= 255
-            // makes the chunk unbounded, kBig) -- with several pooled samples
-            // every sample's own peaks hold escapes, and sending all of them
-            // exact made K1b several times longer.  (4-bit tracks: any count
-            // >= 8 goes exact.)  Only strips where some lane saw an escape
-            // re-read their bytes (L2) for the per-field positions.
+            // A chunk holding an escaped field (a count >= kEsc stored as the
+            // escape).  One pooled sample: the chunk goes exact (kBig) -- its
+            // escapes sit at peaks that are exact anyway.  Several pooled
+            // samples (2-bit tracks): every sample's own peaks hold escapes,
+            // and sending them all exact made K1b several times longer, so the
+            // chunk sum takes the chunk's true counts instead -- the escape
+            // tile holds min(count, 255) of every escaped position of its
+            // 1024-position block (0 elsewhere), so one 16-byte tile load per
+            // chunk gives the correction (a 255 leaves the chunk unbounded,
+            // kBig).  Per lane piece (64 positions, one block): the pieces'
+            // tile indices are loaded together, then each piece's tile
+            // chunks together -- two dependent round trips per piece, not per
+            // escape.  Only strips where some lane saw an escape re-read
+            // their bytes (L2).  (4-bit tracks: any count >= 8 goes exact.)
             if (__ballot((anybig & kBigMask) != 0u) != 0) {
+                constexpr bool kBound = kTB == 2 && POOL != 0;
+                constexpr int NP = kLoads + 1;  // the lane's strip pieces and its halo piece
+                const uint32_t nblk = ovf_nblk(U.len);
                 for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
                     for (int k = 0; k < P.nnc; ++k) {
+                        const int tix = st * P.nnc + k;  // only the tracks that saw an escape
+                        if (tix < 64 ? !((esc_tracks >> tix) & 1ull) : !esc_far) continue;
                         const uint32_t trk = (uint32_t)(st * S + ncs[k]);
                         const uint32_t w = POOL == 2 ? cptr(P.wscreen)[k] : 1u;
                         gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, ncs[k]) + fbyte(kPadPos + p0 - 1));
-                        // field f of dword j of the 16 bytes at strip byte B:
-                        // position p0 + kPerByte * (B + 4 j) + f
-                        auto chunk_fix = [&](const uint32_t (&d)[4], int i, int64_t B, uint32_t &sum) -> uint32_t {
-                            uint32_t b = 0;
+                        const bool hl_ok = lane < 2 * HL;
+                        const int hl = lane < HL ? lane - HL : kLoads * kWave + lane - HL;
+                        u32x4 x[NP];
 #pragma unroll
-                            for (int j = 0; j < DPC; ++j) {
-                                if constexpr (kTB == 2) {
-                                    uint32_t e = fbig32(d[DPC * i + j]);
-                                    while (e) {
-                                        const int f = __builtin_ctz(e) >> 1;
-                                        e &= e - 1;
-                                        const uint32_t v =
-                                            esc_bound(U, trk, p0 + kPerByte * (B + 4 * (DPC * i + j)) + f);
-                                        if (v >= 255u) b = 1;
-                                        else sum += (v - kEsc) * w;
+                        for (int q = 0; q < kLoads; ++q) x[q] = t[64 * q + lane];
+                        x[kLoads] = hl_ok ? t[hl] : u32x4{0u, 0u, 0u, 0u};
+                        uint32_t em[NP];  // chunks of each piece holding an escape
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) {
+                            const uint32_t d[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
+                            em[q] = 0;
+#pragma unroll
+                            for (int i = 0; i < CPL; ++i) {
+                                uint32_t e = 0;
+#pragma unroll
+                                for (int j = 0; j < DPC; ++j) e |= fbig32(d[DPC * i + j]);
+                                em[q] |= (e ? 1u : 0u) << i;
+                            }
+                        }
+                        if constexpr (!kBound) {
+#pragma unroll
+                            for (int q = 0; q < kLoads; ++q) big |= em[q] << (CPL * q);
+                            hbig |= em[kLoads];
+                        } else {
+                            // first position of each piece (16 bytes = 64 positions)
+                            auto ppos = [&](int q) -> int64_t {
+                                return p0 + (int64_t)kPerByte * 16 * (q < kLoads ? 64 * q + lane : hl);
+                            };
+                            uint32_t ti[NP];
+#pragma unroll
+                            for (int q = 0; q < NP; ++q) {
+                                ti[q] = kNoTile;
+                                const int64_t pp = ppos(q);
+                                if (em[q] && U.ovf_tidx && pp >= 1 && pp <= (int64_t)U.len)
+                                    ti[q] = ((const uint32_t *)U.ovf_tidx)[(size_t)trk * nblk +
+                                                                           ((uint32_t)(pp - 1) >> kOvfBlkShift)];
+                            }
+#pragma unroll
+                            for (int q = 0; q < NP; ++q) {
+                                if (!em[q]) continue;
+                                if (ti[q] == kNoTile) {  // cannot happen for a stored escape: stay exact
+                                    if (q < kLoads) big |= em[q] << (CPL * q);
+                                    else hbig |= em[q];
+                                    continue;
+                                }
+                                const uint8_t *tile = (const uint8_t *)U.ovf_tiles + (size_t)ti[q] * kOvfBlk +
+                                                      ((uint32_t)(ppos(q) - 1) & (kOvfBlk - 1u));
+                                u32x4 tv[CPL];
+#pragma unroll
+                                for (int i = 0; i < CPL; ++i)
+                                    if ((em[q] >> i) & 1u) tv[i] = *(const u32x4 *)(tile + 16 * i);
+                                const uint32_t d[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
+#pragma unroll
+                                for (int i = 0; i < CPL; ++i) {
+                                    if (!((em[q] >> i) & 1u)) continue;
+                                    const uint32_t v[4] = {tv[i].x, tv[i].y, tv[i].z, tv[i].w};
+                                    uint32_t tsum = 0, full = 0;
+#pragma unroll
+                                    for (int m = 0; m < 4; ++m) {
+                                        tsum = __builtin_amdgcn_sad_u8(v[m], 0u, tsum);
+                                        const uint32_t nv = ~v[m];  // a byte of 255 (count >= 255)
+                                        full |= (nv - 0x01010101u) & ~nv & 0x80808080u;
                                     }
-                                } else {
-                                    b |= fbig32(d[DPC * i + j]);
+                                    uint32_t nesc = 0;
+#pragma unroll
+                                    for (int j = 0; j < DPC; ++j) nesc += (uint32_t)__builtin_popcount(fbig32(d[DPC * i + j]));
+                                    const uint32_t corr = (tsum - kEsc * nesc) * w;
+                                    if (q < kLoads) {
+                                        if (full) big |= 1u << (CPL * q + i);
+                                        else cs[CPL * q + i] += corr;
+                                    } else {
+                                        if (full) hbig |= 1u << i;
+                                        else hs[i] += corr;
+                                    }
                                 }
                             }
-                            return b;
-                        };
-#pragma unroll 1
-                        for (int q = 0; q < kLoads; ++q) {
-                            const u32x4 x = t[64 * q + lane];
-                            const uint32_t d[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                            for (int i = 0; i < CPL; ++i)
-                                big |= (chunk_fix(d, i, 16 * (64 * q + lane), cs[CPL * q + i]) ? 1u : 0u)
-                                       << (CPL * q + i);
-                        }
-                        if (lane < 2 * HL) {
-                            const int hl = lane < HL ? lane - HL : kLoads * kWave + lane - HL;
-                            const u32x4 x = t[hl];
-                            const uint32_t d[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                            for (int i = 0; i < CPL; ++i) hbig |= (chunk_fix(d, i, 16 * hl, hs[i]) ? 1u : 0u) << i;
                         }
                     }
                 }
@@ -2487,23 +2537,14 @@ __global__ void synth_bgc_kernel(uint32_t *stage, uint64_t tkey, int64_t lo, int
     }
 }
 
-// the bench's achievable-HBM reference: a float4 (16 B per lane) streaming
-// copy, four loads in flight per lane before their stores (the guide's
-// measured ceiling is a float4 copy, ~6.3 TB/s)
+// the bench's achievable-HBM reference: a float4 (16 B per lane) copy, one
+// vector per thread over a grid that covers the buffer (tools/copy_probe.hip
+// on MI355X: 6.08 TB/s; grid-stride loops with 1-8 vectors in flight per
+// lane, nontemporal or not, and hipMemcpyDtoD reached 4.8-5.55 TB/s)
 __global__ void __launch_bounds__(256) hbm_copy_kernel(const u32x4 *__restrict__ a, u32x4 *__restrict__ b,
                                                        uint64_t n) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        const u32x4 x0 = __builtin_nontemporal_load(a + i), x1 = __builtin_nontemporal_load(a + i + stride);
-        const u32x4 x2 = __builtin_nontemporal_load(a + i + 2 * stride);
-        const u32x4 x3 = __builtin_nontemporal_load(a + i + 3 * stride);
-        __builtin_nontemporal_store(x0, b + i);
-        __builtin_nontemporal_store(x1, b + i + stride);
-        __builtin_nontemporal_store(x2, b + i + 2 * stride);
-        __builtin_nontemporal_store(x3, b + i + 3 * stride);
-    }
-    for (; i < n; i += stride) b[i] = a[i];
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) b[i] = a[i];
 }
 
 // sum of a track's counts, escapes excluded (their counts are added on the
