@@ -74,6 +74,15 @@ typedef struct {
 } up_params;
 
 #define UP_CLOSE_RULE 0xFFFFFFFFu
+/* region threshold <= 0 (quirk Q11, run in parallel): closed by the add
+ * after the unit's first add at pos >= right + bw + 1 (the first add at a
+ * larger position), else by the unit's flush */
+#define UP_CLOSE_Q11 0xFFFFFFFEu
+/* region threshold <= 0: the region the buffer's previous unit left open
+ * after its flush, relabelled to this unit (misc/peakcall.cpp:164-168) and
+ * closed by this unit's first add at a position above its first add's, else
+ * by its flush; left/right/peak are positions of the previous unit */
+#define UP_CLOSE_Q11_HEAD 0xFFFFFFFDu
 
 /* One candidate region (accepted or rejected by processRegion). */
 typedef struct {
@@ -85,6 +94,8 @@ typedef struct {
     int32_t accepted;         /* passed the hit/kurtosis/correlation filters */
     uint32_t close_pos;       /* UP_CLOSE_RULE: closed by the unit's first add at
                                  pos >= right + bw + 2, else by its flush;
+                                 UP_CLOSE_Q11 / UP_CLOSE_Q11_HEAD: threshold
+                                 <= 0, see above;
                                  0: closed by the unit's flush; otherwise the
                                  position of the add whose retirement closed it
                                  (head-hit units replayed by the emulator, Q1) */
@@ -158,12 +169,15 @@ int up_unit_set_last_add(up_ctx *ctx, uint32_t unit, uint32_t last_add);
 int up_unit_last_add(up_ctx *ctx, uint32_t unit, uint32_t *last_add);
 int up_reset_units(up_ctx *ctx);
 
-/* Run K1..K3 over every unit (stream-ordered, blocking).  Configurations
- * the parallel scan does not represent -- region threshold <= 0 (the leap
- * branch of processPosition is live, quirk Q11) or bw > 255 (kMaxBw: K1's
- * halo of NH <= 4 words) -- run the exact state machine over every unit
- * instead (K0 replay, sequential per buffer: exact, slow); up_run_async and
- * up_unit_profile* refuse them (UP_E_UNSUPPORTED).  up_shift_scan correlates a replayed region's stored
+/* Run K1..K3 over every unit (stream-ordered, blocking).  A region
+ * threshold <= 0 makes the leap branch of processPosition live (quirk Q11):
+ * with non-negative scores every run of processed positions is a region,
+ * found in parallel (K1q; records as UP_CLOSE_Q11 / UP_CLOSE_Q11_HEAD
+ * describe), except when a unit processes position 1 (an add at <= bw + 1)
+ * or a coefficient is negative.  Those, and bw > 255 (kMaxBw: K1's halo of
+ * NH <= 4 words), run the exact state machine over every unit instead (K0
+ * replay, sequential per buffer: exact, slow).  up_run_async refuses both
+ * (UP_E_UNSUPPORTED); up_unit_profile* refuse the replay.  up_shift_scan correlates a replayed region's stored
  * scores (Region::scores), as strandCorr does. */
 int up_run(up_ctx *ctx, uint64_t *n_regions);
 /* Pipelined form of up_run: up_run_async enqueues one pass and returns

@@ -298,6 +298,20 @@ def test_configs0_chr21_cli(gpu_lib, oracle, tmp_path):
     assert len(rows) > 300, len(rows)
 
 
+def test_configs0_chr21_cli_threshold_zero(gpu_lib, oracle, tmp_path):
+    """configs[0]'s input at -r 0 (quirk Q11 live: every run of processed
+    positions is a region, found in parallel by K1q; each buffer's last
+    region never closes) and at -r -1 with -k 0 -t 0: the whole table
+    byte-identical to the oracle CLI"""
+    hg = read_table("hg19")
+    ci = [n for n, _ in hg].index("chr21")
+    _write_inputs(tmp_path, oracle, [hg[ci]], [ci], False)
+    out = _same(tmp_path, "regions", ["-f", "-r", "0", "-m", str(HG19_BP), "-c", "contigs.txt", "s0.wig"],
+                "c0r0.txt")
+    assert sum(1 for l in out.splitlines() if l.startswith("chr21:")) > 100_000
+    _same(tmp_path, "regions", ["-r", "-1", "-k", "0", "-t", "0", "-c", "contigs.txt", "s0.wig"], "c0m1.txt")
+
+
 def test_configs1_hg19_cli(gpu_lib, oracle, tmp_path):
     """BASELINE configs[1] through bin/regions: the whole table byte-identical"""
     hg = read_table("hg19")

@@ -236,6 +236,7 @@ struct up_ctx {
         uint64_t req_reg_cap = 0;    // record / overflow capacities: the caller's thread
         uint32_t req_ovf_cap = 0;    // grows them, the launcher thread only reads these
         int req_tl = 0;
+        bool req_q11 = false;        // K1q instead of K1a/K1x/K1b (threshold <= 0, run_q11)
         bool lpending = false;       // queued for / being launched by the launcher thread
         int lrc = 0;                 // its launch result
         uint64_t cap = 0;            // reg_cap at launch
@@ -288,6 +289,12 @@ struct up_ctx {
     uint32_t emu_reg_cap = 1u << 18;     // K0: positions of one open region
     uint32_t emu_out_cap = 1u << 16;     // K0: region records
     bool host_regions = false;  // merged list lives on the host
+    // threshold <= 0 through K1q (run_q11): the blocking pass in progress,
+    // and per host record the unit whose tracks hold its positions (a region
+    // closed in the buffer's next unit keeps the previous unit's positions)
+    bool q11_run = false;
+    std::vector<uint32_t> h_src_unit;
+    DevBuf<uint32_t> d_q11_head;
     std::vector<up_region> h_regions;
     std::vector<uint32_t> h_counts;
     std::vector<uint8_t> h_emulated;
@@ -1167,7 +1174,24 @@ static void dispatch_stats(up_ctx *c, hipStream_t st, const StatParams &P, uint6
 // <= 0 makes the leap branch of processPosition live (quirk Q11, the leap
 // position joins a region without setting its left end), and kernels wider
 // than kMaxBw exceed the scan's register-resident halo.
-static bool replay_mode(const up_ctx *c) { return c->p.bw > kMaxBw || !(c->p.region_thr > 0); }
+// A threshold <= 0 with non-negative scores (no negative coefficient) runs
+// in parallel instead (K1q, run_q11): every processed position qualifies, so
+// regions are the runs of processed positions; units that start processing
+// at position 1 still take the replay.  UNIPEAK_Q11_REPLAY=1: always replay.
+static bool q11_mode(const up_ctx *c) {
+    if (c->p.region_thr > 0 || c->p.bw > kMaxBw || kTB != 2) return false;
+    for (double q : c->coef)
+        if (!(q >= 0)) return false;
+    static const bool off = [] {
+        const char *e = getenv("UNIPEAK_Q11_REPLAY");
+        return e && *e && *e != '0';
+    }();
+    return !off;
+}
+
+static bool replay_mode(const up_ctx *c) {
+    return c->p.bw > kMaxBw || (!(c->p.region_thr > 0) && !q11_mode(c));
+}
 
 static int check_params(up_ctx *c) {
     if (!c || !c->have_params) return UP_E_STATE;
@@ -1176,10 +1200,13 @@ static int check_params(up_ctx *c) {
     return UP_OK;
 }
 
-static int check_runnable(up_ctx *c) {  // the parallel scan
+// the parallel scan; K1q passes only inside the blocking up_run (their
+// records are finished on the host), K1q's dense profile always
+static int check_runnable(up_ctx *c, bool profile = false) {
     int r = check_params(c);
     if (r) return r;
-    return replay_mode(c) ? UP_E_UNSUPPORTED : UP_OK;
+    if (replay_mode(c)) return UP_E_UNSUPPORTED;
+    return q11_mode(c) && !c->q11_run && !profile ? UP_E_UNSUPPORTED : UP_OK;
 }
 
 // Quirk Q1: units whose pooled hits include a position <= bw are replayed
@@ -1494,13 +1521,15 @@ static int enqueue_rest(up_ctx *c, int slot, const ScanParams &SP, const StatPar
     up_ctx::Pass &ps = c->pass[slot];
     const uint32_t ns = c->nstrips;
     const uint32_t nsb = (ns + kSegBlock - 1) / kSegBlock;
-    if (k1a_waves) {  // K1x: list the stashed work-list entries for K1b
-        hipLaunchKernelGGL(xref_kernel, dim3(1), dim3(1024), 0, ps.stream, ps.d_xwcount.p, k1a_waves,
-                           k1a_xcap, ps.d_xref.p, ps.d_xcount.p);
+    if (!ps.req_q11) {  // (K1q wrote every strip's runs itself)
+        if (k1a_waves) {  // K1x: list the stashed work-list entries for K1b
+            hipLaunchKernelGGL(xref_kernel, dim3(1), dim3(1024), 0, ps.stream, ps.d_xwcount.p, k1a_waves,
+                               k1a_xcap, ps.d_xref.p, ps.d_xcount.p);
+            HIPCHK(hipGetLastError());
+        }
+        dispatch_scan<false, kModeExact>(c, ps.stream, SP, 0, ns);    // K1b: exact blocks
         HIPCHK(hipGetLastError());
     }
-    dispatch_scan<false, kModeExact>(c, ps.stream, SP, 0, ns);    // K1b: exact blocks
-    HIPCHK(hipGetLastError());
     if (events) HIPCHK(hipEventRecord(ps.ev[2], ps.stream));
     unsigned long long *thdr = (unsigned long long *)ps.target;
     if (int r = launch_seg_count_head(c, slot)) return r;
@@ -1628,7 +1657,16 @@ static int launch_pass(up_ctx *c, int slot) {
     const int tl = ps.tl;
     if (tl >= 1) HIPCHK(hipEventRecord(ps.ev[0], s1));
     c->k1a_waves = 0;
-    dispatch_scan<false, kModeScreen>(c, s1, SP, 0, ns);   // K1a: stream + screen
+    if (ps.req_q11) {  // K1q: runs of processed positions (threshold <= 0)
+        graph = false;
+        P.peak_pos = nullptr;  // K3 runs its KDE for the peaks
+        P.peak_val = nullptr;
+        P.q11 = 1;
+        const unsigned blocks = (unsigned)std::min<uint64_t>((ns + 3) / 4, 4096);
+        hipLaunchKernelGGL(proc_runs_kernel, dim3(std::max(1u, blocks)), dim3(256), 0, s1, SP);
+    } else {
+        dispatch_scan<false, kModeScreen>(c, s1, SP, 0, ns);   // K1a: stream + screen
+    }
     HIPCHK(hipGetLastError());
     hipEvent_t k1a_end = ps.k1a_end;  // a timed pass's end-of-K1a event serves as well
     if (tl >= 1) k1a_end = ps.ev[1];
@@ -1747,6 +1785,7 @@ int up_run_async(up_ctx *c) {
     ps.req_target_hostp = c->target_hostp;
     ps.req_target_cap = c->target_cap;
     ps.req_tl = c->timing;
+    ps.req_q11 = c->q11_run;
     ps.req_last_nreg = c->last_nreg;
     ps.req_reg_cap = c->reg_cap;
     ps.req_ovf_cap = c->ovf_cap;
@@ -1907,12 +1946,114 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
     return UP_OK;
 }
 
+// the records of a K1q pass -> the reference's regions (host list):
+//  * every run [s, e] was reached by a leap: Region::left = s + 1, right =
+//    e + 1, peak = (first maximum over s + 1 .. e) + 1 (K3 skipped s), its
+//    statistics over s .. e as K3 computed them (peakcall.cpp:76-78,
+//    data.cpp:92-102); closed by the add after the first add at pos >=
+//    right + bw + 1, else by the flush (UP_CLOSE_Q11);
+//  * the last run of a unit is still open after its flush: the buffer's
+//    next unit relabels it (peakcall.cpp:164-168) and its first leap closes
+//    it -- the record moves there (UP_CLOSE_Q11_HEAD, positions still the
+//    previous unit's); the buffer's last unit's last run is never closed
+static int q11_finish(up_ctx *c) {
+    const up_ctx::Pass &ps = c->pass[c->cur_slot];
+    const int S = c->p.n_samples;
+    const uint32_t nu = (uint32_t)c->units.size();
+    const up_region *par = c->hp_regions[c->cur_slot].p;
+    const uint32_t *pcnt = c->hp_counts[c->cur_slot].p;
+    std::vector<up_region> dpar;
+    std::vector<uint32_t> dcnt;
+    if (ps.target && ps.target_hostp) {
+        par = (const up_region *)((const uint8_t *)ps.target_hostp + 8);
+        pcnt = (const uint32_t *)((const uint8_t *)ps.target_hostp + 8 + ps.target_cap * sizeof(up_region));
+    } else if (ps.target) {
+        dpar.resize(c->nreg);
+        dcnt.resize((size_t)c->nreg * S);
+        if (c->nreg) {
+            HIPCHK(hipMemcpy(dpar.data(), ps.target + 8, c->nreg * sizeof(up_region), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(dcnt.data(), ps.target + 8 + ps.target_cap * sizeof(up_region),
+                             dcnt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        }
+        par = dpar.data();
+        pcnt = dcnt.data();
+    }
+    std::vector<uint64_t> first(nu + 1, c->nreg);  // records of unit u: [first[u], first[u + 1])
+    for (uint64_t i = c->nreg; i-- > 0;) first[par[i].unit] = i;
+    for (uint32_t u = nu; u-- > 0;) first[u] = std::min(first[u], first[u + 1]);
+    std::vector<int64_t> moved_in(nu, -1);  // the record a unit closes for its buffer's previous unit
+    int64_t prev[2] = {-1, -1};
+    for (uint32_t u = 0; u < nu; ++u) {
+        if (first[u] == first[u + 1]) continue;  // no adds: no relabel (add() never ran)
+        const int b = c->units[u].buffer;
+        if (prev[b] >= 0) moved_in[u] = (int64_t)first[prev[b] + 1] - 1;
+        prev[b] = u;
+    }
+    c->h_regions.clear();
+    c->h_counts.clear();
+    c->h_emulated.clear();
+    c->h_score_off.clear();
+    c->h_src_unit.clear();
+    auto push = [&](uint64_t i, uint32_t unit, uint32_t close) {
+        up_region r = par[i];
+        c->h_src_unit.push_back(r.unit);
+        r.left += 1;
+        r.right += 1;
+        r.peak += 1;
+        r.unit = unit;
+        r.close_pos = close;
+        c->h_regions.push_back(r);
+        c->h_counts.insert(c->h_counts.end(), pcnt + i * S, pcnt + (i + 1) * S);
+        c->h_emulated.push_back(2);
+        c->h_score_off.push_back(~0ull);
+    };
+    for (uint32_t u = 0; u < nu; ++u) {
+        if (moved_in[u] >= 0) push((uint64_t)moved_in[u], u, UP_CLOSE_Q11_HEAD);
+        for (uint64_t i = first[u]; i + 1 < first[u + 1]; ++i) push(i, u, UP_CLOSE_Q11);
+    }
+    c->h_resync.assign(nu, 0);
+    c->h_pf_off.assign(nu + 1, 0);
+    return publish_host_regions(c, ps);
+}
+
+static int run_replay(up_ctx *c, uint64_t *n_regions);
+
+// threshold <= 0 (q11_mode): one K1q pass, unless a unit processes position
+// 1 (an add at <= bw + 1), which the whole-buffer replay handles
+static int run_q11(up_ctx *c, uint64_t *n_regions) {
+    HIPCHK(hipSetDevice(c->dev));
+    int r = sync_units(c);
+    if (r) return r;
+    const uint32_t nu = (uint32_t)c->units.size();
+    if (nu) {
+        HIPCHK(c->d_q11_head.ensure(nu));
+        HIPCHK(hipMemsetAsync(c->d_q11_head.p, 0, nu * sizeof(uint32_t), c->stream));
+        hipLaunchKernelGGL(q11_head_kernel, dim3(nu), dim3(256), 0, c->stream, c->d_units.p,
+                           (int)c->p.n_samples, (int)c->p.bw, c->d_q11_head.p);
+        HIPCHK(hipGetLastError());
+        std::vector<uint32_t> f(nu);
+        HIPCHK(hipMemcpyAsync(f.data(), c->d_q11_head.p, nu * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (uint32_t v : f)
+            if (v) return run_replay(c, n_regions);
+    }
+    c->q11_run = true;
+    r = up_run_async(c);
+    if (!r) r = up_run_wait(c, nullptr);
+    c->q11_run = false;
+    if (r) return r;
+    if ((r = q11_finish(c))) return r;
+    if (n_regions) *n_regions = c->nreg;
+    return UP_OK;
+}
+
 int up_run(up_ctx *c, uint64_t *n_regions) {
     if (!c) return UP_E_ARG;
     if (busy(c)) return UP_E_STATE;
     int rc = check_params(c);
     if (rc) return rc;
     if (replay_mode(c)) return run_replay(c, n_regions);
+    if (q11_mode(c)) return run_q11(c, n_regions);
     int r = up_run_async(c);
     if (r) return r;
     return up_run_wait(c, n_regions);
@@ -2029,9 +2170,12 @@ static int shift_run(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shif
         // cannot reproduce; refuse rather than return something else
         std::vector<uint32_t> un(c->nreg);
         for (uint64_t i = 0; i < c->nreg; ++i) {
-            st[i] = c->h_regions[i].left;
-            en[i] = c->h_regions[i].right;
-            un[i] = c->h_regions[i].unit;
+            // K1q records (h_emulated 2): positions left - 1 .. right - 1 of
+            // their source unit
+            const bool q = c->h_emulated[i] == 2;
+            st[i] = c->h_regions[i].left - (q ? 1u : 0u);
+            en[i] = c->h_regions[i].right - (q ? 1u : 0u);
+            un[i] = q ? c->h_src_unit[i] : c->h_regions[i].unit;
         }
         // replayed regions (Q1 heads, whole-buffer replay) correlate the
         // scores the state machine stored (Region::scores), copied below
@@ -2053,7 +2197,7 @@ static int shift_run(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shif
     for (size_t j = 0; j < n; ++j) {
         if (idx[j] >= c->nreg) return UP_E_ARG;
         const uint64_t len = (uint64_t)en[idx[j]] - st[idx[j]] + 1;
-        pref[j] = c->host_regions && c->h_emulated[idx[j]] ? 1 : 0;
+        pref[j] = c->host_regions && c->h_emulated[idx[j]] == 1 ? 1 : 0;
         if (pref[j] || len > (uint64_t)kShiftLds) {
             off[j] = tot;
             tot += 2ull * len;
@@ -2113,7 +2257,7 @@ int up_timings(up_ctx *c, double *ms, int n) {
 
 int up_unit_profile_range(up_ctx *c, uint32_t unit, uint64_t first, uint32_t count, double *out_f,
                           double *out_r) {
-    int r = check_runnable(c);
+    int r = check_runnable(c, true);
     if (r) return r;
     if (busy(c)) return UP_E_STATE;  // a pass in flight reads this state
     if (unit >= c->units.size() || !out_f || first < 1 || count == 0) return UP_E_ARG;

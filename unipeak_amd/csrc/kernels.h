@@ -157,6 +157,8 @@ struct StatParams {
     double *corr_scratch; // -D -y: per K3 wave corr_cap (f, r) pairs, or null
     uint32_t corr_cap;
     int32_t qmode;        // K1 peaks are Q keys (ScanParams::qmode): K3 scores the peak
+    int32_t q11;          // runs of K1q (threshold <= 0): the peak skips the run's first
+                          // position (it joined by a leap, peakcall.cpp:76-78)
 };
 
 }  // namespace upk

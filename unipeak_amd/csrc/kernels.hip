@@ -1461,6 +1461,187 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 }
 
 #ifndef UPK_NH_TU  // the per-NH translation units hold only the templated kernels
+// ------------------------------------------------------------------------
+// K1q: the region scan of a threshold <= 0 (quirk Q11 live), parallel.
+// With thr <= 0 and non-negative scores every processed position qualifies,
+// so processPosition (misc/peakcall.cpp:55-86) turns every maximal run of
+// processed positions -- the positions within bw of an add() (any sample,
+// controls included: control-only adds retire positions too; both strands
+// of a nondirectional unit) -- into one region, reached by a leap: the
+// run's first position joins without setting `left` (peakcall.cpp:76-78),
+// so the host shifts the run's coordinates by one.  This
+// kernel writes each strip's run boundaries in K1b's record format (peaks
+// unknown: K3 runs its KDE), so K2 and K3 follow unchanged.  A run starts at
+// a - bw for an add a with no add in [a - 2bw - 1, a - 1] and ends at a + bw
+// for an add with none in [a + 1, a + 2bw + 1].  One wave per strip: 64-
+// position presence words of the strip and a 4-word halo on each side (bw
+// <= 255), five words per lane; the previous / next add of every word by
+// wave scans.  2-bit tracks (the host checks).
+__device__ __forceinline__ uint64_t nz_bits64(u32x4 x) {
+    auto c16 = [](uint32_t d) {  // nonzero 2-bit fields -> 16 bits
+        uint32_t v = (d | (d >> 1)) & 0x55555555u;
+        v = (v | (v >> 1)) & 0x33333333u;
+        v = (v | (v >> 2)) & 0x0F0F0F0Fu;
+        v = (v | (v >> 4)) & 0x00FF00FFu;
+        v = (v | (v >> 8)) & 0x0000FFFFu;
+        return (uint64_t)v;
+    };
+    return c16(x.x) | (c16(x.y) << 16) | (c16(x.z) << 32) | (c16(x.w) << 48);
+}
+
+__device__ __forceinline__ uint64_t rl_u64(uint64_t v, int l) {
+    return (uint64_t)rl_u((uint32_t)v, l) | ((uint64_t)rl_u((uint32_t)(v >> 32), l) << 32);
+}
+
+// bits of word [base, base + 63] inside [lo, hi]
+__device__ __forceinline__ uint64_t range_bits(int64_t base, int64_t lo, int64_t hi) {
+    const int64_t a = lo > base ? lo - base : 0, b = hi < base + 63 ? hi - base : 63;
+    if (a > b) return 0;
+    const uint64_t up = b == 63 ? ~0ull : ((1ull << (b + 1)) - 1);
+    return up & ~((1ull << a) - 1);
+}
+
+constexpr int kQHalo = 4;                                   // words of halo each side (bw <= 255)
+constexpr int kQWords = kStrip / 64 + 2 * kQHalo;           // 264
+constexpr int kQRounds = (kQWords + kWave - 1) / kWave;     // 5
+
+__global__ void __launch_bounds__(256) proc_runs_kernel(ScanParams P) {
+    const auto *units = cptr(P.units);
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    const int64_t bw = P.bw, gap = 2 * bw + 1;
+    const int S = P.S;
+    constexpr int64_t kNone = -((int64_t)1 << 40);
+    uint32_t cur = 0;
+    bool have = false;
+    for (uint32_t strip = wave; strip < P.nstrips; strip += nwaves) {
+        if (!have) { cur = find_unit(units, P.nunits, strip); have = true; }
+        while (strip >= units[cur].strip0 + units[cur].nstrips) ++cur;
+        const UnitDesc U = units[cur];
+        const uint32_t local = strip - U.strip0;
+        const int64_t p0 = 1 + (int64_t)local * kStrip, pend = p0 + kStrip - 1;
+        // presence words: word w (lane l, round r: w = 64 r + l - kQHalo) covers p0 + 64 w ..
+        uint64_t m[kQRounds];
+#pragma unroll
+        for (int r = 0; r < kQRounds; ++r) m[r] = 0;
+        for (int st = 0; st < U.nstrands; ++st)
+            for (int k = 0; k < S; ++k) {
+                gu32x4 *t = (gu32x4 *)(track_u8(U, S, st, k) + fbyte(kPadPos + p0 - 1));
+#pragma unroll
+                for (int r = 0; r < kQRounds; ++r) {
+                    const int w = 64 * r + lane - kQHalo;
+                    if (w < kQWords - kQHalo) m[r] |= nz_bits64((u32x4)t[w]);
+                }
+            }
+        // previous add before each word (exclusive prefix max of the words'
+        // last adds) and next add after it (exclusive suffix min of firsts)
+        int64_t prv[kQRounds], nxt[kQRounds];
+        int64_t carry = kNone;
+#pragma unroll
+        for (int r = 0; r < kQRounds; ++r) {
+            const int64_t base = p0 + 64 * (64 * r + lane - kQHalo);
+            int64_t v = m[r] ? base + 63 - __builtin_clzll(m[r]) : kNone;
+            for (int d = 1; d < 64; d <<= 1) {
+                const int64_t o = __shfl_up((long long)v, d);
+                if (lane >= d && o > v) v = o;
+            }
+            const int64_t ex = __shfl_up((long long)v, 1);
+            prv[r] = lane == 0 ? carry : (ex > carry ? ex : carry);
+            const int64_t top = __shfl((long long)v, 63);
+            carry = top > carry ? top : carry;
+        }
+        carry = -kNone;  // +inf
+#pragma unroll
+        for (int r = kQRounds - 1; r >= 0; --r) {
+            const int64_t base = p0 + 64 * (64 * r + lane - kQHalo);
+            int64_t v = m[r] ? base + __builtin_ctzll(m[r]) : -kNone;
+            for (int d = 1; d < 64; d <<= 1) {
+                const int64_t o = __shfl_down((long long)v, d);
+                if (lane + d < 64 && o < v) v = o;
+            }
+            const int64_t ex = __shfl_down((long long)v, 1);
+            nxt[r] = lane == 63 ? carry : (ex < carry ? ex : carry);
+            const int64_t bot = __shfl((long long)v, 0);
+            carry = bot < carry ? bot : carry;
+        }
+        // per word: adds that start / end a run (bits at the add positions;
+        // the boundary itself sits bw away), and the strip-edge flags
+        uint64_t sa[kQRounds], ea[kQRounds];
+        bool f0 = false, fl = false;
+#pragma unroll
+        for (int r = 0; r < kQRounds; ++r) {
+            const int64_t base = p0 + 64 * (64 * r + lane - kQHalo);
+            sa[r] = ea[r] = 0;
+            int64_t prev = prv[r];
+            uint64_t mm = m[r];
+            while (mm) {
+                const int b = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                const int64_t a = base + b;
+                const int64_t nx = mm ? base + __builtin_ctzll(mm) : nxt[r];
+                if (prev == kNone || a - prev > gap) sa[r] |= 1ull << b;
+                if (nx == -kNone || nx - a > gap) ea[r] |= 1ull << b;
+                prev = a;
+            }
+            f0 |= (m[r] & range_bits(base, p0 - bw, p0 + bw)) != 0;
+            fl |= (m[r] & range_bits(base, pend - bw, pend + bw)) != 0;
+        }
+        const bool F0 = __ballot(f0) != 0, FL = __ballot(fl) != 0;
+        // records in position order: starts in (p0, pend], ends in [p0, pend)
+        RecList R_{0, 0, kInline};
+#pragma unroll
+        for (int r = 0; r < kQRounds; ++r) {
+            uint64_t live = __ballot(sa[r] != 0);
+            while (live) {
+                const int l = __builtin_ctzll(live);
+                live &= live - 1;
+                uint64_t bits = rl_u64(sa[r], l);
+                const int64_t base = p0 + 64 * (64 * r + l - kQHalo);
+                while (bits) {
+                    const int b = __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const int64_t x = base + b - bw;
+                    if (x > p0 && x <= pend) rec_start(R_, (uint32_t)x, P, strip, lane);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kQRounds; ++r) {
+            uint64_t live = __ballot(ea[r] != 0);
+            while (live) {
+                const int l = __builtin_ctzll(live);
+                live &= live - 1;
+                uint64_t bits = rl_u64(ea[r], l);
+                const int64_t base = p0 + 64 * (64 * r + l - kQHalo);
+                while (bits) {
+                    const int b = __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const int64_t x = base + b + bw;
+                    if (x >= p0 && x < pend) rec_end(R_, (uint32_t)x, 0u, -__builtin_inf(), P, strip, lane);
+                }
+            }
+        }
+        const uint64_t info = (uint64_t)R_.ns | ((uint64_t)R_.ne << 16) | ((uint64_t)F0 << 32) |
+                              ((uint64_t)FL << 33) | ((uint64_t)(local == 0) << 34) |
+                              ((uint64_t)(local + 1 == U.nstrips) << 35) | ((uint64_t)(R_.slot != kInline) << 36);
+        if (lane == 0) P.strip_info[strip] = info;
+    }
+}
+
+// K1q's fallback test: a unit with an add at a position <= bw + 1 starts
+// processing at position 1 (a single step, or the misaligned window of quirk
+// Q1): the host then replays the whole buffer.  One block per unit.
+__global__ void __launch_bounds__(256) q11_head_kernel(const UnitDesc *units, int S, int bw, uint32_t *flag) {
+    const UnitDesc U = units[blockIdx.x];
+    bool any = false;
+    for (int st = 0; st < U.nstrands; ++st)
+        for (int k = 0; k < S; ++k)
+            for (int p = 1 + (int)threadIdx.x; p <= bw + 1 && p <= (int)U.len; p += blockDim.x)
+                any |= fld_at(track_u8(U, S, st, k), p) != 0u;
+    if (__syncthreads_or(any) && threadIdx.x == 0) flag[blockIdx.x] = 1u;
+}
+
 // K1x: the K1a waves' stash counts -> xref (stash indices of the listed
 // entries, every front entry first) and the totals in xcount.  One block:
 // thread t owns K1a waves [t*per, (t+1)*per).
@@ -2060,7 +2241,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 hr_c = hr[NH];
             }
             const double score = NONDIR ? f + r : f;
-            if (valid && (best_x < 0 || score > best)) { best = score; best_x = x; }
+            // (K1q runs: the first position joined by a leap with peakPos 0,
+            // so Region::addPos re-seeds the peak at the next one, data.cpp:98-101)
+            if (valid && (!P.q11 || x > (int64_t)left) && (best_x < 0 || score > best)) {
+                best = score;
+                best_x = x;
+            }
             if (NONDIR && P.want_corr) {
                 // pass 3 reads f, r back from this wave's slab instead of
                 // recomputing the KDE

@@ -479,9 +479,21 @@ std::vector<Emitted> order_candidates(const PassResult &out, uint16_t bw, bool a
     for (const Candidate &c : out.cands) {
         const UnitBuild &u = out.units[c.unit_index];
         // closed by the first add at pos >= right + bw + 2, else by the flush;
-        // regions from the Q1 replay name their closing add (0: the flush)
+        // regions from the Q1 replay name their closing add (0: the flush);
+        // threshold <= 0 (Q11): by the first add past the first add at pos >=
+        // right + bw + 1, or (a region left open by the previous unit) past
+        // the unit's first add -- an add at the same position (the other
+        // strand) retires nothing
         uint64_t key = (uint64_t)c.r.right + bw + 2;
-        if (c.r.close_pos != UP_CLOSE_RULE) key = c.r.close_pos ? c.r.close_pos : ~0ull;
+        if (c.r.close_pos == UP_CLOSE_Q11 || c.r.close_pos == UP_CLOSE_Q11_HEAD) {
+            auto a1 = u.add_pos.begin();
+            if (c.r.close_pos == UP_CLOSE_Q11)
+                a1 = std::lower_bound(u.add_pos.begin(), u.add_pos.end(), (uint64_t)c.r.right + bw + 1,
+                                      [](uint32_t a, uint64_t k) { return (uint64_t)a < k; });
+            key = a1 != u.add_pos.end() ? (uint64_t)*a1 + 1 : ~0ull;
+        } else if (c.r.close_pos != UP_CLOSE_RULE) {
+            key = c.r.close_pos ? c.r.close_pos : ~0ull;
+        }
         auto it = std::lower_bound(u.add_pos.begin(), u.add_pos.end(), key,
                                    [](uint32_t a, uint64_t k) { return (uint64_t)a < k; });
         const uint64_t t = it != u.add_pos.end() ? u.add_time[it - u.add_pos.begin()] : u.flush_time;
