@@ -308,7 +308,7 @@ def test_configs0_chr21_cli_threshold_zero(gpu_lib, oracle, tmp_path):
     _write_inputs(tmp_path, oracle, [hg[ci]], [ci], False)
     out = _same(tmp_path, "regions", ["-f", "-r", "0", "-m", str(HG19_BP), "-c", "contigs.txt", "s0.wig"],
                 "c0r0.txt")
-    assert sum(1 for l in out.splitlines() if l.startswith("chr21:")) > 100_000
+    assert sum(1 for l in out.splitlines() if l.startswith("chr21:")) > 100  # (-t 10: most runs hold a tag or two)
     _same(tmp_path, "regions", ["-r", "-1", "-k", "0", "-t", "0", "-c", "contigs.txt", "s0.wig"], "c0m1.txt")
 
 
