@@ -6,7 +6,8 @@
   non-negative scores every run of processed positions is a region, found in
   parallel (K1q); a negative coefficient or a unit that
   processes position 1 takes the exact replay below;
-* kernel bandwidth > 255 -- wider than the scan's register-resident halo:
+* kernel bandwidth > 511 -- wider than the scan's register-resident halo
+  (NH <= 8 window words; round 3 stopped at 255):
   the exact state machine on the GPU over every unit (K0 replay,
   unipeak_amd/csrc/emulate.hip); windows up to 64 KiB live in LDS, wider ones
   in global scratch.
@@ -66,8 +67,9 @@ def test_threshold_le_zero_q11(gpu_lib, oracle, thr, seed):
     compare(ref, ref_sums, regs, gcnt)
 
 
-@pytest.mark.parametrize("bw", [128, 150, 300, 1000, 2500])
+@pytest.mark.parametrize("bw", [128, 150, 256, 300, 450, 511, 512, 1000, 2500])
 def test_wide_bandwidth(gpu_lib, oracle, bw):
+    """up to 511 the parallel scan (NH <= 8 window words), wider the replay"""
     rng = np.random.default_rng(bw)
     length, bg = 400_000, 0.002
     pos, cnt = random_unit(rng, length, bw, n_clusters=40)
@@ -105,10 +107,10 @@ def test_replay_multi_sample_control_and_coeffs(gpu_lib, oracle):
 
 
 def test_replay_refuses_pipelined_and_profile(gpu_lib):
-    """bw > 255 (kMaxBw): outside the parallel scan, the whole-buffer replay"""
+    """bw > 511 (kMaxBw): outside the parallel scan, the whole-buffer replay"""
     capi = gpu_lib
     with capi.Lib(0) as g:
-        g.set_params(300, 1, 0.003)
+        g.set_params(600, 1, 0.003)
         u = g.add_unit(10_000)
         g.scatter(u, 0, 0, np.array([5000], np.uint32), np.array([3], np.uint32))
         assert g.run() >= 0

@@ -66,7 +66,7 @@ def test_tag_total_counts_escapes(gpu_lib):
 
 
 @pytest.mark.parametrize("thr", [0.05, 1.0, 25.0, 400.0])
-@pytest.mark.parametrize("bw", [1, 15, 16, 17, 33, 64, 127, 128, 150, 191, 192, 255])
+@pytest.mark.parametrize("bw", [1, 15, 16, 17, 33, 64, 127, 128, 150, 191, 192, 255, 256, 300, 383, 384, 449, 511])
 def test_screen_thresholds_and_bandwidths(gpu_lib, oracle, thr, bw):
     rng = np.random.default_rng(1000 * bw + int(thr * 10))
     length, bg = 70_000, 0.003

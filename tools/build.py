@@ -32,7 +32,7 @@ def _run(cmd, cwd=ROOT):
 def compile_lib(out, extra=(), jobs=None):
     """libunipeak_hip.so from six translation units compiled in parallel:
     api.hip (C-ABI, non-templated kernels), tir.hip (tags_in_regions) and
-    nh_tu.hip once per window width NH = 1..4 (the templated K1/K3/K4
+    nh_tu.hip once per window width NH = 1..8 (the templated K1/K3/K4
     kernels)."""
     from concurrent.futures import ThreadPoolExecutor
     csrc = os.path.join(ROOT, "unipeak_amd", "csrc")
@@ -44,7 +44,7 @@ def compile_lib(out, extra=(), jobs=None):
     units = [("api", os.path.join(csrc, "api.hip"), []),
              ("tir", os.path.join(csrc, "tir.hip"), []),
              ("countmap", os.path.join(csrc, "countmap.hip"), [])] + [
-        (f"nh{k}", os.path.join(csrc, "nh_tu.hip"), [f"-DUPK_NH_TU={k}"]) for k in (1, 2, 3, 4)]
+        (f"nh{k}", os.path.join(csrc, "nh_tu.hip"), [f"-DUPK_NH_TU={k}"]) for k in range(1, 9)]
     def one(u):
         name, src, defs = u
         obj = os.path.join(objdir, name + ".o")

@@ -23,7 +23,7 @@ def main():
             if l.strip() and not l.startswith("#")]
     ci = [r[0] for r in rows].index(name)
     L = int(rows[ci][1])
-    for bw, thr in ((50, 25.0), (50, 0.0), (150, 25.0), (300, 25.0)):
+    for bw, thr in ((50, 25.0), (50, 0.0), (150, 25.0), (300, 25.0), (511, 25.0), (300, 0.0)):
         with capi.Lib(0) as g:
             g.set_params(bw, 1, 0.0029, region_thr=thr)
             for buf in (0, 1):
@@ -35,7 +35,7 @@ def main():
             dt = time.perf_counter() - t0
             regs, _ = g.regions(n)
             print(json.dumps({"contig": name, "bp": L, "bw": bw, "region_thr": thr,
-                              "replay": bw > 255 or thr <= 0, "ms": round(dt * 1e3, 3),
+                              "path": "replay" if bw > 511 else ("K1q" if thr <= 0 else "scan"), "ms": round(dt * 1e3, 3),
                               "gbps": round(L / dt / 1e9, 3), "candidates": int(n),
                               "accepted": int(regs["accepted"].sum())}), flush=True)
 

@@ -28,14 +28,26 @@ const void *scan_kernel_nh1(int, bool, bool, int);
 const void *scan_kernel_nh2(int, bool, bool, int);
 const void *scan_kernel_nh3(int, bool, bool, int);
 const void *scan_kernel_nh4(int, bool, bool, int);
+const void *scan_kernel_nh5(int, bool, bool, int);
+const void *scan_kernel_nh6(int, bool, bool, int);
+const void *scan_kernel_nh7(int, bool, bool, int);
+const void *scan_kernel_nh8(int, bool, bool, int);
 const void *stats_kernel_nh1(int, bool);
 const void *stats_kernel_nh2(int, bool);
 const void *stats_kernel_nh3(int, bool);
 const void *stats_kernel_nh4(int, bool);
+const void *stats_kernel_nh5(int, bool);
+const void *stats_kernel_nh6(int, bool);
+const void *stats_kernel_nh7(int, bool);
+const void *stats_kernel_nh8(int, bool);
 const void *shift_kernel_nh1(int);
 const void *shift_kernel_nh2(int);
 const void *shift_kernel_nh3(int);
 const void *shift_kernel_nh4(int);
+const void *shift_kernel_nh5(int);
+const void *shift_kernel_nh6(int);
+const void *shift_kernel_nh7(int);
+const void *shift_kernel_nh8(int);
 // window words on each side of an output word: ceil((bw + 1) / 64)
 static int window_nh(int bw) { return (bw + 64) / 64; }
 static const void *scan_kernel_for(int bw, int pool, bool nd, bool prof, int mode) {
@@ -43,7 +55,11 @@ static const void *scan_kernel_for(int bw, int pool, bool nd, bool prof, int mod
     case 1: return scan_kernel_nh1(pool, nd, prof, mode);
     case 2: return scan_kernel_nh2(pool, nd, prof, mode);
     case 3: return scan_kernel_nh3(pool, nd, prof, mode);
-    default: return scan_kernel_nh4(pool, nd, prof, mode);
+    case 4: return scan_kernel_nh4(pool, nd, prof, mode);
+    case 5: return scan_kernel_nh5(pool, nd, prof, mode);
+    case 6: return scan_kernel_nh6(pool, nd, prof, mode);
+    case 7: return scan_kernel_nh7(pool, nd, prof, mode);
+    default: return scan_kernel_nh8(pool, nd, prof, mode);
     }
 }
 static const void *stats_kernel_for(int bw, int pool, bool nd) {
@@ -51,7 +67,11 @@ static const void *stats_kernel_for(int bw, int pool, bool nd) {
     case 1: return stats_kernel_nh1(pool, nd);
     case 2: return stats_kernel_nh2(pool, nd);
     case 3: return stats_kernel_nh3(pool, nd);
-    default: return stats_kernel_nh4(pool, nd);
+    case 4: return stats_kernel_nh4(pool, nd);
+    case 5: return stats_kernel_nh5(pool, nd);
+    case 6: return stats_kernel_nh6(pool, nd);
+    case 7: return stats_kernel_nh7(pool, nd);
+    default: return stats_kernel_nh8(pool, nd);
     }
 }
 static const void *shift_kernel_for(int bw, int pool) {
@@ -59,7 +79,11 @@ static const void *shift_kernel_for(int bw, int pool) {
     case 1: return shift_kernel_nh1(pool);
     case 2: return shift_kernel_nh2(pool);
     case 3: return shift_kernel_nh3(pool);
-    default: return shift_kernel_nh4(pool);
+    case 4: return shift_kernel_nh4(pool);
+    case 5: return shift_kernel_nh5(pool);
+    case 6: return shift_kernel_nh6(pool);
+    case 7: return shift_kernel_nh7(pool);
+    default: return shift_kernel_nh8(pool);
     }
 }
 }  // namespace upk
@@ -1221,7 +1245,6 @@ static int launch_seg_count_head(up_ctx *c, int slot) {
     const uint32_t nsb = (ns + kSegBlock - 1) / kSegBlock;
     HIPCHK(ps.d_head.ensure(nu));
     HIPCHK(c->hp_head[slot].ensure(nu));
-    if (c->p.bw > kSegBlock) return UP_E_INTERNAL;  // one thread per head position
     if (pool_mode(c) == 2)
         hipLaunchKernelGGL(seg_count_head_kernel<2>, dim3(nsb + nu), dim3(kSegBlock), 0, ps.stream, ps.d_info.p,
                            ps.d_cnt.p, ps.d_bsum.p, ns, nsb, c->d_units.p, (int)c->p.n_samples,

@@ -416,9 +416,8 @@ __device__ __forceinline__ void head_detect_unit(const UnitDesc *units, uint32_t
                                                  const int32_t *nc, const double *coef, int bw,
                                                  uint32_t *head, uint32_t *mirror) {
     const UnitDesc U = units[unit];
-    const int p = 1 + (int)threadIdx.x;
     uint32_t hit = 0;
-    if (p <= bw && (uint32_t)p <= U.len) {
+    for (int p = 1 + (int)threadIdx.x; p <= bw && (uint32_t)p <= U.len; p += blockDim.x) {
         for (int st = 0; st < U.nstrands; ++st) {
             double cs = 0.0;
             for (int k = 0; k < nnc; ++k) {
@@ -438,7 +437,7 @@ __device__ __forceinline__ void head_detect_unit(const UnitDesc *units, uint32_t
 }
 
 // K2a with the head detection in its trailing blocks (one block per unit;
-// threads 0..bw-1 = positions 1..bw): one launch fewer per pass
+// its threads stride over positions 1..bw): one launch fewer per pass
 template <int POOL>
 __global__ void __launch_bounds__(kSegBlock) seg_count_head_kernel(
     const uint64_t *__restrict__ info, uint64_t *__restrict__ cnt, uint64_t *__restrict__ bsum,

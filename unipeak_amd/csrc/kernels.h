@@ -41,8 +41,13 @@ constexpr int kChunkBytes = kChunk / kPerByte;    // bytes of one 16-position ch
 constexpr int kPadBytes = 256;      // zero bytes before position 1 and after the domain
 constexpr int kPadPos = kPerByte * kPadBytes;  // the same padding in positions
 constexpr int kStripBytes = kStrip / kPerByte;  // one strip of one track
-constexpr int kMaxBw = 255;         // register-resident halo: NH <= 4 words (wider: the replay)
-constexpr int kScrHalo = 16;        // K1a screen: chunks of halo on each side (kMaxBw / kChunk)
+constexpr int kMaxBw = 511;         // register-resident halo: NH <= 8 words (wider: the replay)
+// K1a screen: chunks of halo on each side -- kScrHalo places the halos in the
+// LDS layout and bounds the fine-screen weights; a kernel of window width NH
+// loads scr_halo(NH) of them (16 up to bw 255: the halo bytes a narrow
+// kernel streams stay 3 % of a strip)
+constexpr int kScrHalo = 32;        // kMaxBw / kChunk, rounded up
+__host__ __device__ constexpr int scr_halo(int nh) { return nh <= 4 ? 16 : 32; }
 constexpr int kCap = 32;            // inline run records per strip (starts, ends each)
 constexpr int kOvfHalf = kStrip / 2 + 1;  // max starts (= max ends) of one strip
 // record areas (uint32 words): starts [0,H), ends [H,2H), end-peak positions
@@ -98,7 +103,7 @@ struct ScanParams {
     const double *kern; // 2*bw+1 weights
     const uint32_t *wscreen;  // per non-control sample: integer weight >= |pooled share|
     uint32_t wskip;     // a window whose weighted tag sum is <= wskip cannot reach thr
-    float fw[kScrHalo + 1];  // fine screen: weight bound per chunk distance 0..16 (K1 screen_bits)
+    float fw[kScrHalo + 1];  // fine screen: weight bound per chunk distance 0..32 (K1 screen_bits)
     float fthr;         // a chunk whose weighted bound is <= fthr cannot reach thr
     int32_t bw;
     double thr;

@@ -115,6 +115,15 @@ __device__ __forceinline__ uint32_t fsum32(uint32_t x, uint32_t acc) {
     }
 }
 
+// K1a learns which tracks may hold an escape in a strip from the escape
+// tiles' index (scalar loads) rather than from the bytes (two VALU per
+// dword); UPK_ESC_VALU builds the byte test for A/B.  4-bit tracks: bytes.
+#ifdef UPK_ESC_VALU
+constexpr bool kScalarEsc = false;
+#else
+constexpr bool kScalarEsc = kTB == 2;
+#endif
+
 // bits of a dword that make the screen treat a chunk as exact: any escaped
 // field (2-bit: a field of 3; 4-bit: any count >= 8, the escape 15 among them)
 __device__ __forceinline__ uint32_t fbig32(uint32_t x) {
@@ -777,7 +786,8 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 #else
     constexpr bool kPf = true;
 #endif
-    constexpr int HL_ = kScrHalo * kChunkBytes / 16;  // halo lane loads per side (kScrHalo chunks)
+    constexpr int SH = scr_halo(NH);  // screen halo chunks this width loads on each side
+    constexpr int HL_ = SH * kChunkBytes / 16;  // halo lane loads per side (SH chunks)
     u32x4 pv[MODE == kModeScreen && !PROF ? kLoads : 1];
     u32x4 phv = {0u, 0u, 0u, 0u};
     uint32_t pf_strip = 0, pf_cur = 0;
@@ -840,9 +850,10 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             // lane l of wave load q holds 16 bytes = CPL chunks: chunks
             // CPL * (64q + l) + i, i < CPL (DPC dwords each)
             constexpr int CPL = 16 / kChunkBytes, DPC = kChunkBytes / 4;
-            constexpr int HL = kScrHalo * kChunkBytes / 16;  // halo lane loads per side (kScrHalo chunks)
+            constexpr int HL = SH * kChunkBytes / 16;  // halo lane loads per side (SH chunks)
             uint32_t cs[CPL * kLoads];
-            uint32_t big = 0, hs[CPL], hbig = 0, anybig = 0;
+            uint32_t big = 0, hs[CPL], hbig = 0;
+            bool any_esc = false;  // wave-uniform: some track may hold an escape (esc_tracks)
             // tracks (strand * nnc + k < 64) whose bytes in this strip hold an
             // escape; esc_far: one of the tracks beyond the first 64 does
             uint64_t esc_tracks = 0;
@@ -859,7 +870,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     u32x4 v[kLoads];
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) v[q] = pv[q];
-                    // halos: 8 chunks on each side, HL lanes per side
+                    // halos: SH chunks on each side, HL lanes per side
                     const u32x4 hv = phv;
                     pf_ok = false;
                     if (!kPf) {
@@ -873,7 +884,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                         pf_issue(it + istep, nc_, 0, 0);
                     }
                     const uint32_t w = POOL == 2 ? cptr(P.wscreen)[k] : 1u;
-                    uint32_t tbig = 0;  // this track's escape bits
+                    uint32_t tbig = 0;  // this track's escape bits (VALU detection)
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
                         const uint32_t d[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
@@ -885,7 +896,8 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
                             cs[CPL * q + i] = POOL == 2 ? cs[CPL * q + i] + a * w : a;
                         }
-                        tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
+                        if constexpr (!kScalarEsc)
+                            tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
                     }
                     {
                         const uint32_t d[4] = {hv.x, hv.y, hv.z, hv.w};
@@ -896,14 +908,37 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
                             hs[i] = POOL == 2 ? hs[i] + a * w : a;
                         }
-                        tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
+                        if constexpr (!kScalarEsc)
+                            tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
                     }
-                    if (__ballot((tbig & kBigMask) != 0u) != 0) {  // wave-uniform
+                    bool tesc;  // wave-uniform: this track may hold an escape in the strip or its halos
+                    if constexpr (kScalarEsc) {
+                        // the escape tiles of the strip's blocks and of both
+                        // neighbours (the halos reach into them) -- a tile
+                        // exists exactly where a block holds an escape -- read
+                        // with scalar loads instead of two VALU per dword
+                        tesc = false;
+                        if (U.ovf_tidx) {
+                            const uint32_t nb = ovf_nblk(U.len);
+                            const auto *tix = cptr((const uint32_t *)U.ovf_tidx) + (size_t)(st * S + ncs[k]) * nb;
+                            const int32_t b0 = (int32_t)(local * (uint32_t)(kStrip / kOvfBlk)) - 1;
+                            const int32_t lo = b0 < 0 ? 0 : b0;
+                            const int32_t hi = b0 + kStrip / (int)kOvfBlk + 1 < (int32_t)nb
+                                                   ? b0 + kStrip / (int)kOvfBlk + 1 : (int32_t)nb - 1;
+                            uint32_t all = ~0u;  // AND of the indices: ~0 (kNoTile) iff no tile
+#pragma unroll 2
+                            for (int32_t bb = lo; bb <= hi; ++bb) all &= tix[bb];
+                            tesc = all != kNoTile;
+                        }
+                    } else {
+                        tesc = __ballot((tbig & kBigMask) != 0u) != 0;
+                    }
+                    if (tesc) {
                         const int ti = st * P.nnc + k;
                         if (ti < 64) esc_tracks |= 1ull << ti;
                         else esc_far = true;
+                        any_esc = true;
                     }
-                    anybig |= tbig;
                 }
             }
             // Register pre-screen (no LDS): group g = lane l of load q holds
@@ -917,7 +952,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 #ifndef UPK_NO_K1A_DPP
             if constexpr (MODE == kModeScreen) {
                 const int D = (R + CPL - 1) / CPL;
-                if (D <= 2 && __ballot((anybig & kBigMask) != 0u) == 0) {
+                if (D <= 2 && !any_esc) {
                     uint32_t T[kLoads];
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
@@ -977,7 +1012,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             // chunks together -- two dependent round trips per piece, not per
             // escape.  Only strips where some lane saw an escape re-read
             // their bytes (L2).  (4-bit tracks: any count >= 8 goes exact.)
-            if (__ballot((anybig & kBigMask) != 0u) != 0) {
+            if (any_esc) {
                 constexpr bool kBound = kTB == 2 && POOL != 0;
                 constexpr int NP = kLoads + 1;  // the lane's strip pieces and its halo piece
                 const uint32_t nblk = ovf_nblk(U.len);
@@ -1076,7 +1111,8 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 for (int i = 0; i < CPL; ++i) d[i] = ((big >> (CPL * q + i)) & 1u) ? kBig : cs[CPL * q + i];
             }
             if (lane < 2 * HL) {
-                uint32_t *d = scr + scr_at(lane < HL ? CPL * lane : kScrHalo + kBlocks * kWave + CPL * (lane - HL));
+                uint32_t *d = scr + scr_at(lane < HL ? kScrHalo - SH + CPL * lane
+                                                     : kScrHalo + kBlocks * kWave + CPL * (lane - HL));
 #pragma unroll
                 for (int i = 0; i < CPL; ++i) d[i] = ((hbig >> i) & 1u) ? kBig : hs[i];
             }
@@ -1474,9 +1510,9 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 // unknown: K3 runs its KDE), so K2 and K3 follow unchanged.  A run starts at
 // a - bw for an add a with no add in [a - 2bw - 1, a - 1] and ends at a + bw
 // for an add with none in [a + 1, a + 2bw + 1].  One wave per strip: 64-
-// position presence words of the strip and a 4-word halo on each side (bw
-// <= 255), five words per lane; the previous / next add of every word by
-// wave scans.  2-bit tracks (the host checks).
+// position presence words of the strip and a kQHalo-word halo on each side
+// (bw <= kMaxBw), five words per lane; the previous / next add of every word
+// by wave scans.  2-bit tracks (the host checks).
 __device__ __forceinline__ uint64_t nz_bits64(u32x4 x) {
     auto c16 = [](uint32_t d) {  // nonzero 2-bit fields -> 16 bits
         uint32_t v = (d | (d >> 1)) & 0x55555555u;
@@ -1501,7 +1537,7 @@ __device__ __forceinline__ uint64_t range_bits(int64_t base, int64_t lo, int64_t
     return up & ~((1ull << a) - 1);
 }
 
-constexpr int kQHalo = 4;                                   // words of halo each side (bw <= 255)
+constexpr int kQHalo = (kMaxBw + 64) / 64;                  // words of halo each side (bw <= kMaxBw)
 constexpr int kQWords = kStrip / 64 + 2 * kQHalo;           // 264
 constexpr int kQRounds = (kQWords + kWave - 1) / kWave;     // 5
 

@@ -1,12 +1,12 @@
 // unipeak_amd/csrc/nh_tu.hip -- one translation unit per window width NH
-// (= ceil((bw + 1) / 64) words on each side, 1..4): compiled four times with
-// -DUPK_NH_TU=1..4, so the templated K1 / K3 / K4 kernels of the four widths
+// (= ceil((bw + 1) / 64) words on each side, 1..8): compiled eight times with
+// -DUPK_NH_TU=1..8, so the templated K1 / K3 / K4 kernels of the eight widths
 // build in parallel.  Each unit exports the addresses of its kernels; api.hip
 // launches them with hipLaunchKernel (kernels.hip holds the code).
 #include "kernels.hip"
 
 #ifndef UPK_NH_TU
-#error "compile with -DUPK_NH_TU=1..4"
+#error "compile with -DUPK_NH_TU=1..8"
 #endif
 
 #define UPK_CAT2(a, b) a##b
