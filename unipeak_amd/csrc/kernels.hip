@@ -115,15 +115,6 @@ __device__ __forceinline__ uint32_t fsum32(uint32_t x, uint32_t acc) {
     }
 }
 
-// K1a learns which tracks may hold an escape in a strip from the escape
-// tiles' index (scalar loads) rather than from the bytes (two VALU per
-// dword); UPK_ESC_VALU builds the byte test for A/B.  4-bit tracks: bytes.
-#ifdef UPK_ESC_VALU
-constexpr bool kScalarEsc = false;
-#else
-constexpr bool kScalarEsc = kTB == 2;
-#endif
-
 // bits of a dword that make the screen treat a chunk as exact: any escaped
 // field (2-bit: a field of 3; 4-bit: any count >= 8, the escape 15 among them)
 __device__ __forceinline__ uint32_t fbig32(uint32_t x) {
@@ -884,7 +875,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                         pf_issue(it + istep, nc_, 0, 0);
                     }
                     const uint32_t w = POOL == 2 ? cptr(P.wscreen)[k] : 1u;
-                    uint32_t tbig = 0;  // this track's escape bits (VALU detection)
+                    uint32_t tbig = 0;  // this track's escape bits
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
                         const uint32_t d[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
@@ -896,8 +887,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
                             cs[CPL * q + i] = POOL == 2 ? cs[CPL * q + i] + a * w : a;
                         }
-                        if constexpr (!kScalarEsc)
-                            tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
+                        tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
                     }
                     {
                         const uint32_t d[4] = {hv.x, hv.y, hv.z, hv.w};
@@ -908,31 +898,12 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
                             hs[i] = POOL == 2 ? hs[i] + a * w : a;
                         }
-                        if constexpr (!kScalarEsc)
-                            tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
+                        tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
                     }
-                    bool tesc;  // wave-uniform: this track may hold an escape in the strip or its halos
-                    if constexpr (kScalarEsc) {
-                        // the escape tiles of the strip's blocks and of both
-                        // neighbours (the halos reach into them) -- a tile
-                        // exists exactly where a block holds an escape -- read
-                        // with scalar loads instead of two VALU per dword
-                        tesc = false;
-                        if (U.ovf_tidx) {
-                            const uint32_t nb = ovf_nblk(U.len);
-                            const auto *tix = cptr((const uint32_t *)U.ovf_tidx) + (size_t)(st * S + ncs[k]) * nb;
-                            const int32_t b0 = (int32_t)(local * (uint32_t)(kStrip / kOvfBlk)) - 1;
-                            const int32_t lo = b0 < 0 ? 0 : b0;
-                            const int32_t hi = b0 + kStrip / (int)kOvfBlk + 1 < (int32_t)nb
-                                                   ? b0 + kStrip / (int)kOvfBlk + 1 : (int32_t)nb - 1;
-                            uint32_t all = ~0u;  // AND of the indices: ~0 (kNoTile) iff no tile
-#pragma unroll 2
-                            for (int32_t bb = lo; bb <= hi; ++bb) all &= tix[bb];
-                            tesc = all != kNoTile;
-                        }
-                    } else {
-                        tesc = __ballot((tbig & kBigMask) != 0u) != 0;
-                    }
+                    // wave-uniform: this track holds an escape in the strip or its halos
+                    // (reading the escape tiles' index with scalar loads instead
+                    // measured slower: K1a 0.34 -> 0.40 ms on configs[1])
+                    const bool tesc = __ballot((tbig & kBigMask) != 0u) != 0;
                     if (tesc) {
                         const int ti = st * P.nnc + k;
                         if (ti < 64) esc_tracks |= 1ull << ti;
