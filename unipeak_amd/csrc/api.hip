@@ -286,6 +286,7 @@ struct up_ctx {
     hipEvent_t host_work = nullptr;  // marks work on `stream` that a pass must follow
     DevBuf<uint32_t> d_resync, d_emu_n, d_emu_err, d_emu_counts, d_ring_hits, d_reg_hit, d_reg_hits;
     DevBuf<int32_t> d_unit_buffer;
+    DevBuf<uint32_t> d_gunits, d_goff;  // K0 chain groups (emulate_units)
     DevBuf<double> d_reg_f, d_reg_r;
     DevBuf<up_region> d_emu_out;
     DevBuf<double> d_ring_f, d_ring_r;   // K0 window in global memory (very wide kernels)
@@ -1273,21 +1274,64 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
     for (uint32_t i = 0; i < nu; ++i) ub[i] = c->units[i].buffer;
     HIPCHK(c->d_unit_buffer.ensure(nu));
     HIPCHK(hipMemcpy(c->d_unit_buffer.p, ub.data(), nu * sizeof(int32_t), hipMemcpyHostToDevice));
+    // chain groups (EmuParams::gunits): the whole buffer when every unit is
+    // replayed; otherwise a new group after every unit with an add past bw
+    // (it cannot leave state behind), so independent head-hit units replay in
+    // parallel instead of one wave walking the buffer
+    std::vector<uint32_t> aligned(nu, 0);
+    if (!replay_all && nu) {
+        HIPCHK(c->d_q11_head.ensure(nu));
+        HIPCHK(hipMemsetAsync(c->d_q11_head.p, 0, nu * sizeof(uint32_t), c->stream));
+        hipLaunchKernelGGL(unit_aligned_kernel, dim3(nu), dim3(256), 0, c->stream, c->d_units.p, S, (int)c->p.bw,
+                           c->d_q11_head.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(aligned.data(), c->d_q11_head.p, nu * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    std::vector<std::vector<uint32_t>> groups;
+    {
+        int64_t open[2] = {-1, -1};  // the buffer's current group
+        for (uint32_t u = 0; u < nu; ++u) {
+            const int b = c->units[u].buffer;
+            if (open[b] < 0) {
+                open[b] = (int64_t)groups.size();
+                groups.emplace_back();
+            }
+            groups[open[b]].push_back(u);
+            if (!replay_all && aligned[u]) open[b] = -1;
+        }
+    }
+    std::vector<uint32_t> gunits, goff{0};
+    for (const auto &g : groups) {
+        gunits.insert(gunits.end(), g.begin(), g.end());
+        goff.push_back((uint32_t)gunits.size());
+    }
+    const uint32_t ngroups = (uint32_t)groups.size();
+    HIPCHK(c->d_gunits.ensure(std::max<size_t>(gunits.size(), 1)));
+    HIPCHK(c->d_goff.ensure(goff.size()));
+    if (!gunits.empty())
+        HIPCHK(hipMemcpy(c->d_gunits.p, gunits.data(), gunits.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_goff.p, goff.data(), goff.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(c->d_resync.ensure(nu));
     HIPCHK(c->d_emu_n.ensure(1));
     HIPCHK(c->d_emu_err.ensure(1));
-    HIPCHK(c->d_ring_hits.ensure(2ull * W * S));
     // the window in LDS when it fits (64 KiB), else in global scratch
     const size_t ring_bytes = (size_t)W * (2 * sizeof(double) + 1);
     const bool ring_lds = ring_bytes <= 65536 - 64;
-    if (!ring_lds) {
-        HIPCHK(c->d_ring_f.ensure(2ull * W));
-        HIPCHK(c->d_ring_r.ensure(2ull * W));
-        HIPCHK(c->d_ring_has.ensure(2ull * W));
-    }
     for (int attempt = 0;; ++attempt) {
         if (attempt == 6) return UP_E_NOMEM;
         const uint32_t reg_cap = c->emu_reg_cap, out_cap = c->emu_out_cap;
+        // workgroups (scratch slots): every group at once, within ~1 GiB of scratch
+        const uint64_t slot_bytes = (uint64_t)W * S * 4 + (uint64_t)reg_cap * (8 + 8 + 4 + 4ull * S) +
+                                    (ring_lds ? 0 : (uint64_t)W * 17);
+        const uint32_t nslots = (uint32_t)std::max<uint64_t>(
+            1, std::min<uint64_t>({(uint64_t)std::max(ngroups, 1u), 256, (1ull << 30) / std::max<uint64_t>(slot_bytes, 1)}));
+        HIPCHK(c->d_ring_hits.ensure((uint64_t)nslots * W * S));
+        if (!ring_lds) {
+            HIPCHK(c->d_ring_f.ensure((uint64_t)nslots * W));
+            HIPCHK(c->d_ring_r.ensure((uint64_t)nslots * W));
+            HIPCHK(c->d_ring_has.ensure((uint64_t)nslots * W));
+        }
         HIPCHK(hipMemsetAsync(c->d_resync.p, 0, nu * sizeof(uint32_t), c->stream));
         HIPCHK(hipMemsetAsync(c->d_emu_n.p, 0, 4, c->stream));
         HIPCHK(hipMemsetAsync(c->d_emu_err.p, 0, 4, c->stream));
@@ -1296,20 +1340,23 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
         HIPCHK(c->d_emu_scores.ensure(c->emu_scores_cap));
         HIPCHK(c->d_emu_score_off.ensure(out_cap));
         if (!ring_lds) {
-            HIPCHK(hipMemsetAsync(c->d_ring_f.p, 0, 2ull * W * sizeof(double), c->stream));
-            HIPCHK(hipMemsetAsync(c->d_ring_r.p, 0, 2ull * W * sizeof(double), c->stream));
-            HIPCHK(hipMemsetAsync(c->d_ring_has.p, 0, 2ull * W, c->stream));
+            HIPCHK(hipMemsetAsync(c->d_ring_f.p, 0, (uint64_t)nslots * W * sizeof(double), c->stream));
+            HIPCHK(hipMemsetAsync(c->d_ring_r.p, 0, (uint64_t)nslots * W * sizeof(double), c->stream));
+            HIPCHK(hipMemsetAsync(c->d_ring_has.p, 0, (uint64_t)nslots * W, c->stream));
         }
         HIPCHK(c->d_emu_out.ensure(out_cap));
         HIPCHK(c->d_emu_counts.ensure((size_t)out_cap * S));
-        HIPCHK(c->d_reg_f.ensure(2ull * reg_cap));
-        HIPCHK(c->d_reg_r.ensure(2ull * reg_cap));
-        HIPCHK(c->d_reg_hit.ensure(2ull * reg_cap));
-        HIPCHK(c->d_reg_hits.ensure(2ull * reg_cap * S));
+        HIPCHK(c->d_reg_f.ensure((uint64_t)nslots * reg_cap));
+        HIPCHK(c->d_reg_r.ensure((uint64_t)nslots * reg_cap));
+        HIPCHK(c->d_reg_hit.ensure((uint64_t)nslots * reg_cap));
+        HIPCHK(c->d_reg_hits.ensure((uint64_t)nslots * reg_cap * S));
         EmuParams E{};
         E.units = c->d_units.p;
         E.nunits = nu;
         E.unit_buffer = c->d_unit_buffer.p;
+        E.gunits = c->d_gunits.p;
+        E.goff = c->d_goff.p;
+        E.ngroups = ngroups;
         E.unit_head = d_head;
         E.S = S;
         E.nnc = (int32_t)c->nc.size();
@@ -1360,7 +1407,7 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
             E.nprof = c->d_pf_n.p;
             E.prof_cap = c->pf_cap;
         }
-        hipLaunchKernelGGL(emulate_kernel, dim3(2), dim3(64), ring_lds ? ring_bytes : 0, c->stream, E);
+        hipLaunchKernelGGL(emulate_kernel, dim3(nslots), dim3(64), ring_lds ? ring_bytes : 0, c->stream, E);
         HIPCHK(hipGetLastError());
         uint32_t nemu = 0, err = 0;
         resync.assign(nu, 0);

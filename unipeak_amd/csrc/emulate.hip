@@ -25,6 +25,12 @@ struct EmuParams {
     const UnitDesc *units;
     uint32_t nunits;
     const int32_t *unit_buffer;
+    // chain groups: group g = units gunits[goff[g] .. goff[g + 1]) of one
+    // buffer in its order; groups are independent (each starts from a fresh
+    // buffer state), so workgroups take them in parallel (scratch per
+    // workgroup slot)
+    const uint32_t *gunits, *goff;
+    uint32_t ngroups;
     const uint32_t *unit_head;   // 1: unit has a head hit
     int32_t S, nnc;
     const int32_t *nc;
@@ -41,7 +47,7 @@ struct EmuParams {
     uint32_t *out_counts;
     uint32_t *nout;
     uint32_t out_cap;
-    // scratch per buffer (index = buffer id)
+    // scratch per workgroup slot (index = blockIdx.x)
     uint32_t *ring_hits;         // [2][W][S]
     double *reg_f, *reg_r;       // [2][reg_cap]
     uint32_t *reg_hit;           // [2][reg_cap] index into reg_hits or 0xFFFFFFFF
@@ -300,7 +306,7 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
     extern __shared__ double emu_lds[];  // the window when P.ring_lds: rf[W], rr[W], rhas[W]
     __shared__ int stop_flag;
     const int lane = threadIdx.x;
-    const int buffer = blockIdx.x;
+    const int buffer = blockIdx.x;  // scratch slot
     const int S = P.S;
     EmuState E;
     E.W = 2 * P.bw + 1;
@@ -321,9 +327,10 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
     E.ghit = P.reg_hit + (uint64_t)buffer * P.reg_cap;
     E.ghits = P.reg_hits + (uint64_t)buffer * P.reg_cap * S;
 
+    for (uint32_t g = blockIdx.x; g < P.ngroups; g += gridDim.x) {
     bool in_chain = false;
-    for (uint32_t u = 0; u < P.nunits; ++u) {
-        if (P.unit_buffer[u] != buffer) continue;
+    for (uint32_t gk = P.goff[g]; gk < P.goff[g + 1]; ++gk) {
+        const uint32_t u = P.gunits[gk];
         if (!in_chain) {
             if (!P.unit_head[u]) continue;
             // chain start: fresh buffer state (the previous unit ended clean)
@@ -407,6 +414,28 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
         __syncthreads();
         if (stop_flag) in_chain = false;
         __syncthreads();
+    }
+    }  // groups
+}
+
+// a unit with an add() past bw cannot end its pass dirty (quirk Q1 leaks
+// need every add at <= bw), so the buffer's next unit starts a new chain
+// group.  One block per unit scans from bw + 1 until it finds a tag of any
+// track (typically within a few hundred positions).
+__global__ void __launch_bounds__(256) unit_aligned_kernel(const UnitDesc *units, int S, int bw, uint32_t *flag) {
+    const UnitDesc U = units[blockIdx.x];
+    for (uint64_t base = (uint64_t)bw + 1; base <= U.len; base += 4096) {
+        bool any = false;
+        for (int i = 0; i < 16; ++i) {
+            const uint64_t p = base + (uint64_t)threadIdx.x * 16 + i;
+            if (p > U.len) break;
+            for (int st = 0; st < U.nstrands && !any; ++st)
+                for (int k = 0; k < S && !any; ++k) any = fld_at(track_u8(U, S, st, k), (int64_t)p) != 0u;
+        }
+        if (__syncthreads_or(any)) {
+            if (threadIdx.x == 0) flag[blockIdx.x] = 1u;
+            return;
+        }
     }
 }
 
