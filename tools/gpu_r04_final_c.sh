@@ -3,6 +3,8 @@
 # side of the scaling runs), and the 8-rank rehearsal (records vs N=1)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:?}"; F=$R/gpurun_out/${1:-final_c}; mkdir -p "$F"; cd "$R" || exit 1
+timeout -k 10 300 python bench.py --workload hg19-shift --steps 10 --warmup 2 > "$F/bench_hg19-shift.json" 2> "$F/bench_hg19-shift.err" || exit 1
+python -c "import json; d=json.load(open('$F/bench_hg19-shift.json')); print('shift', d['value'], d['ms_per_step'], d['phases_ms'])"
 for w in hg19-dir1 hg19-8s1c hg19mm9-32rep; do
   st=200; [ $w = hg19-dir1 ] || st=20
   for r in 0 1 2 3 4 5 6 7; do
