@@ -432,8 +432,8 @@ def main():
     if final is not None and dump:  # rehearsals: the merged records of the last step
         blocks, _, _ = border.blocks(final[1])
         recs = [b.copy() for _, b, _ in blocks]
-        for (g, _, _), r in zip(blocks, recs):
-            r["unit"] = g  # rank-local unit id -> global unit id
+        for (gunit, _, _), r in zip(blocks, recs):
+            r["unit"] = gunit  # rank-local unit id -> global unit id
         np.savez(dump, recs=np.concatenate(recs) if recs else np.zeros(0, capi.REGION_DTYPE),
                  counts=np.concatenate([c for _, _, c in blocks]) if blocks else np.zeros((0, S), np.uint32))
     if final is not None:  # the last step's records: accepted count (outside the timing)
