@@ -195,3 +195,82 @@ def test_run_edge_on_strip_boundary(gpu_lib, oracle, want):
     ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt)
     regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos, cnt)
     compare(ref, ref_sums, regs, gcnt)
+
+
+def _isolated_escapes(length, where, counts):
+    dense = {}
+    for p, c in zip(where, counts):
+        if 1 <= p <= length:
+            dense[int(p)] = dense.get(int(p), 0) + int(c)
+    pos = np.array(sorted(dense), np.uint32)
+    return pos, np.array([[dense[int(p)]] for p in pos], np.uint32)
+
+
+@pytest.mark.parametrize("bg_tags", [False, True])
+def test_isolated_escapes_strip_halo_block_edges(gpu_lib, oracle, bg_tags):
+    """K1a's one-track screen bounds a strip's tags by 2 x popcount of its
+    bytes, which an escaped field (count >= 3, stored as 3) breaks: the
+    escape bitmap (ScanParams::esc) must send every strip whose bytes or
+    halos hold one down the exact path.  Lone escapes in otherwise empty
+    strips -- interior, on strip and block edges, and in the halo only
+    (the first / last positions of the neighbouring strip) -- on the second
+    unit of the context (global strip numbers != local ones)."""
+    rng = np.random.default_rng(31 + bg_tags)
+    bw, bg = 50, 0.003
+    lens = [40_000, 200_000]
+    S = 16384
+    where = [3 * S // 2, S, S + 1, 2 * S - 120, 2 * S + 100, 3 * S + 1023, 3 * S + 1024, 5 * S + 7,
+             7 * S - 40, 8 * S + 30, 1024 * 100, 1024 * 150 + 1]
+    counts = [3, 4, 9, 40, 300, 70_000, 5, 12, 1000, 6, 255, 256]
+    with gpu_lib.Lib(0) as g:
+        g.set_params(bw, 1, bg)
+        units = [g.add_unit(L) for L in lens]
+        data = []
+        for u, L in zip(units, lens):
+            if u == units[0]:
+                pos, cnt = random_unit(rng, L, bw)
+            else:
+                pos, cnt = _isolated_escapes(L, where, counts)
+                if bg_tags:  # sparse background tags as well (no escapes among them)
+                    extra = rng.choice(np.arange(2 * bw + 2, L - 2 * bw), size=300, replace=False)
+                    d = {int(p): int(c[0]) for p, c in zip(pos, cnt)}
+                    for p in extra:
+                        d[int(p)] = d.get(int(p), 0) + 1
+                    pos = np.array(sorted(d), np.uint32)
+                    cnt = np.array([[d[int(p)]] for p in pos], np.uint32)
+            g.scatter(u, 0, 0, pos, cnt[:, 0])
+            data.append((pos, cnt))
+        n = g.run()
+        regs, gcnt = g.regions(n)
+        regs, gcnt = regs.copy(), gcnt.copy()
+    refs = [oracle.run_unit(bw, bg, p, c) for p, c in data]
+    ref = np.concatenate([r for r, _ in refs])
+    ref_sums = np.concatenate([s for _, s in refs])
+    compare(ref, ref_sums, regs, gcnt)
+    assert int(np.count_nonzero(regs["unit"] == units[1])) >= 8
+
+
+def test_escape_added_after_a_run(gpu_lib, oracle):
+    """the escape bitmap follows the tracks: an escape scattered into a
+    strip that was clean in an earlier pass (and one removed) changes the
+    next pass's regions exactly as the oracle's"""
+    bw, bg, L = 50, 0.003, 150_000
+    pos0, cnt0 = _isolated_escapes(L, [20_000], [500])
+    with gpu_lib.Lib(0) as g:
+        g.set_params(bw, 1, bg)
+        u = g.add_unit(L)
+        g.scatter(u, 0, 0, pos0, cnt0[:, 0])
+        n0 = g.run()
+        r0 = g.regions(n0)[0].copy()
+        # add escapes in strips that held nothing, remove the first
+        g.scatter(u, 0, 0, np.array([20_000, 70_000, 16384 * 6], np.uint32),
+                  np.array([0, 800, 3], np.uint32))
+        n1 = g.run()
+        r1, c1 = g.regions(n1)
+        r1, c1 = r1.copy(), c1.copy()
+    ref0, _ = oracle.run_unit(bw, bg, pos0, cnt0)
+    assert np.array_equal(ref0["left"], r0["left"]) and len(r0) == 1
+    pos1, cnt1 = _isolated_escapes(L, [70_000, 16384 * 6], [800, 3])
+    ref1, s1 = oracle.run_unit(bw, bg, pos1, cnt1)
+    compare(ref1, s1, r1, c1)
+    assert 70_000 >= r1["left"][0] and len(r1) >= 1

@@ -215,6 +215,10 @@ struct up_ctx {
     DevBuf<UnitDesc> d_units;
     uint32_t nstrips = 0;
     int bw_layout = -1;  // bw the strip layout was computed for
+    // per (track slot strand * S + sample, global strip): the strip or its
+    // halo blocks hold an escape (ScanParams::esc, K1a's cheap bound)
+    DevBuf<uint32_t> d_esc;
+    uint32_t esc_nw = 0;
     DevBuf<uint32_t> d_unit_last;
     uint32_t k1a_waves = 0, k1a_xcap = 0;  // grid and per-wave stash size of the last K1a launch
     uint32_t ovf_cap = 256;
@@ -1049,6 +1053,31 @@ static int sync_units(up_ctx *c) {
     c->nstrips = strip;
     c->ovf_max_all = 0;
     for (const Unit &u : c->units) c->ovf_max_all = std::max(c->ovf_max_all, u.ovf_max);
+    {
+        // escape bitmap: bit (strip) of row (strand * S + sample) is set when
+        // a block of the strip, or the block either side (the screen's halos,
+        // <= kScrHalo chunks < kOvfBlk), holds an escaped field of that track
+        const uint32_t S = (uint32_t)std::max<int32_t>(1, (int32_t)c->p.n_samples);
+        const uint32_t nw = (strip + 31) / 32;
+        std::vector<uint32_t> esc((size_t)2 * S * nw, 0u);
+        auto set = [&](size_t row, uint32_t g) { esc[row * nw + (g >> 5)] |= 1u << (g & 31); };
+        for (const Unit &u : c->units) {
+            for (size_t t = 0; t < u.ovf.size() && t < (size_t)2 * S; ++t) {
+                for (const auto &kv : u.ovf[t]) {
+                    const uint32_t kb = (uint32_t)((kv.first - 1) >> kOvfBlkShift);
+                    const uint32_t local = kb / kBlocks;
+                    if (local >= u.nstrips) continue;  // past the scan domain (cannot happen)
+                    set(t, u.strip0 + local);
+                    if (kb % kBlocks == 0 && local > 0) set(t, u.strip0 + local - 1);
+                    if (kb % kBlocks == kBlocks - 1 && local + 1 < u.nstrips) set(t, u.strip0 + local + 1);
+                }
+            }
+        }
+        HIPCHK(c->d_esc.ensure(std::max<size_t>(esc.size(), 1)));
+        if (!esc.empty())
+            HIPCHK(hipMemcpy(c->d_esc.p, esc.data(), esc.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        c->esc_nw = nw;
+    }
     HIPCHK(c->d_units.ensure(d.size()));
     HIPCHK(hipMemcpy(c->d_units.p, d.data(), d.size() * sizeof(UnitDesc), hipMemcpyHostToDevice));
     c->units_dirty = false;
@@ -1095,6 +1124,8 @@ static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps, uint32_t ovf_cap) {
     P.qmode = q_mode(c) ? 1 : 0;
     P.qno = c->qno;
     P.qyes = c->qyes;
+    P.esc = c->esc_nw ? c->d_esc.p : nullptr;
+    P.esc_nw = c->esc_nw;
     return P;
 }
 

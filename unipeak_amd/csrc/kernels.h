@@ -65,6 +65,7 @@ constexpr uint32_t kBig = 1u << 22; // screen value of a chunk holding an escape
 // searches one block's entries instead of the whole track's
 constexpr uint32_t kOvfBlkShift = 10, kOvfBlk = 1u << kOvfBlkShift;
 __host__ __device__ inline uint32_t ovf_nblk(uint32_t len) { return (len + kOvfBlk - 1) >> kOvfBlkShift; }
+static_assert(kStepWords * kWave == (int)kOvfBlk, "an overflow block is one scan block (escape bitmap per strip)");
 
 struct UnitDesc {
     uint64_t base;      // device address of track (0, 0)
@@ -132,6 +133,12 @@ struct ScanParams {
     // proves score >= thr; only words with a lane in between run the FP64 walk
     int32_t qmode;
     uint32_t qno, qyes;
+    // escape bitmap: bit g of row (strand * S + sample) = global strip g or
+    // its halo blocks hold an escaped field of that track (null: unknown, so
+    // every strip counts as escaped).  K1a's one-track screen bounds a
+    // strip's tags by 2 x popcount of its bytes, valid without escapes only
+    const uint32_t *esc;
+    uint32_t esc_nw;        // words per row
 #if defined(UPK_DEBUG_COUNTS) || defined(UPK_DEBUG_TIMES)
     unsigned long long *dbg;  // counters: exact blocks, live words
 #endif

@@ -115,6 +115,14 @@ __device__ __forceinline__ uint32_t fsum32(uint32_t x, uint32_t acc) {
     }
 }
 
+// popcount(x) + acc in one v_bcnt (K1a's one-track bound: 2 x popcount of a
+// 2-bit field >= its value unless the field is an escape)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm volatile("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+
 // bits of a dword that make the screen treat a chunk as exact: any escaped
 // field (2-bit: a field of 3; 4-bit: any count >= 8, the escape 15 among them)
 __device__ __forceinline__ uint32_t fbig32(uint32_t x) {
@@ -779,11 +787,27 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 #endif
     constexpr int SH = scr_halo(NH);  // screen halo chunks this width loads on each side
     constexpr int HL_ = SH * kChunkBytes / 16;  // halo lane loads per side (SH chunks)
+    // One directional track (configs[1]): the register pre-screen runs on
+    // an upper bound of the tags, 2 x popcount of each dword (a 2-bit field
+    // f <= 2 popcount(f) unless f is an escape), one v_bcnt per dword instead
+    // of the chunk sums and escape bits (five VALU per dword); a strip whose
+    // bound is clean and whose escape bit (ScanParams::esc, loaded with the
+    // prefetch) is clear is done.  The others compute the exact sums from the
+    // same registers and go on as below.
+#ifdef UPK_NO_K1A_CHEAP  // A/B: every track's chunk sums and escape bits first
+    constexpr bool kCheap = false;
+#else
+    constexpr bool kCheap = MODE == kModeScreen && !PROF && POOL == 0 && !NONDIR && kTB == 2 && kPf;
+#endif
     u32x4 pv[MODE == kModeScreen && !PROF ? kLoads : 1];
     u32x4 phv = {0u, 0u, 0u, 0u};
     uint32_t pf_strip = 0, pf_cur = 0;
     int pf_st = 0, pf_k = 0;
     bool pf_ok = false;
+    // kCheap: the prefetched strip's word of the escape bitmap and its bit
+    // (the bit is taken when the strip is screened, so the scalar load's
+    // wait lands a strip later)
+    uint32_t pf_escw = ~0u, pf_escb = 0;
     auto pf_issue = [&](uint32_t strip_n, uint32_t cur_n, int st, int k) {
         const UnitDesc Un = units[cur_n];
         const int64_t q0 = 1 + (int64_t)(strip_n - Un.strip0) * kStrip;
@@ -793,6 +817,11 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             pv[q] = __builtin_nontemporal_load(t + 64 * q + lane);
         phv = u32x4{0u, 0u, 0u, 0u};
         if (lane < 2 * HL_) phv = t[lane < HL_ ? lane - HL_ : kLoads * kWave + lane - HL_];
+        if constexpr (kCheap) {
+            const uint32_t *eb = cptr(P.esc);
+            pf_escw = eb ? eb[(size_t)(st * S + ncs[k]) * P.esc_nw + (strip_n >> 5)] : ~0u;
+            pf_escb = strip_n & 31u;
+        }
         pf_strip = strip_n;
         pf_cur = cur_n;
         pf_st = st;
@@ -853,7 +882,94 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             for (int k = 0; k < CPL * kLoads; ++k) cs[k] = 0;
 #pragma unroll
             for (int i = 0; i < CPL; ++i) hs[i] = 0;
-            for (int st = 0; st < (NONDIR ? 2 : 1); ++st) {
+            bool clean = false;
+            // the pre-screen bound of every lane: max over its groups of the
+            // tags of groups g-D .. g+D, plus both halos (below)
+            auto pre_bound = [&](const uint32_t (&T)[kLoads], uint32_t hl) -> uint32_t {
+                const int D = (R + CPL - 1) / CPL;
+                uint32_t htot = 0;  // both halos (lanes 0 .. 2HL-1)
+#pragma unroll
+                for (int l = 0; l < 2 * HL; ++l) htot += rl_u(hl, l);
+                uint32_t l1[kLoads], r1[kLoads], bmax = 0;
+#pragma unroll
+                for (int q = 0; q < kLoads; ++q) {
+                    l1[q] = dpp32<0x138, 0xf, false>(0u, T[q]);  // wave_shr:1 -> T(g - 1)
+                    r1[q] = dpp32<0x130, 0xf, false>(0u, T[q]);  // wave_shl:1 -> T(g + 1)
+                    const uint32_t lf = q > 0 ? rl_u(T[q > 0 ? q - 1 : 0], 63) : 0u;
+                    const uint32_t rf = q + 1 < kLoads ? rl_u(T[q + 1 < kLoads ? q + 1 : q], 0) : 0u;
+                    l1[q] = lane == 0 ? lf : l1[q];
+                    r1[q] = lane == 63 ? rf : r1[q];
+                }
+#pragma unroll
+                for (int q = 0; q < kLoads; ++q) {
+                    uint32_t b = T[q] + l1[q] + r1[q];
+                    if (D == 2) {
+                        uint32_t l2 = dpp32<0x138, 0xf, false>(0u, l1[q]);  // T(g - 2)
+                        uint32_t r2 = dpp32<0x130, 0xf, false>(0u, r1[q]);  // T(g + 2)
+                        const uint32_t lf = q > 0 ? rl_u(l1[q > 0 ? q - 1 : 0], 63) : 0u;
+                        const uint32_t rf = q + 1 < kLoads ? rl_u(r1[q + 1 < kLoads ? q + 1 : q], 0) : 0u;
+                        l2 = lane == 0 ? lf : l2;
+                        r2 = lane == 63 ? rf : r2;
+                        b += l2 + r2;
+                    }
+                    bmax = b > bmax ? b : bmax;
+                }
+                return bmax + htot;
+            };
+            if constexpr (kCheap) {
+                u32x4 v[kLoads];
+#pragma unroll
+                for (int q = 0; q < kLoads; ++q) v[q] = pv[q];
+                const u32x4 hv = phv;
+                const bool mesc = (pf_escw >> pf_escb) & 1u;
+                pf_ok = false;
+                if (it + istep < it_end) {
+                    uint32_t nc_ = cur;
+                    while (it + istep >= units[nc_].strip0 + units[nc_].nstrips) ++nc_;
+                    pf_issue(it + istep, nc_, 0, 0);
+                }
+#ifndef UPK_NO_K1A_DPP
+                if (!mesc && (R + CPL - 1) / CPL <= 2) {
+                    uint32_t T[kLoads];
+#pragma unroll
+                    for (int q = 0; q < kLoads; ++q)
+                        T[q] = bcnt_acc(v[q].w, bcnt_acc(v[q].z, bcnt_acc(v[q].y, bcnt_acc(v[q].x, 0u))));
+                    const uint32_t hl = bcnt_acc(hv.w, bcnt_acc(hv.z, bcnt_acc(hv.y, bcnt_acc(hv.x, 0u))));
+                    clean = __ballot(2u * pre_bound(T, hl) > P.wskip) == 0;
+                }
+#endif
+                if (!clean) {  // the exact chunk sums and escape bits of the same registers
+                    uint32_t tbig = 0;
+#pragma unroll
+                    for (int q = 0; q < kLoads; ++q) {
+                        const uint32_t d[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                        for (int i = 0; i < CPL; ++i) {
+                            uint32_t a = 0;
+#pragma unroll
+                            for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
+                            cs[CPL * q + i] = a;
+                        }
+                        tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
+                    }
+                    {
+                        const uint32_t d[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+                        for (int i = 0; i < CPL; ++i) {
+                            uint32_t a = 0;
+#pragma unroll
+                            for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
+                            hs[i] = a;
+                        }
+                        tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
+                    }
+                    if (__ballot((tbig & kBigMask) != 0u) != 0) {
+                        esc_tracks = 1;
+                        any_esc = true;
+                    }
+                }
+            }
+            for (int st = 0; st < (kCheap ? 0 : NONDIR ? 2 : 1); ++st) {
                 for (int k = 0; k < P.nnc; ++k) {
                     // this track's loads were issued one step ahead (pf_issue);
                     // issue the next (strip, track)'s before reducing these
@@ -919,11 +1035,9 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             // readlane) plus both halos bounds it.  Background strips -- most
             // of the genome -- end here; the others (and any escaped field,
             // whose count the screen does not know) take the LDS screen below.
-            bool clean = false;
 #ifndef UPK_NO_K1A_DPP
             if constexpr (MODE == kModeScreen) {
-                const int D = (R + CPL - 1) / CPL;
-                if (D <= 2 && !any_esc) {
+                if (!clean && (R + CPL - 1) / CPL <= 2 && !any_esc) {
                     uint32_t T[kLoads];
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
@@ -934,34 +1048,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     uint32_t hl = 0;
 #pragma unroll
                     for (int i = 0; i < CPL; ++i) hl += hs[i];
-                    uint32_t htot = 0;  // both halos (lanes 0 .. 2HL-1)
-#pragma unroll
-                    for (int l = 0; l < 2 * HL; ++l) htot += rl_u(hl, l);
-                    uint32_t l1[kLoads], r1[kLoads], bmax = 0;
-#pragma unroll
-                    for (int q = 0; q < kLoads; ++q) {
-                        l1[q] = dpp32<0x138, 0xf, false>(0u, T[q]);  // wave_shr:1 -> T(g - 1)
-                        r1[q] = dpp32<0x130, 0xf, false>(0u, T[q]);  // wave_shl:1 -> T(g + 1)
-                        const uint32_t lf = q > 0 ? rl_u(T[q > 0 ? q - 1 : 0], 63) : 0u;
-                        const uint32_t rf = q + 1 < kLoads ? rl_u(T[q + 1 < kLoads ? q + 1 : q], 0) : 0u;
-                        l1[q] = lane == 0 ? lf : l1[q];
-                        r1[q] = lane == 63 ? rf : r1[q];
-                    }
-#pragma unroll
-                    for (int q = 0; q < kLoads; ++q) {
-                        uint32_t b = T[q] + l1[q] + r1[q];
-                        if (D == 2) {
-                            uint32_t l2 = dpp32<0x138, 0xf, false>(0u, l1[q]);  // T(g - 2)
-                            uint32_t r2 = dpp32<0x130, 0xf, false>(0u, r1[q]);  // T(g + 2)
-                            const uint32_t lf = q > 0 ? rl_u(l1[q > 0 ? q - 1 : 0], 63) : 0u;
-                            const uint32_t rf = q + 1 < kLoads ? rl_u(r1[q + 1 < kLoads ? q + 1 : q], 0) : 0u;
-                            l2 = lane == 0 ? lf : l2;
-                            r2 = lane == 63 ? rf : r2;
-                            b += l2 + r2;
-                        }
-                        bmax = b > bmax ? b : bmax;
-                    }
-                    clean = __ballot(bmax + htot > P.wskip) == 0;
+                    clean = __ballot(pre_bound(T, hl) > P.wskip) == 0;
                 }
             }
 #endif
