@@ -864,6 +864,9 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         const UnitDesc U = units[cur];
         const uint32_t local = strip - U.strip0;
         const int64_t p0 = 1 + (int64_t)local * kStrip;  // first position of the strip
+#ifdef UPK_AB_SKIP_K1B  // upper-bound experiment only (wrong regions): K1b's blocks cost nothing
+        if constexpr (MODE == kModeExact) exact_blocks = 0;
+#endif
 
         // ---- screen: which blocks can hold a flagged position ----
         if constexpr (!PROF && MODE != kModeExact) {
@@ -1968,6 +1971,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
     // dependent round trip behind the streaming loads on every strip)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+#ifdef UPK_AB_SKIP_K3  // upper-bound experiment only (no records): K3 costs nothing
+    return;
+#endif
     const uint64_t nreg = *P.nreg < P.cap ? *P.nreg : P.cap;
     uint64_t wm[2 * NH + 1];
 #pragma unroll
