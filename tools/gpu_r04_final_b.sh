@@ -13,4 +13,6 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD
 UNIPEAK_SIM_WORLD=8 UNIPEAK_SIM_RANK=0 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$F/sim_fetch" -o p -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$F/sim_fetch.log" 2>&1 || exit 1
 UNIPEAK_SIM_WORLD=8 UNIPEAK_SIM_RANK=0 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$F/sim_write" -o p -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$F/sim_write.log" 2>&1 || exit 1
 tail -1 "$F/sim_fetch.log" | cut -c1-200
+python3 "$R/tools/sq_summary.py" "$F/sq_counters.json" "rocprofv3 --pmc SQ counters per launch (mean over the bench passes; two passes of 8 counters), hg19 configs[1]" "$F/pmc_a" "$F/pmc_b" || exit 1
+cp "$F"/trace/*kernel_stats.csv "$F/bench_kernel_stats.csv" 2>/dev/null || cp "$(ls "$F"/trace/*/*kernel_stats.csv | head -1)" "$F/bench_kernel_stats.csv"
 echo final-b-ok
