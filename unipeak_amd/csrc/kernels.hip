@@ -787,13 +787,13 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 #endif
     constexpr int SH = scr_halo(NH);  // screen halo chunks this width loads on each side
     constexpr int HL_ = SH * kChunkBytes / 16;  // halo lane loads per side (SH chunks)
-    // One directional track (configs[1]): the register pre-screen runs on
-    // an upper bound of the tags, 2 x popcount of each dword (a 2-bit field
-    // f <= 2 popcount(f) unless f is an escape), one v_bcnt per dword instead
-    // of the chunk sums and escape bits (five VALU per dword); a strip whose
-    // bound is clean and whose escape bit (ScanParams::esc, loaded with the
-    // prefetch) is clear is done.  The others compute the exact sums from the
-    // same registers and go on as below.
+    // One directional track (configs[1]): the strip's escape bit
+    // (ScanParams::esc, its word loaded with the prefetch) replaces the
+    // per-dword escape test (two VALU per dword) when it is clear; the exact
+    // chunk sums stay (the pre-screen needs them: configs[1]'s wskip is ~4
+    // tags).  UPK_K1A_BOUND2 (A/B): a first pre-screen on 2 x popcount of
+    // each dword, one v_bcnt per dword -- it fails on most strips at
+    // configs[1]'s threshold and then costs both.
 #ifdef UPK_NO_K1A_CHEAP  // A/B: every track's chunk sums and escape bits first
     constexpr bool kCheap = false;
 #else
@@ -931,7 +931,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     while (it + istep >= units[nc_].strip0 + units[nc_].nstrips) ++nc_;
                     pf_issue(it + istep, nc_, 0, 0);
                 }
-#ifndef UPK_NO_K1A_DPP
+#if !defined(UPK_NO_K1A_DPP) && defined(UPK_K1A_BOUND2)
                 if (!mesc && (R + CPL - 1) / CPL <= 2) {
                     uint32_t T[kLoads];
 #pragma unroll
@@ -941,8 +941,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     clean = __ballot(2u * pre_bound(T, hl) > P.wskip) == 0;
                 }
 #endif
-                if (!clean) {  // the exact chunk sums and escape bits of the same registers
-                    uint32_t tbig = 0;
+                if (!clean) {  // the exact chunk sums of the same registers
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
                         const uint32_t d[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
@@ -953,7 +952,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
                             cs[CPL * q + i] = a;
                         }
-                        tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
                     }
                     {
                         const uint32_t d[4] = {hv.x, hv.y, hv.z, hv.w};
@@ -964,11 +962,17 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                             for (int j = 0; j < DPC; ++j) a = fsum32(d[DPC * i + j], a);
                             hs[i] = a;
                         }
-                        tbig = fbig_acc(d[3], fbig_acc(d[2], fbig_acc(d[1], fbig_acc(d[0], tbig))));
                     }
-                    if (__ballot((tbig & kBigMask) != 0u) != 0) {
-                        esc_tracks = 1;
-                        any_esc = true;
+                    if (mesc) {  // the strip or a halo block holds an escape: where, exactly
+                        uint32_t tbig = 0;
+#pragma unroll
+                        for (int q = 0; q < kLoads; ++q)
+                            tbig = fbig_acc(v[q].w, fbig_acc(v[q].z, fbig_acc(v[q].y, fbig_acc(v[q].x, tbig))));
+                        tbig = fbig_acc(hv.w, fbig_acc(hv.z, fbig_acc(hv.y, fbig_acc(hv.x, tbig))));
+                        if (__ballot((tbig & kBigMask) != 0u) != 0) {
+                            esc_tracks = 1;
+                            any_esc = true;
+                        }
                     }
                 }
             }
