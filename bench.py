@@ -18,8 +18,9 @@ resident in HBM before timing.  Other BASELINE configs are available with
   hg19mm9-32rep configs[4] the same table and flags on 32 replicates (shared peak
                            centres), read with -s 75: the filters decide
 
-One step = the whole hot path over the genome: RCCL all-reduce of the tag
-totals -> background -> up_run_async (K1a stream+screen on a high-priority
+One step = the whole hot path over the genome: the tag totals summed over
+the ranks (node-shared StepBoard on one node; RCCL across nodes) ->
+background -> up_run_async (K1a stream+screen on a high-priority
 stream -> K1b exact blocks -> K2 segmentation -> K3 region statistics +
 filters on a chain stream, records written straight into pinned host memory;
 up to five passes in flight) -> rank 0 reads every rank's records from the
@@ -108,7 +109,7 @@ def load_table(names):
 def pmc_traffic(bytes_per_launch):
     """HBM bytes per K1a launch from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.py) when they were taken on this exact workload."""
-    for rnd in ("r03", "r02", "r01"):
+    for rnd in ("r04", "r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", rnd, "k1a_pmc_traffic.json")
         try:
             d = json.load(open(p))
@@ -122,8 +123,8 @@ def pmc_traffic(bytes_per_launch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--bw", type=int, default=50)
     ap.add_argument("--seed", type=int, default=1000)
     ap.add_argument("--workload", default="hg19-dir1", choices=sorted(WORKLOADS))

@@ -1410,6 +1410,16 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             double mx = -__builtin_inf();
 #pragma unroll
             for (int k = 0; k < SW; ++k) {
+#ifndef UPK_K1B_ALL_WORDS
+                // a dead word holds no flag (the screen's proof): no key, no
+                // LDS store (the flag loop skips it) -- 3/4 of a block's words
+                if constexpr (!PROF) {
+                    if (!((lw >> k) & 1u)) {
+                        sc[k] = -1.0;
+                        continue;
+                    }
+                }
+#endif
                 if constexpr (NONDIR) sc[k] = af[k] + ar[k];  // forwardScore + reverseScore
                 else sc[k] = af[k];
                 if constexpr (!PROF) {
@@ -1457,7 +1467,12 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     // scores through LDS so the word loop below stays a loop
                     // (unrolled, its run bookkeeping overflows the I-cache)
 #pragma unroll
-                    for (int k = 0; k < SW; ++k) scs[64 * k + lane] = sc[k];
+                    for (int k = 0; k < SW; ++k) {
+#ifndef UPK_K1B_ALL_WORDS
+                        if (!((lw >> k) & 1u)) continue;  // never read (dead word)
+#endif
+                        scs[64 * k + lane] = sc[k];
+                    }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1959,11 +1974,20 @@ __device__ __forceinline__ void region_words(WinT<POOL> (&cs)[2 * NH + 1], uint6
     for (int w = 0; w < 2 * NH + 1; ++w) hm[w] = __ballot(nz(cs[w]));
 }
 
-template <int NH, int POOL, bool NONDIR>
+// K3's occupancy: one pooled directional sample (configs[1]) at 5 waves
+// per EU, i.e. <= 96 VGPRs (a 40-byte spill), so two K3 waves fit beside
+// K1a's three per SIMD: K3 alone 0.160 -> 0.144 ms, step +1.2 % over three
+// same-box rounds (profiles/r04/k1b_dead/); the other instantiations keep the
+// compiler's choice (unmeasured at 96)
 #ifndef UPK_K3_WPE
 #define UPK_K3_WPE 1
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3_WPE))) stats_kernel(StatParams P) {
+#ifndef UPK_K3_WPE_DIR1
+#define UPK_K3_WPE_DIR1 5
+#endif
+template <int NH, int POOL, bool NONDIR>
+__global__ void __launch_bounds__(256)
+    __attribute__((amdgpu_waves_per_eu(POOL == 0 && !NONDIR ? UPK_K3_WPE_DIR1 : UPK_K3_WPE))) stats_kernel(StatParams P) {
     extern __shared__ double lds_[];
     const int bw = P.bw;
     const double *ktab = load_ktab(lds_, P.kern, bw);
