@@ -1974,20 +1974,16 @@ __device__ __forceinline__ void region_words(WinT<POOL> (&cs)[2 * NH + 1], uint6
     for (int w = 0; w < 2 * NH + 1; ++w) hm[w] = __ballot(nz(cs[w]));
 }
 
-// K3's occupancy: one pooled directional sample (configs[1]) at 5 waves
-// per EU, i.e. <= 96 VGPRs (a 40-byte spill), so two K3 waves fit beside
-// K1a's three per SIMD: K3 alone 0.160 -> 0.144 ms, step +1.2 % over three
-// same-box rounds (profiles/r04/k1b_dead/); the other instantiations keep the
-// compiler's choice (unmeasured at 96)
+// K3's occupancy: 5 waves per EU, i.e. <= 96 VGPRs (one directional
+// sample: a 40-byte spill), so two K3 waves fit beside K1a's three per SIMD.
+// Same-box A/B (profiles/r04/k1b_dead/, k3_all/): configs[1] K3 alone 0.160
+// -> 0.144 ms, step +1.2 % over three rounds; configs[2] K3 0.54 -> 0.49 ms,
+// step +4.3 % over two; configs[4] replicates unchanged
 #ifndef UPK_K3_WPE
-#define UPK_K3_WPE 1
-#endif
-#ifndef UPK_K3_WPE_DIR1
-#define UPK_K3_WPE_DIR1 5
+#define UPK_K3_WPE 5
 #endif
 template <int NH, int POOL, bool NONDIR>
-__global__ void __launch_bounds__(256)
-    __attribute__((amdgpu_waves_per_eu(POOL == 0 && !NONDIR ? UPK_K3_WPE_DIR1 : UPK_K3_WPE))) stats_kernel(StatParams P) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3_WPE))) stats_kernel(StatParams P) {
     extern __shared__ double lds_[];
     const int bw = P.bw;
     const double *ktab = load_ktab(lds_, P.kern, bw);
