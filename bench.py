@@ -120,6 +120,66 @@ def pmc_traffic(bytes_per_launch):
     return None, None
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started without torchrun: run the N ranks as
+    children of this process (torch.distributed.run, one process per GPU on
+    this node) and return their exit status.  Called before anything touches
+    the GPU; this process only waits (nothing is exec'd).  Rank 0's JSON
+    line reaches stdout through the inherited descriptor."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    port = env.get("UNIPEAK_BENCH_PORT") or str(free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + argv
+    print(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    r = subprocess.run(cmd, env=env)
+    if r.returncode != 0:
+        print(f"[bench] rank processes failed (exit {r.returncode})", file=sys.stderr, flush=True)
+    return r.returncode
+
+
+def check_world(args):
+    """--gpus against the launcher's world size.  Returns the world size
+    this process belongs to, or None when this process must launch the
+    ranks itself; raises SystemExit (status 2) on a mismatch."""
+    ws = os.environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus {args.gpus}: must be >= 1")
+    if ws is None:
+        return None if args.gpus > 1 else 1
+    if int(ws) != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={ws} (launch N ranks with --gpus N)",
+              file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    return int(ws)
+
+
+def launch_probe():
+    """UNIPEAK_BENCH_LAUNCH_PROBE=<rc> (tests/test_bench_launch.py, CPU): each
+    rank joins a gloo world, all-reduces its rank, rank 0 prints the world it
+    saw; rank world-1 exits with <rc> -- the launcher's plumbing without a GPU."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    t = torch.tensor([rank], dtype=torch.int64)
+    dist.all_reduce(t)
+    dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "rank_sum": int(t.item()),
+                          "local_world": int(os.environ.get("LOCAL_WORLD_SIZE", "0"))}), flush=True)
+    rc = int(os.environ["UNIPEAK_BENCH_LAUNCH_PROBE"])
+    return rc if rank == world - 1 else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -133,6 +193,12 @@ def main():
     args = ap.parse_args()
     W = WORKLOADS[args.workload]
 
+    if W.get("shift_pipeline") and args.gpus != 1:
+        raise SystemExit("hg19-shift runs on one GPU (--gpus 1)")
+    if check_world(args) is None:  # --gpus N > 1 without a launcher
+        return launch_ranks(args.gpus, sys.argv[1:])
+    if os.environ.get("UNIPEAK_BENCH_LAUNCH_PROBE") is not None:
+        return launch_probe()
     if W.get("shift_pipeline"):
         return shift_pipeline(args, W)
     rank = int(os.environ.get("RANK", "0"))
@@ -809,4 +875,4 @@ def cpu_baseline(contigs, args, gpu_value, background, gpu_regions):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

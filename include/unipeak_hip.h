@@ -174,11 +174,20 @@ int up_reset_units(up_ctx *ctx);
  * with non-negative scores every run of processed positions is a region,
  * found in parallel (K1q; records as UP_CLOSE_Q11 / UP_CLOSE_Q11_HEAD
  * describe), except when a unit processes position 1 (an add at <= bw + 1)
- * or a coefficient is negative.  Those, and bw > 255 (kMaxBw: K1's halo of
- * NH <= 4 words), run the exact state machine over every unit instead (K0
- * replay, sequential per buffer: exact, slow).  up_run_async refuses both
- * (UP_E_UNSUPPORTED); up_unit_profile* refuse the replay.  up_shift_scan correlates a replayed region's stored
- * scores (Region::scores), as strandCorr does. */
+ * or a coefficient is negative.  Those, and bw > UP_MAX_PARALLEL_BW (511:
+ * K1's register-resident halo of NH <= 8 64-position words), run the exact
+ * state machine instead (K0 replay, sequential per buffer: exact, slow).
+ * up_run_async refuses both (UP_E_UNSUPPORTED); up_unit_profile* refuse the
+ * replay.  up_shift_scan correlates a replayed region's stored scores
+ * (Region::scores), as strandCorr does.
+ * With a threshold <= 0 the last region of a unit is still open after its
+ * flush and is closed in the buffer's next unit (UP_CLOSE_Q11_HEAD); the
+ * last region of a buffer's last unit in the context is never closed (the
+ * reference never writes it).  So every unit of one buffer must be in ONE
+ * context at -r <= 0: a caller that splits a buffer's units over contexts
+ * or ranks loses the region that crosses the split (bin/regions' multi-device
+ * split keeps buffers whole for this reason). */
+#define UP_MAX_PARALLEL_BW 511
 int up_run(up_ctx *ctx, uint64_t *n_regions);
 /* Pipelined form of up_run: up_run_async enqueues one pass and returns
  * (at most UP_MAX_IN_FLIGHT passes in flight); up_run_wait completes the OLDEST pass in
@@ -243,8 +252,9 @@ int up_timings(up_ctx *ctx, double *ms, int n);
 /* dense per-position score f+r of one unit (testing/-w): out[len] */
 int up_unit_profile(up_ctx *ctx, uint32_t unit, double *out_f, double *out_r,
                     uint32_t len);
-/* -w for units the exact replay produced (K0: quirk Q1 head hits, -r <= 0,
- * bw > 255), whose retirements the dense KDE does not reproduce.  With the
+/* -w for units the exact replay produced (K0: quirk Q1 head hits, -r <= 0
+ * with a unit processing position 1 or a negative coefficient,
+ * bw > UP_MAX_PARALLEL_BW), whose retirements the dense KDE does not reproduce.  With the
  * capture on before up_run, the replay records every processPosition() with
  * a nonzero score (misc/peakcall.cpp:80-83: profileOut_->write), and
  * up_unit_replay_profile returns them for one unit in emission order:

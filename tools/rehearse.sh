@@ -1,5 +1,6 @@
 #!/bin/bash
-# The N-rank bench path (torchrun, StepBoard, node-shared record slots, rank
+# The N-rank bench path (`bench.py --gpus N` launches the ranks itself through
+# torch.distributed.run, StepBoard, node-shared record slots, rank
 # 0's merge in global unit order) end to end on a one-GPU box: every rank on
 # device 0 (UNIPEAK_SHARE_GPU), gloo for the setup collectives (RCCL refuses
 # two ranks on one GPU).  Rank 0's merged records and exptSums of the last
@@ -12,8 +13,7 @@ for W in ${WS:-hg19-dir1 hg19-8s1c}; do
     --no-cpu-baseline > $D/${W}_n1.json 2> $D/${W}_n1.err || { tail -20 $D/${W}_n1.err; exit 1; }
   for N in ${NS:-2 4 8}; do
     UNIPEAK_BENCH_DUMP=$D/${W}_n$N.npz UNIPEAK_SHARE_GPU=1 UNIPEAK_DIST_BACKEND=gloo timeout -k 10 400 \
-      python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
-      --master-port $((29500 + N)) bench.py --workload $W --gpus $N --steps $ST --warmup 2 --no-cpu-baseline \
+      python bench.py --workload $W --gpus $N --steps $ST --warmup 2 --no-cpu-baseline \
       > $D/${W}_n$N.json 2> $D/${W}_n$N.err || { tail -20 $D/${W}_n$N.err; exit 1; }
     python - "$D/${W}_n1.npz" "$D/${W}_n$N.npz" "$D/${W}_n$N.json" "$W" "$N" <<'EOF' || exit 1
 import json, sys
