@@ -200,8 +200,16 @@ static FILE *filter_open(const char *fname, int write) {
     if (!ends_with(fname, ".gz")) return fopen(fname, write ? "wb" : "rb");
     gzFile g = gzopen(fname, write ? "wb" : "rb");
     if (!g) return NULL;
+    if (!write) {  /* boost's gzip_decompressor throws on a file without a gzip header */
+        char c;
+        const int r = gzread(g, &c, 1);
+        if (r == 1 && gzdirect(g)) fail("error: could not read %s: not in gzip format\n\n", fname);
+        if (r == 1) gzungetc((unsigned char)c, g);
+    }
     cookie_io_functions_t io = {write ? NULL : gzc_read, write ? gzc_write : NULL, NULL, gzc_close};
-    return fopencookie(g, write ? "w" : "r", io);
+    FILE *f = fopencookie(g, write ? "w" : "r", io);
+    if (!f) gzclose(g);
+    return f;
 }
 
 /* line reader with std::getline/istream::good() semantics */

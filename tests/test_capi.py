@@ -26,6 +26,22 @@ def test_header_constants_match_capi():
     assert m and int(m.group(1)) == capi.MAX_IN_FLIGHT
 
 
+def test_header_bw_limit_matches_kernels():
+    """the boundary's stated parallel-scan limit is the kernels' kMaxBw, and
+    every bandwidth the header, INTEGRATION.md and DESIGN.md name as the
+    replay threshold is that value (rounds 3 and 4 left stale copies)"""
+    hdr = open(os.path.join(ROOT, "include", "unipeak_hip.h")).read()
+    ker = open(os.path.join(ROOT, "unipeak_amd", "csrc", "kernels.h")).read()
+    m = re.search(r"#define\s+UP_MAX_PARALLEL_BW\s+(\d+)", hdr)
+    k = re.search(r"constexpr int kMaxBw = (\d+);", ker)
+    assert m and k and int(m.group(1)) == int(k.group(1))
+    lim = int(k.group(1))
+    for f in ("include/unipeak_hip.h", "INTEGRATION.md", "DESIGN.md"):
+        txt = open(os.path.join(ROOT, f)).read()
+        for v in re.findall(r"(?:bw|-b)\s*(?:>|&gt;)\s*(\d+)", txt):
+            assert int(v) in (lim, 63), (f, v)  # 63: the NH=1 kernel's own width
+
+
 def test_library_exports_header():
     L = capi.load_library()
     syms = declared_symbols()

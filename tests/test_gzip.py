@@ -70,6 +70,16 @@ def test_oracle_refuses_bz2(orc_bin, tmp_path, where):
     assert not (tmp_path / "o.txt.bz2").exists()
 
 
+def test_oracle_refuses_plain_bytes_named_gz(orc_bin, tmp_path):
+    """boost's gzip_decompressor throws on a missing gzip header; zlib's
+    transparent mode would read the file as plain text -- refused instead"""
+    plain = _inputs(tmp_path, n=1)
+    (tmp_path / "s0.wig.gz").write_bytes((tmp_path / plain[0]).read_bytes())
+    r = subprocess.run([orc_bin, "regions", "-q", "-c", "ct.txt", "-o", "o.txt", "s0.wig.gz"], cwd=tmp_path,
+                       capture_output=True, text=True)
+    assert r.returncode == 1 and "not in gzip format" in r.stderr, r.stderr[-300:]
+
+
 # ---- bin/ (GPU) --------------------------------------------------------------
 
 def _same(orc_bin, tmp_path, tool, args, out):
@@ -153,3 +163,17 @@ def test_bin_refuses_bz2(gpu_lib, tmp_path, tool, where):
                        cwd=tmp_path, capture_output=True, text=True)
     assert r.returncode == 1 and "error:" in r.stderr and "bz2" in r.stderr, r.stderr[-500:]
     assert not (tmp_path / "o.txt.bz2").exists() or (tmp_path / "o.txt.bz2").stat().st_size == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tool", ["regions", "tags_in_regions"])
+def test_bin_refuses_plain_bytes_named_gz(gpu_lib, tmp_path, tool):
+    plain = _inputs(tmp_path, n=1)
+    (tmp_path / "s0.wig.gz").write_bytes((tmp_path / plain[0]).read_bytes())
+    orc = os.path.join(ROOT, "oracle", "_build", "orc")
+    run([orc, "regions", "-q", "-c", "ct.txt", "-o", "reg.txt", plain[0]], tmp_path)
+    extra = {"tags_in_regions": ["-f", "reg.txt"]}.get(tool, [])
+    quiet = ["-q"] if tool == "regions" else []
+    r = subprocess.run([os.path.join(BIN, tool)] + quiet + ["-c", "ct.txt", "-o", "o.txt"] + extra + ["s0.wig.gz"],
+                       cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 1 and "not in gzip format" in r.stderr, r.stderr[-500:]

@@ -858,8 +858,18 @@ int up_unit_synth_ex(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, 
     uint32_t *trk = c->d_stage.p;  // dense uint32 staging, packed below
     HIPCHK(hipMemsetAsync(trk, 0, (size_t)len * sizeof(uint32_t), c->stream));
     const uint64_t npos = (uint64_t)(hi - lo + 1);
-    uint64_t *d_tab = nullptr;
-    uint64_t tab[1024];  // host source of an async copy: lives until the sync below
+    // device scratch of this call, freed on every return path after the
+    // stream has drained (an early HIPCHK return included)
+    struct StreamScratch {
+        hipStream_t s;
+        void *p[2] = {nullptr, nullptr};
+        ~StreamScratch() {
+            if (p[0] || p[1]) (void)hipStreamSynchronize(s);
+            for (void *q : p)
+                if (q) (void)hipFree(q);
+        }
+    } scratch{c->stream};
+    uint64_t tab[1024];
     if (!peak_seed) {
         hipLaunchKernelGGL(synth_bg_kernel, dim3((unsigned)((npos + 255) / 256)), dim3(256), 0,
                            c->stream, trk, tkey, lo, hi, thr, (int64_t)offset, (int64_t)len);
@@ -872,8 +882,11 @@ int up_unit_synth_ex(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, 
             pr *= mu / (double)(k + 1);
             cdf += pr;
         }
-        HIPCHK(hipMalloc(&d_tab, sizeof tab));
-        HIPCHK(hipMemcpyAsync(d_tab, tab, sizeof tab, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMalloc(&scratch.p[0], sizeof tab));
+        const uint64_t *d_tab = (const uint64_t *)scratch.p[0];
+        // stream-ordered, then waited for: the source is this stack frame
+        HIPCHK(hipMemcpyAsync(scratch.p[0], tab, sizeof tab, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
         const uint32_t nch = (uint32_t)((npos + 65535) >> 16);
         hipLaunchKernelGGL(synth_bgc_kernel, dim3((nch + 255) / 256), dim3(256), 0, c->stream, trk,
                            tkey, lo, hi, d_tab, (int64_t)offset, (int64_t)len, nch);
@@ -915,20 +928,15 @@ int up_unit_synth_ex(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, 
             }
         }
         if (!tags.empty()) {
-            uint32_t *d = nullptr;
-            HIPCHK(hipMalloc(&d, tags.size() * sizeof(uint32_t)));
+            HIPCHK(hipMalloc(&scratch.p[1], tags.size() * sizeof(uint32_t)));
+            uint32_t *d = (uint32_t *)scratch.p[1];
             HIPCHK(hipMemcpyAsync(d, tags.data(), tags.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
             hipLaunchKernelGGL(synth_peak_kernel, dim3((unsigned)((tags.size() + 255) / 256)), dim3(256), 0,
                                c->stream, trk, d, (uint64_t)tags.size());
             HIPCHK(hipGetLastError());
-            HIPCHK(hipStreamSynchronize(c->stream));
-            HIPCHK(hipFree(d));
         }
     }
-    if (d_tab) {
-        HIPCHK(hipStreamSynchronize(c->stream));  // the table is read by synth_bgc_kernel
-        HIPCHK(hipFree(d_tab));
-    }
+    HIPCHK(hipStreamSynchronize(c->stream));  // the scratch tables are read by the kernels above
     if ((r = pack_track(c, unit, strand, sample, trk))) return r;
     c->ran = false;
     return UP_OK;

@@ -317,25 +317,27 @@ __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const Uni
         for (int q = 0; q < NV; ++q)
             if (64 * q + lane < NL) v[q] = t[64 * q + lane];
         __builtin_amdgcn_wave_barrier();  // earlier readers of the stage are done
+        uint32_t eb = 0;  // escaped fields in this lane's 16 bytes
 #pragma unroll
         for (int q = 0; q < NV; ++q)
-            if (64 * q + lane < NL) *(u32x4 *)(stage + 16 * (64 * q + lane)) = v[q];
+            if (64 * q + lane < NL) {
+                *(u32x4 *)(stage + 16 * (64 * q + lane)) = v[q];
+                eb |= fbig32(v[q].x) | fbig32(v[q].y) | fbig32(v[q].z) | fbig32(v[q].w);
+            }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         uint32_t c[N];
 #pragma unroll
         for (int w = 0; w < N; ++w) c[w] = ((uint32_t)stage[kWordBytes * w + fbyte(lane)] >> sh) & kTMask;
-        resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[0]), x0, lane);
+        // most windows hold no escape: one ballot instead of N per-word tests
+        if (__ballot(eb != 0u)) resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[0]), x0, lane);
 #pragma unroll
         for (int w = 0; w < N; ++w) cs[w] = c[w];
     } else {
         // tracks per batch: two wave loads' worth (more held the K1b
         // register budget: 14 tracks in flight spilled)
-#ifndef UPK_K1B_NQ
-#define UPK_K1B_NQ 2
-#endif
-        constexpr int NQ = UPK_K1B_NQ;
+        constexpr int NQ = 2;
         constexpr int KB = (NQ * 64 / NL) < (kStageBytes / (NL * 16)) ? NQ * 64 / NL : kStageBytes / (NL * 16);
 #pragma unroll
         for (int w = 0; w < N; ++w) cs[w] = 0;
@@ -534,6 +536,10 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return wave_reduce_u32(v, 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return b < a ? b : a; });
 }
 
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    return wave_reduce_u32(v, 0u, [](uint32_t a, uint32_t b) { return b > a ? b : a; });
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return wave_reduce_u32(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
 }
@@ -629,10 +635,7 @@ __device__ __forceinline__ int scr_at(int i) { return i + (i >> 4); }
 // the lane reads of the screen fold into the ds_read2 offset fields
 constexpr size_t kScreenLds = 4 * kScrWords * sizeof(uint32_t);
 constexpr size_t kScanLds = kKTab * sizeof(double) + kScreenLds + 4 * kStepWords * kWave * sizeof(double);
-#ifndef UPK_XFRONT
-#define UPK_XFRONT 2
-#endif
-constexpr int kXFront = UPK_XFRONT;  // K1b work items with >= this many exact blocks go first
+constexpr int kXFront = 2;  // K1b work items with >= this many exact blocks go first
 constexpr size_t kExactLds = kKTab * sizeof(double) + 4 * kStepWords * kWave * sizeof(double);
 static_assert(2 * kStageBytes <= kStepWords * kWave * sizeof(double), "both strands' stages fit a wave's score area");
 
@@ -780,25 +783,17 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     // are issued before the current one is reduced, so two tracks' bytes are
     // in flight per wave instead of one (the stream is latency-bound at the
     // two waves per SIMD K1a keeps, launch_scan)
-#ifdef UPK_NO_K1A_PF  // A/B: each track's loads issued right before it is reduced
-    constexpr bool kPf = false;
-#else
     constexpr bool kPf = true;
-#endif
     constexpr int SH = scr_halo(NH);  // screen halo chunks this width loads on each side
     constexpr int HL_ = SH * kChunkBytes / 16;  // halo lane loads per side (SH chunks)
     // One directional track (configs[1]): the strip's escape bit
     // (ScanParams::esc, its word loaded with the prefetch) replaces the
     // per-dword escape test (two VALU per dword) when it is clear; the exact
     // chunk sums stay (the pre-screen needs them: configs[1]'s wskip is ~4
-    // tags).  UPK_K1A_BOUND2 (A/B): a first pre-screen on 2 x popcount of
-    // each dword, one v_bcnt per dword -- it fails on most strips at
-    // configs[1]'s threshold and then costs both.
-#ifdef UPK_NO_K1A_CHEAP  // A/B: every track's chunk sums and escape bits first
-    constexpr bool kCheap = false;
-#else
+    // tags).  (Round 4 measured a first pre-screen on 2 x popcount of each
+    // dword, one v_bcnt per dword: it fails on most strips at configs[1]'s
+    // threshold and then costs both.)
     constexpr bool kCheap = MODE == kModeScreen && !PROF && POOL == 0 && !NONDIR && kTB == 2 && kPf;
-#endif
     u32x4 pv[MODE == kModeScreen && !PROF ? kLoads : 1];
     u32x4 phv = {0u, 0u, 0u, 0u};
     uint32_t pf_strip = 0, pf_cur = 0;
@@ -864,9 +859,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         const UnitDesc U = units[cur];
         const uint32_t local = strip - U.strip0;
         const int64_t p0 = 1 + (int64_t)local * kStrip;  // first position of the strip
-#ifdef UPK_AB_SKIP_K1B  // upper-bound experiment only (wrong regions): K1b's blocks cost nothing
-        if constexpr (MODE == kModeExact) exact_blocks = 0;
-#endif
 
         // ---- screen: which blocks can hold a flagged position ----
         if constexpr (!PROF && MODE != kModeExact) {
@@ -931,16 +923,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     while (it + istep >= units[nc_].strip0 + units[nc_].nstrips) ++nc_;
                     pf_issue(it + istep, nc_, 0, 0);
                 }
-#if !defined(UPK_NO_K1A_DPP) && defined(UPK_K1A_BOUND2)
-                if (!mesc && (R + CPL - 1) / CPL <= 2) {
-                    uint32_t T[kLoads];
-#pragma unroll
-                    for (int q = 0; q < kLoads; ++q)
-                        T[q] = bcnt_acc(v[q].w, bcnt_acc(v[q].z, bcnt_acc(v[q].y, bcnt_acc(v[q].x, 0u))));
-                    const uint32_t hl = bcnt_acc(hv.w, bcnt_acc(hv.z, bcnt_acc(hv.y, bcnt_acc(hv.x, 0u))));
-                    clean = __ballot(2u * pre_bound(T, hl) > P.wskip) == 0;
-                }
-#endif
                 if (!clean) {  // the exact chunk sums of the same registers
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
@@ -1042,7 +1024,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             // readlane) plus both halos bounds it.  Background strips -- most
             // of the genome -- end here; the others (and any escaped field,
             // whose count the screen does not know) take the LDS screen below.
-#ifndef UPK_NO_K1A_DPP
             if constexpr (MODE == kModeScreen) {
                 if (!clean && (R + CPL - 1) / CPL <= 2 && !any_esc) {
                     uint32_t T[kLoads];
@@ -1058,7 +1039,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     clean = __ballot(pre_bound(T, hl) > P.wskip) == 0;
                 }
             }
-#endif
             if (clean) {
                 mchunk = 0;
                 exact_blocks = 0;
@@ -1213,46 +1193,34 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             continue;
         }
 
+        // Run state of the strip, wave-uniform (scalar registers): the flag
+        // loop below visits only live words, so a run that reaches the end of
+        // the last visited word and finds no flag in the next visited one
+        // ended at that word's last position.
         RecList R_{0, 0, kInline};
-        uint64_t prevF = 0, F0 = 0;
-        double lb = -__builtin_inf();  // open run: this lane's best key so far
-        uint32_t lp = 0;               // and its (first) position
-        bool lt = false;               // a later position of this lane equals lb
-        bool pk_ok = false;            // the run started inside this strip
-        // the run's (first) largest key and its position; with Q keys a
-        // second position holding the largest Q is marked by +0.5 (K3 then
-        // orders the tied positions by their FP64 scores)
-        auto run_peak = [&](double &m, uint32_t &pp) {
-            m = wave_max_d(lb);
-            pp = wave_min_u32(lb == m ? lp : 0xFFFFFFFFu);
-            if (kQ && qm) {
-                const uint64_t at = __ballot(lb == m);
-                if ((at & (at - 1)) != 0 || __ballot(lb == m && lt) != 0) m += 0.5;
-            }
-        };
+        uint64_t F0 = 0;
+        bool open = false;      // a run is open at the last position of word `last`
+        int last = -2;          // strip word index (0..255) of the last visited live word
+        bool pk_ok = false;     // the open run started inside this strip
+        // the open run's first largest key, its position, and whether a
+        // second position holds the same key (Q keys: K3 then orders the tied
+        // positions by their FP64 scores; marked by +0.5)
+        double best = -__builtin_inf();
+        uint32_t bpos = 0;
+        bool btie = false;
+        auto run_key = [&]() { return (kQ && qm && btie) ? best + 0.5 : best; };
         auto close_run = [&](uint32_t end_pos) {
-            double m;
-            uint32_t pp;
-            run_peak(m, pp);
-            rec_end(R_, end_pos, pk_ok ? pp : 0u, m, P, strip, lane);
+            const double m = run_key();
+            rec_end(R_, end_pos, pk_ok ? bpos : 0u, m, P, strip, lane);
             if (!pk_ok && lane == 0) {  // the run open at p0: its part in this strip
                 P.spk[4ull * strip] = (uint64_t)__double_as_longlong(m);
-                P.spk[4ull * strip + 1] = pp;
+                P.spk[4ull * strip + 1] = bpos;
             }
-            lb = -__builtin_inf();
-            lt = false;
+            open = false;
         };
 
-        for (int j = 0; j < kBlocks; ++j) {
-            if (!((exact_blocks >> j) & 1u)) {
-                // no flag in this block: a run open at its left edge ends there
-                if constexpr (!PROF) {
-                    if (prevF >> 63)  // the run open at the previous word's last lane ends there
-                        close_run((uint32_t)(p0 + 64 * (j * SW) - 1));
-                    prevF = 0;
-                }
-                continue;
-            }
+        for (uint32_t eb = exact_blocks; eb; eb &= eb - 1u) {
+            const int j = __builtin_ctz(eb);  // blocks without a flag are never visited
             // words of this block that can hold a flag (the others keep F = 0
             // and receive no scatter)
             uint32_t lw = 0;
@@ -1273,16 +1241,15 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             const uint64_t tq0 = __builtin_amdgcn_s_memtime();
 #endif
             T wf[NWIN], wr[NONDIR ? NWIN : 1];
-            uint64_t hf[NWIN], hr[NONDIR ? NWIN : 1];
             load_words_staged<NWIN, POOL>(wf, U, S, 0, x0, lane, P.nnc, P.nc, P.coef, (uint8_t *)scs);
             if constexpr (NONDIR)
                 load_words_staged<NWIN, POOL>(wr, U, S, 1, x0, lane, P.nnc, P.nc, P.coef,
                                               (uint8_t *)scs + kStageBytes);
-#pragma unroll
-            for (int w = 0; w < NWIN; ++w) {
-                hf[w] = __ballot(nz(wf[w]));
-                if constexpr (NONDIR) hr[w] = __ballot(nz(wr[w]));
-            }
+            // the hit bitmaps of the window words are ballots taken where they
+            // are used (Q scans, FP64 walk), not held for the whole block: 2 x
+            // NWIN SGPRs live across the block made the compiler spill SGPRs
+            // into VGPR lanes (K1b 65 -> 79 M VALU per launch when NWIN's
+            // kernels widened to NH <= 8)
 #ifdef UPK_DEBUG_TIMES
             const uint64_t tq1 = __builtin_amdgcn_s_memtime();
             dt_load += tq1 - tq0;
@@ -1291,7 +1258,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             const uint64_t tq1 = __builtin_amdgcn_s_memtime();
             if (lane == 0) {
                 uint32_t nh = 0;
-                for (int w = 0; w < NWIN; ++w) nh += __builtin_popcountll(hf[w]);
+                for (int w = 0; w < NWIN; ++w) nh += __builtin_popcountll(__ballot(nz(wf[w])));
                 atomicAdd(&P.dbg[2], (unsigned long long)nh);
                 atomicAdd(&P.dbg[3], (unsigned long long)(tq1 - tq0));
             }
@@ -1315,12 +1282,21 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     // (W is a difference of two prefixes: any common base
                     // cancels) and end with the last one's
                     uint32_t c0 = 0, c1 = 0, c2 = 0;  // totals of the words before
-                    const int wlo = __builtin_ctz(lw), whi = 31 - __builtin_clz(lw) + 2 * NH;
+                    // window words some live word reads (output word k reads
+                    // window words k .. k + 2NH); no window spans a word
+                    // outside them, so the base restarts there
+                    uint32_t nd = lw;
+#pragma unroll
+                    for (int d = 1; d <= 2 * NH; ++d) nd |= lw << d;
                     WordLoop<0, NWIN>::run([&](auto wc) {
                         constexpr int w = decltype(wc)::value;
-                        uint64_t any = hf[w];
-                        if constexpr (NONDIR) any |= hr[NONDIR ? w : 0];
-                        if (w < wlo || w > whi) any = 0;
+                        uint64_t any = 0;
+                        if ((nd >> w) & 1u) {
+                            if constexpr (NONDIR) any = __ballot(nz(wf[w]) || nz(wr[NONDIR ? w : 0]));
+                            else any = __ballot(nz(wf[w]));
+                        } else {
+                            c0 = c1 = c2 = 0u;
+                        }
                         if (any == 0) {
                             P0[w] = c0;
                             P1[w] = c1;
@@ -1377,7 +1353,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 constexpr int OHI = W > SW - 1 ? SW - 1 : W;
                 const uint32_t reach = xw & (((2u << OHI) - 1u) & ~((1u << OLO) - 1u));
                 if (!reach) return;
-                uint64_t m = hf[W];
+                uint64_t m = __ballot(nz(wf[W]));
                 if constexpr (W < NH) m &= edge_lo[W];
                 if constexpr (W >= NH + SW) m &= edge_hi[W - NH - SW];
                 while (m) {
@@ -1387,7 +1363,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     scatter_hits<NH, SW, W>(af, hb, hc, lane, bw, ktab, reach);
                 }
                 if constexpr (NONDIR) {
-                    uint64_t q = hr[W];
+                    uint64_t q = __ballot(nz(wr[W]));
                     if constexpr (W < NH) q &= edge_lo[W];
                     if constexpr (W >= NH + SW) q &= edge_hi[W - NH - SW];
                     while (q) {
@@ -1410,7 +1386,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             double mx = -__builtin_inf();
 #pragma unroll
             for (int k = 0; k < SW; ++k) {
-#ifndef UPK_K1B_ALL_WORDS
                 // a dead word holds no flag (the screen's proof): no key, no
                 // LDS store (the flag loop skips it) -- 3/4 of a block's words
                 if constexpr (!PROF) {
@@ -1419,7 +1394,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                         continue;
                     }
                 }
-#endif
                 if constexpr (NONDIR) sc[k] = af[k] + ar[k];  // forwardScore + reverseScore
                 else sc[k] = af[k];
                 if constexpr (!PROF) {
@@ -1463,71 +1437,73 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                 }
 #endif
                 const uint64_t anyflag = __ballot(mx >= kthr);
-                if (anyflag | prevF) {
-                    // scores through LDS so the word loop below stays a loop
-                    // (unrolled, its run bookkeeping overflows the I-cache)
+                if (anyflag || open) {
+                    // keys / scores through LDS so the word loop below stays a
+                    // loop (unrolled, its run bookkeeping overflows the I-cache)
 #pragma unroll
                     for (int k = 0; k < SW; ++k) {
-#ifndef UPK_K1B_ALL_WORDS
                         if (!((lw >> k) & 1u)) continue;  // never read (dead word)
-#endif
                         scs[64 * k + lane] = sc[k];
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll 1
-                    for (int k = 0; k < SW; ++k) {
-                        const int64_t wpos = p0 + 64 * (j * SW + k);
-                        if (!((lw >> k) & 1u)) {  // dead word: no flag; a run open at its left edge ends
-                            if (prevF >> 63) close_run((uint32_t)(wpos - 1));
-                            if (j == 0 && k == 0) F0 = 0;
-                            prevF = 0;
-                            continue;
-                        }
+                    for (uint32_t lm = lw; lm; lm &= lm - 1u) {
+                        const int k = __builtin_ctz(lm);
+                        const int g = j * SW + k;  // word of the strip
+                        const int64_t wpos = p0 + 64 * g;
+                        // a run open at the end of an earlier word met a word
+                        // without flags before this one: it ended there
+                        if (open && g != last + 1) close_run((uint32_t)(p0 + 64 * (last + 1) - 1));
+                        last = g;
                         const double sck = scs[64 * k + lane];
                         const uint64_t F = __ballot(sck >= kthr);
-                        const bool cont = (prevF >> 63) != 0;  // run open at the previous position
-                        if (cont && !(F & 1ull)) close_run((uint32_t)(wpos - 1));
-                        uint64_t st;
-                        if (j == 0 && k == 0) {
-                            F0 = F;
-                            st = F & ~((F << 1) | 1ull);  // no interior start at p0
-                        } else {
-                            st = F & ~((F << 1) | (cont ? 1ull : 0ull));
-                        }
+                        if (g == 0) F0 = F;
+                        if (open && !(F & 1ull)) close_run((uint32_t)(wpos - 1));
+                        // no interior start at p0 (K2 joins it to the previous strip's run)
+                        uint64_t st = F & ~((F << 1) | ((open || g == 0) ? 1ull : 0ull));
                         while (st) {
                             const int b = __builtin_ctzll(st);
                             st &= st - 1;
                             rec_start(R_, (uint32_t)(wpos + b), P, strip, lane);
                         }
-                        // per run segment of this word: running first maximum of
-                        // f+r per lane (Region::addPos, data.cpp:98-101); one
-                        // wave reduction when the run closes
+                        // each maximal segment of F: its largest key and the
+                        // lanes holding it (Region::addPos keeps the first
+                        // maximum, data.cpp:98-101), merged into the run's
                         uint64_t rem = F;
                         while (rem) {
                             const int a = __builtin_ctzll(rem);
                             const uint64_t up = ~(rem >> a);
                             const int len = up ? __builtin_ctzll(up) : 64 - a;
-                            const uint64_t seg = (len >= 64 ? ~0ull : ((1ull << len) - 1ull)) << a;
-                            rem &= ~seg;
-                            if (!(a == 0 && cont)) {  // a new run
-                                lb = -__builtin_inf();
-                                lt = false;
-                                pk_ok = !(j == 0 && k == 0 && a == 0);  // may continue the previous strip
+                            rem = len + a >= 64 ? 0ull : rem & (~0ull << (a + len));
+                            const bool in = lane >= a && lane < a + len;
+                            double m;
+                            uint64_t at;
+                            if (kQ && qm) {  // integer keys >= 1
+                                const uint32_t kq = in ? (uint32_t)sck : 0u;
+                                const uint32_t mq = wave_max_u32(kq);
+                                at = __ballot(kq == mq);
+                                m = (double)mq;
+                            } else {
+                                m = wave_max_d(in ? sck : -__builtin_inf());
+                                at = __ballot(in && sck == m);
                             }
-                            if ((seg >> lane) & 1ull) {
-                                if (sck > lb) {
-                                    lb = sck;
-                                    lp = (uint32_t)(wpos + lane);
-                                    lt = false;
-                                } else if (sck == lb) {
-                                    lt = true;
-                                }
+                            if (!(a == 0 && open)) {  // a new run
+                                best = m;
+                                bpos = (uint32_t)(wpos + __builtin_ctzll(at));
+                                btie = (at & (at - 1)) != 0;
+                                pk_ok = g != 0 || a != 0;  // one at p0 may continue the previous strip
+                            } else if (m > best) {
+                                best = m;
+                                bpos = (uint32_t)(wpos + __builtin_ctzll(at));
+                                btie = (at & (at - 1)) != 0;
+                            } else if (m == best) {
+                                btie = true;
                             }
+                            open = true;
                             if (a + len < 64) close_run((uint32_t)(wpos + a + len - 1));
                         }
-                        prevF = F;
                     }
                     __builtin_amdgcn_wave_barrier();  // scs reused by the next block
                 }
@@ -1537,18 +1513,17 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 #endif
         }
         if constexpr (PROF) continue;
-        if (prevF >> 63) {  // the run open at the strip's last position: its part here
-            double m;
-            uint32_t pp;
-            run_peak(m, pp);
+        // a run open at the end of the last visited word: it ends there,
+        // unless that word is the strip's last (K2 joins it to the next strip)
+        if (open && last != kStripWords - 1) close_run((uint32_t)(p0 + 64 * (last + 1) - 1));
+        if (open) {  // the run open at the strip's last position: its part here
             if (lane == 0) {
-                P.spk[4ull * strip + 2] = (uint64_t)__double_as_longlong(m);
-                P.spk[4ull * strip + 3] = pp;
+                P.spk[4ull * strip + 2] = (uint64_t)__double_as_longlong(run_key());
+                P.spk[4ull * strip + 3] = bpos;
             }
         }
-        // a run open at the strip's last position has no interior end (K2)
         const uint64_t info = (uint64_t)R_.ns | ((uint64_t)R_.ne << 16) | ((F0 & 1ull) << 32) |
-                              ((prevF >> 63) << 33) | ((uint64_t)(local == 0) << 34) |
+                              ((uint64_t)open << 33) | ((uint64_t)(local == 0) << 34) |
                               ((uint64_t)(local + 1 == U.nstrips) << 35) |
                               ((uint64_t)(R_.slot != kInline) << 36);
         if (lane == 0) P.strip_info[strip] = info;
@@ -1995,9 +1970,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
     // dependent round trip behind the streaming loads on every strip)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-#ifdef UPK_AB_SKIP_K3  // upper-bound experiment only (no records): K3 costs nothing
-    return;
-#endif
     const uint64_t nreg = *P.nreg < P.cap ? *P.nreg : P.cap;
     uint64_t wm[2 * NH + 1];
 #pragma unroll
