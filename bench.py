@@ -282,9 +282,11 @@ def main():
                     local_tags += g2.tag_total(u, st, smp)
         g2.close()
     gen_s = time.time() - t_gen
-    # K1a algorithmic bytes: one TB-bit count per bp per strand per
-    # non-control sample
-    alg_bytes = sum(lens[units[k][0]] * nstr * s_nc for k in mine) * TB // 8
+    # K1a algorithmic bytes per bp per strand per non-control sample: what
+    # its stream reads -- the chunk-sum plane (1 byte per 16 bp) for one
+    # directional track, else the TB-bit counts
+    dens = g.scan_density()  # bytes per 1,024 positions of one pooled track
+    alg_bytes = sum(lens[units[k][0]] * nstr * s_nc for k in mine) * dens // 1024
     copy_gbps = g.hbm_copy_gbps(1 << 30, 5)
 
     phase = {"allreduce": 0.0, "launch": 0.0, "wait": 0.0, "gather_merge": 0.0}
@@ -538,7 +540,7 @@ def main():
         value = genome / dt / 1e9
         if sim_world > 1:  # not a headline line: one rank's shard of an N-GPU plan
             print(json.dumps({"sim_world": sim_world, "sim_rank": sim_rank, "ms_per_step": round(dt * 1e3, 4),
-                              "shard_bp": int(alg_bytes * 8 // TB // max(s_nc, 1)), "k1a_ms": round(k1a_ms, 4),
+                              "shard_bp": int(sum(lens[units[k][0]] * nstr for k in mine)), "k1a_ms": round(k1a_ms, 4),
                               "k1_ms": round(k1_ms, 4), "warmup_timings_ms": [round(x, 4) for x in warm], "phases_ms": {k: round(v / args.steps * 1e3, 4)
                                                                       for k, v in phase.items()}}), flush=True)
             g.set_record_target(0, 0)
@@ -574,7 +576,9 @@ def main():
                          "kernel": "scan_kernel<..., kModeScreen> (K1a: stream + integer screen)",
                          "kernel_ms": round(k1a_ms, 4), "kernel_ms_max_rank": round(k1a_max, 4),
                          "bytes_per_launch": int(alg_bytes),
-                         "bytes_rule": f"{TB / 8} B ({TB}-bit count) per bp per strand per non-control sample",
+                         "bytes_rule": (f"{dens / 1024} B per bp per strand per non-control sample (" +
+                                        ("chunk-sum plane: 1 byte per 16 positions" if dens * 8 != 1024 * TB
+                                         else f"{TB}-bit counts") + ")"),
                          "kernel_note": "mean K1a duration over the timed passes (HIP events on the pass "
                                         "stream); passes overlap, so K1a shares the GPU with earlier "
                                         "passes' K1b/K2/K3",
@@ -599,7 +603,8 @@ def main():
             rf["bytes_per_launch_survey"] = int(survey_bytes)
             rf["frac_survey_rule"] = round(survey_bytes / (k1a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             rf["survey_rule_note"] = ("above 1: the kernel does not read SURVEY's uint32 bytes -- the tracks are "
-                                      f"{TB}-bit counts with an exact overflow table (DESIGN.md §3)")
+                                      f"{TB}-bit counts with an exact overflow table and a chunk-sum plane "
+                                      "(DESIGN.md §3)")
         if world == 1 and not args.no_cpu_baseline and args.workload == "hg19-dir1":
             res["cpu_baseline"] = cpu_baseline(contigs, args, value, bg_set[0], last[1])
         print(json.dumps(res), flush=True)
@@ -743,8 +748,7 @@ def shift_pipeline(args, W):
         ka.append(ga.timings()[0])
         kb.append(gb.timings()[0])
     dt = (time.perf_counter() - t0) / args.steps
-    TB = capi.track_bits()
-    alg = genome * 2 * TB // 8  # K1a of each pass: both strands x TB/8 B per bp
+    alg = genome * 2 * ga.scan_density() // 1024  # K1a of each pass: both strands
     k1a = float(np.mean(ka + kb))
     res = {
         "metric": METRIC, "value": round(genome / dt / 1e9, 3), "unit": "Gbp/s", "n_gpus": 1,
@@ -759,7 +763,7 @@ def shift_pipeline(args, W):
                      "unit": "GB/s", "frac": round(alg / (k1a * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": None, "kernel": "scan_kernel<..., kModeScreen> (K1a), both passes",
                      "kernel_ms": round(k1a, 4), "bytes_per_launch": int(alg),
-                     "bytes_rule": f"{TB / 8} B ({TB}-bit count) per bp per strand, both strands"},
+                     "bytes_rule": f"{ga.scan_density() / 1024} B per bp per strand, both strands"},
     }
     print(json.dumps(res), flush=True)
     for g, _ in ctx:

@@ -3,7 +3,8 @@
 # with its own built library, or "." for this tree): per tree a bench line
 # (isolated per-kernel times) and one rocprofv3 SQ counter pass.
 # usage: TAG=bisect tools/gpu_variants.sh . exp/wt_<commit> lib:NAME ...
-# (lib:NAME = this tree with UNIPEAK_LIB=unipeak_amd/lib/libunipeak_hip_NAME.so)
+# (lib:NAME = this tree with UNIPEAK_LIB=unipeak_amd/lib/libunipeak_hip_NAME.so;
+#  env:NAME:VAR=VALUE = this tree with VAR=VALUE in the environment)
 # Results: gpurun_out/$TAG/<name>.json, <name>_sq/ (counter csv).
 set -o pipefail
 R="${GRAFT_REPO_ROOT:?}"; F=$R/gpurun_out/${TAG:-variants}; mkdir -p "$F"
@@ -11,9 +12,10 @@ WL=${WORKLOAD:-hg19-dir1}
 SQ=${SQ:-"SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM"}
 for rep in $(seq 1 "${REPS:-1}"); do
 for v in "$@"; do
-  unset UNIPEAK_LIB
+  unset UNIPEAK_LIB; [ -n "$ENVSET" ] && unset "${ENVSET%%=*}"; ENVSET=
   case "$v" in
     lib:*) n=${v#lib:}; export UNIPEAK_LIB=$R/unipeak_amd/lib/libunipeak_hip_$n.so; v=. ;;
+    env:*) n=${v#env:}; ENVSET=${n#*:}; n=${n%%:*}; export "$ENVSET"; v=. ;;
     *) n=$(basename "$(cd "$R/$v" && pwd)"); [ "$v" = . ] && n=head ;;
   esac
   cd "$R/$v" || exit 1

@@ -69,7 +69,7 @@ EXPORTS = [
     "up_close", "up_set_params", "up_add_unit", "up_unit_count", "up_unit_pack",
     "up_unit_scatter", "up_unit_synth", "up_unit_synth_offset", "up_unit_synth_ex", "up_unit_tag_total", "up_unit_set_last_add", "up_unit_last_add",
     "up_reset_units", "up_run", "up_get_regions", "up_regions_view", "up_shift_scan", "up_shift_best",
-    "up_timings", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
+    "up_timings", "up_scan_density", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
     "up_host_register", "up_unit_profile_range", "up_run_async", "up_run_wait", "up_set_timing",
     "up_set_profile_capture", "up_unit_replay_profile",
     "up_tir_open", "up_tir_close", "up_tir_set_stream", "up_tir_query", "up_tir_timings",
@@ -122,6 +122,7 @@ def load_library(path=LIB_PATH):
         "up_shift_scan": (c.c_int, [vp, vp, c.c_size_t, c.c_uint16, vp]),
         "up_shift_best": (c.c_int, [vp, vp, c.c_size_t, c.c_uint16, vp, vp]),
         "up_timings": (c.c_int, [vp, vp, c.c_int]),
+        "up_scan_density": (c.c_int, [vp, u32p]),
         "up_unit_profile": (c.c_int, [vp, c.c_uint32, vp, vp, c.c_uint32]),
         "up_hbm_copy_gbps": (c.c_int, [vp, c.c_uint64, c.c_int, c.POINTER(c.c_double)]),
         "up_set_record_target": (c.c_int, [vp, vp, c.c_uint64]),
@@ -331,6 +332,12 @@ class Lib:
     def hbm_copy_gbps(self, nbytes=1 << 30, reps=5):
         v = ctypes.c_double()
         _ck(self.L.up_hbm_copy_gbps(self.ctx, nbytes, reps, ctypes.byref(v)))
+        return v.value
+
+    def scan_density(self):
+        """bytes K1a streams per 1,024 positions of one pooled track (up_scan_density)"""
+        v = ctypes.c_uint32()
+        _ck(self.L.up_scan_density(self.ctx, ctypes.byref(v)))
         return v.value
 
     def timings(self):

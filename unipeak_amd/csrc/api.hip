@@ -19,6 +19,7 @@
 #include "kernels.h"
 
 #include "kernels.hip"  // device code shared with the per-NH units (nh_tu.hip)
+#include "stats1.hip"   // (its LDS size)
 #include "emulate.hip"
 
 namespace upk {
@@ -32,14 +33,14 @@ const void *scan_kernel_nh5(int, bool, bool, int);
 const void *scan_kernel_nh6(int, bool, bool, int);
 const void *scan_kernel_nh7(int, bool, bool, int);
 const void *scan_kernel_nh8(int, bool, bool, int);
-const void *stats_kernel_nh1(int, bool);
-const void *stats_kernel_nh2(int, bool);
-const void *stats_kernel_nh3(int, bool);
-const void *stats_kernel_nh4(int, bool);
-const void *stats_kernel_nh5(int, bool);
-const void *stats_kernel_nh6(int, bool);
-const void *stats_kernel_nh7(int, bool);
-const void *stats_kernel_nh8(int, bool);
+const void *stats_kernel_nh1(int, bool, bool);
+const void *stats_kernel_nh2(int, bool, bool);
+const void *stats_kernel_nh3(int, bool, bool);
+const void *stats_kernel_nh4(int, bool, bool);
+const void *stats_kernel_nh5(int, bool, bool);
+const void *stats_kernel_nh6(int, bool, bool);
+const void *stats_kernel_nh7(int, bool, bool);
+const void *stats_kernel_nh8(int, bool, bool);
 const void *shift_kernel_nh1(int);
 const void *shift_kernel_nh2(int);
 const void *shift_kernel_nh3(int);
@@ -62,16 +63,16 @@ static const void *scan_kernel_for(int bw, int pool, bool nd, bool prof, int mod
     default: return scan_kernel_nh8(pool, nd, prof, mode);
     }
 }
-static const void *stats_kernel_for(int bw, int pool, bool nd) {
+static const void *stats_kernel_for(int bw, int pool, bool nd, bool one) {
     switch (window_nh(bw)) {
-    case 1: return stats_kernel_nh1(pool, nd);
-    case 2: return stats_kernel_nh2(pool, nd);
-    case 3: return stats_kernel_nh3(pool, nd);
-    case 4: return stats_kernel_nh4(pool, nd);
-    case 5: return stats_kernel_nh5(pool, nd);
-    case 6: return stats_kernel_nh6(pool, nd);
-    case 7: return stats_kernel_nh7(pool, nd);
-    default: return stats_kernel_nh8(pool, nd);
+    case 1: return stats_kernel_nh1(pool, nd, one);
+    case 2: return stats_kernel_nh2(pool, nd, one);
+    case 3: return stats_kernel_nh3(pool, nd, one);
+    case 4: return stats_kernel_nh4(pool, nd, one);
+    case 5: return stats_kernel_nh5(pool, nd, one);
+    case 6: return stats_kernel_nh6(pool, nd, one);
+    case 7: return stats_kernel_nh7(pool, nd, one);
+    default: return stats_kernel_nh8(pool, nd, one);
     }
 }
 static const void *shift_kernel_for(int bw, int pool) {
@@ -109,6 +110,7 @@ struct Unit {
     uint32_t *d_ovf_tidx = nullptr;  // [ntracks][nblk] escape tile per block (kNoTile: none)
     uint8_t *d_ovf_tiles = nullptr;  // [ntiles][kOvfBlk]
     bool ovf_dirty = false;
+    bool cs_dirty = false;     // a track changed: rebuild its chunk-sum plane (csum_kernel)
     uint32_t ovf_max = 0;          // largest escaped count of any track
 };
 
@@ -175,6 +177,7 @@ struct up_ctx {
     int k1a_per_cu = 3;
     int k1b_per_cu = 0;              // K1b workgroups per CU (UNIPEAK_K1B_PER_CU; 0 = resident)
     int k3_per_cu = 0;               // K3 workgroups per CU (UNIPEAK_K3_PER_CU; 0 = resident)
+    bool k3_one = true;              // batched K3 for one directional sample (UNIPEAK_K3_ONE=0: off)
     bool use_graphs = true;          // passes as hipGraphs (UNIPEAK_GRAPHS=0: plain launches)
     // streams of the passes: every K1a on one high-priority stream (stream
     // order serialises them; as resources free up the dispatcher serves it
@@ -372,6 +375,17 @@ static void sync_all(up_ctx *c) {
 int up_version(void) { return 10000; }
 int up_track_bits(void) { return kTB; }
 
+// K1a's stream (scan_kernel kPlane): the chunk-sum plane for one pooled
+// directional track when the window reaches the neighbouring lanes only
+static bool plane_scan(const up_ctx *c);
+
+int up_scan_density(up_ctx *c, uint32_t *b) {
+    if (!c || !b) return UP_E_ARG;
+    if (!c->have_params) return UP_E_STATE;
+    *b = plane_scan(c) ? 1024u / 16u : 1024u * (uint32_t)kTB / 8u;
+    return UP_OK;
+}
+
 const char *up_strerror(int code) {
     switch (code) {
     case UP_OK: return "ok";
@@ -423,6 +437,7 @@ int up_open(int hip_device, up_ctx **out) {
     if (const char *e = getenv("UNIPEAK_GRAPHS")) c->use_graphs = e[0] != '0';
     if (const char *e = getenv("UNIPEAK_K1B_PER_CU")) c->k1b_per_cu = atoi(e);
     if (const char *e = getenv("UNIPEAK_K3_PER_CU")) c->k3_per_cu = atoi(e);
+    if (const char *e = getenv("UNIPEAK_K3_ONE")) c->k3_one = atoi(e) != 0;
     if (const char *e = getenv("UNIPEAK_CHAINS")) c->n_chain = std::min(4, std::max(1, atoi(e)));
     if (const char *e = getenv("UNIPEAK_LAUNCHER")) c->use_launcher = e[0] != '0';
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -669,7 +684,8 @@ int up_add_unit(up_ctx *c, uint32_t len, int32_t nstrands, int32_t buffer_id, ui
     u.nstrands = nstrands;
     u.buffer = buffer_id;
     u.stride = unit_stride(len);
-    const size_t bytes = u.stride * (size_t)c->p.n_samples * nstrands;
+    // the tracks, then their chunk-sum planes (stride / 4 bytes each, kernels.h)
+    const size_t bytes = u.stride * (size_t)c->p.n_samples * nstrands / 4 * 5;
     u.ovf.resize((size_t)c->p.n_samples * nstrands);
     hipError_t e = hipMalloc(&u.dptr, bytes);
     if (e != hipSuccess) return UP_E_NOMEM;
@@ -735,6 +751,7 @@ static int pack_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample,
             for (auto v : e) m[(uint32_t)(v >> 32)] = (uint32_t)v;
         }
         u.ovf_dirty = true;
+        u.cs_dirty = true;
         c->units_dirty = true;
         return UP_OK;
     }
@@ -779,7 +796,8 @@ int up_unit_scatter(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, s
             if (counts[i] >= kEsc) { m[pos[i]] = counts[i]; u.ovf_dirty = true; }
             else if (!m.empty() && m.erase(pos[i])) u.ovf_dirty = true;
         }
-        if (u.ovf_dirty) c->units_dirty = true;
+        u.cs_dirty = true;  // the chunk sums change with any count
+        c->units_dirty = true;
     }
     // the caller's arrays are copied into the staging buffers before we
     // return, so they may be reused at once; the kernels stay stream-ordered
@@ -1088,6 +1106,24 @@ static int sync_units(up_ctx *c) {
     }
     HIPCHK(c->d_units.ensure(d.size()));
     HIPCHK(hipMemcpy(c->d_units.p, d.data(), d.size() * sizeof(UnitDesc), hipMemcpyHostToDevice));
+    // chunk-sum planes of the tracks that changed (after their escape tables:
+    // escaped fields enter at their counts); stream-ordered after the writes
+    bool planes = false;
+    for (size_t i = 0; i < c->units.size(); ++i) {
+        Unit &u = c->units[i];
+        if (!u.cs_dirty) continue;
+        const uint64_t n = u.stride / 4 * (uint64_t)u.nstrands * c->p.n_samples;
+        const unsigned blocks = (unsigned)std::min<uint64_t>((n + 255) / 256, 65536);
+        if (kTB == 2 && n)
+            hipLaunchKernelGGL(csum_kernel, dim3(blocks), dim3(256), 0, c->stream, c->d_units.p, (uint32_t)i,
+                               (int)c->p.n_samples);
+        u.cs_dirty = false;
+        planes = true;
+    }
+    if (planes) {
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
     c->units_dirty = false;
     c->bw_layout = c->p.bw;
     return UP_OK;
@@ -1101,6 +1137,10 @@ static int pool_mode(const up_ctx *c) {
     if (c->nc.size() == 1) return 0;
     const double cmax = (double)std::max<uint32_t>(kEsc - 1, c->ovf_max_all) * (double)c->nc.size();
     return cmax < 4294967296.0 ? 1 : 2;
+}
+
+static bool plane_scan(const up_ctx *c) {
+    return kTB == 2 && pool_mode(c) == 0 && c->p.nondir == 0 && (c->p.bw + 64) / 64 <= 4;
 }
 
 static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps, uint32_t ovf_cap) {
@@ -1222,8 +1262,12 @@ static StatParams stat_params(up_ctx *c, up_ctx::Pass &ps) {
 }
 
 static void dispatch_stats(up_ctx *c, hipStream_t st, const StatParams &P, uint64_t nreg) {
-    const size_t lds = kStatLds;
-    const void *k = stats_kernel_for(P.bw, pool_mode(c), c->p.nondir != 0);
+    // one pooled directional sample with K1b's peaks: the batched K3
+    // (stats1.hip; UNIPEAK_K3_ONE=0 keeps the general kernel, for A/B and tests)
+    const bool one = c->k3_one && kTB == 2 && pool_mode(c) == 0 && c->p.nondir == 0 && c->p.n_samples == 1 &&
+                     P.peak_pos != nullptr;
+    const size_t lds = one ? kStat1Lds : kStatLds;
+    const void *k = stats_kernel_for(P.bw, pool_mode(c), c->p.nondir != 0, one);
     uint64_t cap = resident_blocks(c, k, lds);
     if (c->k3_per_cu > 0) cap = std::min<uint64_t>(cap, (uint64_t)c->k3_per_cu * (uint64_t)(c->ncu > 0 ? c->ncu : 256));
     const uint64_t blocks = std::min<uint64_t>((nreg + 3) / 4, cap);

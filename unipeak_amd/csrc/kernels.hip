@@ -86,6 +86,11 @@ __device__ __forceinline__ gu8 *track_u8(const UnitDesc &U, int S, int strand, i
     return (gu8 *)U.base + ((uint64_t)strand * S + sample) * U.stride;
 }
 
+// a track's chunk-sum plane (kernels.h)
+__device__ __forceinline__ gu8 *plane_u8(const UnitDesc &U, int S, int strand, int sample) {
+    return (gu8 *)U.base + (uint64_t)U.nstrands * S * U.stride + ((uint64_t)strand * S + sample) * (U.stride / 4);
+}
+
 // byte and bit offset of field n (n = kPadPos + p - 1 for position p)
 __host__ __device__ __forceinline__ int64_t fbyte(int64_t n) { return n >> kLogPerByte; }
 __host__ __device__ __forceinline__ uint32_t fshift(int64_t n) {
@@ -689,6 +694,51 @@ __device__ __forceinline__ uint32_t screen_any(int R, const uint32_t *rd, uint32
     return screen_bits<RM>(rd, wskip, fw, fthr);
 }
 
+// Register pre-screen over a strip's chunk sums (K1a plane path): lane l
+// holds chunks 16l .. 16l+15 (a); the window of chunk c is c-R .. c+R, R <=
+// 16, so it reaches the neighbouring lanes' chunks only (DPP wave shifts;
+// lane 0 / 63 take the strip's halo chunks from lanes 0 / 1's hv).  The
+// strip is clean when no chunk's window holds more than wskip tags -- every
+// window sum exactly, as screen_bits' coarse test bounds a lane's whole span.
+template <int R>
+__device__ __forceinline__ bool plane_clean(const uint32_t (&a)[16], const u32x4 &hv, int lane, uint32_t wskip) {
+    const uint32_t hd[4] = {hv.x, hv.y, hv.z, hv.w};
+    auto hbyte = [&](int i) { return (hd[i >> 2] >> (8 * (i & 3))) & 0xFFu; };
+    uint32_t e[16 + 2 * R];  // chunks 16l - R .. 16l + 15 + R
+#pragma unroll
+    for (int x = 0; x < R; ++x) {
+        const uint32_t lh = rl_u(hbyte(16 - R + x), 0), rh = rl_u(hbyte(x), 1);
+        const uint32_t l = dpp32<0x138, 0xf, false>(0u, a[16 - R + x]);  // wave_shr:1 -> lane - 1
+        const uint32_t r = dpp32<0x130, 0xf, false>(0u, a[x]);           // wave_shl:1 -> lane + 1
+        e[x] = lane == 0 ? lh : l;
+        e[16 + R + x] = lane == 63 ? rh : r;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) e[R + i] = a[i];
+    if (wskip >= 255u) {  // a saturated chunk could hide more than wskip tags
+#pragma unroll
+        for (int i = 0; i < 16 + 2 * R; ++i) e[i] = e[i] == 255u ? kBig : e[i];
+    }
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i <= 2 * R; ++i) w += e[i];
+    uint32_t mx = w;
+#pragma unroll
+    for (int i = 1; i < 16; ++i) {
+        w += e[i + 2 * R] - e[i - 1];
+        mx = w > mx ? w : mx;
+    }
+    return __ballot(mx > wskip) == 0;
+}
+template <int RM>
+__device__ __forceinline__ bool plane_clean_any(int R, const uint32_t (&a)[16], const u32x4 &hv, int lane,
+                                                uint32_t wskip) {
+    if constexpr (RM > 1) {
+        if (R < RM) return plane_clean_any<RM - 1>(R, a, hv, lane, wskip);
+    }
+    return plane_clean<RM>(a, hv, lane, wskip);
+}
+
 // MODE kModeScreen (K1a): stream + screen every strip; strips without exact
 // blocks get their (empty) summary, the others go to the work list.
 // MODE kModeExact (K1b): run the exact blocks of the listed strips, so the
@@ -793,7 +843,13 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     // tags).  (Round 4 measured a first pre-screen on 2 x popcount of each
     // dword, one v_bcnt per dword: it fails on most strips at configs[1]'s
     // threshold and then costs both.)
-    constexpr bool kCheap = MODE == kModeScreen && !PROF && POOL == 0 && !NONDIR && kTB == 2 && kPf;
+    // One directional track and a window that reaches at most the
+    // neighbouring lanes' chunks (R <= 16, NH <= 4): K1a streams the track's
+    // chunk-sum plane (kernels.h: one byte per 16 positions, escapes at their
+    // counts) instead of its 2-bit fields -- a quarter of the bytes, no
+    // per-dword sums and no escape tests
+    constexpr bool kPlane = MODE == kModeScreen && !PROF && POOL == 0 && !NONDIR && kTB == 2 && NH <= 4;
+    constexpr bool kCheap = MODE == kModeScreen && !PROF && POOL == 0 && !NONDIR && kTB == 2 && kPf && !kPlane;
     u32x4 pv[MODE == kModeScreen && !PROF ? kLoads : 1];
     u32x4 phv = {0u, 0u, 0u, 0u};
     uint32_t pf_strip = 0, pf_cur = 0;
@@ -805,6 +861,19 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     uint32_t pf_escw = ~0u, pf_escb = 0;
     auto pf_issue = [&](uint32_t strip_n, uint32_t cur_n, int st, int k) {
         const UnitDesc Un = units[cur_n];
+        if constexpr (kPlane) {  // the strip's 1,024 chunk sums: 16 per lane; halos in lanes 0, 1
+            gu32x4 *pl = (gu32x4 *)(plane_u8(Un, S, st, ncs[k]) + kPlanePad +
+                                    (uint64_t)(strip_n - Un.strip0) * kPlaneStrip);
+            pv[0] = __builtin_nontemporal_load(pl + lane);
+            phv = u32x4{0u, 0u, 0u, 0u};
+            if (lane < 2) phv = pl[lane == 0 ? -1 : kPlaneStrip / 16];
+            pf_strip = strip_n;
+            pf_cur = cur_n;
+            pf_st = st;
+            pf_k = k;
+            pf_ok = true;
+            return;
+        }
         const int64_t q0 = 1 + (int64_t)(strip_n - Un.strip0) * kStrip;
         gu32x4 *t = (gu32x4 *)(track_u8(Un, S, st, ncs[k]) + fbyte(kPadPos + q0 - 1));
 #pragma unroll
@@ -861,7 +930,52 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         const int64_t p0 = 1 + (int64_t)local * kStrip;  // first position of the strip
 
         // ---- screen: which blocks can hold a flagged position ----
-        if constexpr (!PROF && MODE != kModeExact) {
+        if constexpr (kPlane) {
+            const u32x4 v = pv[0], hv = phv;
+            pf_ok = false;
+            if (it + istep < it_end) {
+                uint32_t nc_ = cur;
+                while (it + istep >= units[nc_].strip0 + units[nc_].nstrips) ++nc_;
+                pf_issue(it + istep, nc_, 0, 0);
+            }
+            // chunks 16l .. 16l+15 of lane l (a 255: >= 255 tags, unbounded)
+            uint32_t a[16];
+            {
+                const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int i = 0; i < 16; ++i) a[i] = (d[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            }
+            const bool clean = plane_clean_any<4 * NH>(R, a, hv, lane, P.wskip);
+            mchunk = 0;
+            exact_blocks = 0;
+            if (!clean) {
+                // the LDS screen of the 2-bit path over these sums: lane l's
+                // chunks, the halos' 16 chunks each side from lanes 0 and 1
+                uint32_t *d = scr + scr_at(kScrHalo + 16 * lane);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) d[i] = a[i] == 255u ? kBig : a[i];
+                if (lane < 2) {
+                    const uint32_t hd[4] = {hv.x, hv.y, hv.z, hv.w};
+                    uint32_t *h = scr + scr_at(lane == 0 ? kScrHalo - 16 : kScrHalo + kBlocks * kWave);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const uint32_t b = (hd[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                        h[i] = b == 255u ? kBig : b;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t *rd = scr + 17 * lane;  // index 16l + j = word 17l + j + j/16
+                const uint32_t m = screen_any<4 * NH>(R, rd, P.wskip, P.fw, P.fthr);
+                const uint64_t lanes = __ballot(m != 0u);
+                mchunk = m;
+#pragma unroll
+                for (int bk = 0; bk < kBlocks; ++bk)
+                    exact_blocks |= ((lanes >> (4 * bk)) & 0xFull) ? (1u << bk) : 0u;
+                __builtin_amdgcn_wave_barrier();  // the next strip reuses scr after every lane read it
+            }
+        } else if constexpr (!PROF && MODE != kModeExact) {
             // lane l of wave load q holds 16 bytes = CPL chunks: chunks
             // CPL * (64q + l) + i, i < CPL (DPC dwords each)
             constexpr int CPL = 16 / kChunkBytes, DPC = kChunkBytes / 4;
@@ -1883,6 +1997,31 @@ __global__ void __launch_bounds__(kSegBlock) seg_compact_kernel(
         ends[oe++] = src[half + k];
     }
     if (xe) { peak_pos[oe] = 0; peak_val[oe] = 0.0; ends[oe++] = (uint32_t)(p0 + kStrip - 1); }
+}
+
+// the chunk-sum planes of one unit's tracks (kernels.h): one thread per
+// chunk (the track's dword j), escaped fields at their overflow counts
+__global__ void __launch_bounds__(256) csum_kernel(const UnitDesc *units, uint32_t unit, int S) {
+    const UnitDesc U = units[unit];
+    const uint64_t nd = U.stride / 4;  // dwords (chunks) per track
+    const uint32_t ntr = (uint32_t)U.nstrands * (uint32_t)S;
+    uint8_t *plane = (uint8_t *)U.base + (uint64_t)ntr * U.stride;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntr * nd;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t t = (uint32_t)(i / nd);
+        const uint64_t j = i - (uint64_t)t * nd;
+        const uint32_t d = ((const uint32_t *)((const uint8_t *)U.base + (uint64_t)t * U.stride))[j];
+        uint32_t s = fsum32(d, 0u);  // an escaped field counts kEsc here
+        uint32_t e = fbig32(d);
+        while (e && s < 255u) {
+            const int b = __builtin_ctz(e);
+            e &= e - 1u;
+            const int64_t p = (int64_t)(16 * j) + b / kTB - kPadPos + 1;  // the field's position
+            const uint32_t c = ovf_lookup(U, t, (uint32_t)p);
+            s = s - kEsc + (c < 255u ? c : 255u);
+        }
+        plane[(uint64_t)t * nd + j] = (uint8_t)(s < 255u ? s : 255u);
+    }
 }
 
 // per-unit last add (the last position whose pooled count is nonzero): one

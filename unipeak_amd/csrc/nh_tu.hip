@@ -4,6 +4,7 @@
 // build in parallel.  Each unit exports the addresses of its kernels; api.hip
 // launches them with hipLaunchKernel (kernels.hip holds the code).
 #include "kernels.hip"
+#include "stats1.hip"
 
 #ifndef UPK_NH_TU
 #error "compile with -DUPK_NH_TU=1..8"
@@ -36,8 +37,9 @@ const void *UPK_CAT(scan_kernel_nh, UPK_NH_TU)(int pool, bool nd, bool prof, int
     return scan_ptr<2, false>(prof, mode);
 }
 
-// K3
-const void *UPK_CAT(stats_kernel_nh, UPK_NH_TU)(int pool, bool nd) {
+// K3 (one: one pooled directional sample with K1b's peaks, stats1.hip)
+const void *UPK_CAT(stats_kernel_nh, UPK_NH_TU)(int pool, bool nd, bool one) {
+    if (one) return (const void *)stats1_kernel<kNH>;
     if (nd) {
         if (pool == 0) return (const void *)stats_kernel<kNH, 0, true>;
         if (pool == 1) return (const void *)stats_kernel<kNH, 1, true>;

@@ -1,0 +1,355 @@
+// unipeak_amd/csrc/stats1.hip -- K3 for one pooled directional sample
+// (S == 1, no coefficients, one strand per unit: BASELINE configs[1]) with
+// the peaks K1b found.  Included by nh_tu.hip after kernels.hip.
+//
+// Same outputs, bit for bit, as stats_kernel's path for this case
+// (processRegion, misc/peakcall.cpp:33-53; Region::exptSums / posMean /
+// posKurtosis, misc/data.cpp:104-182; the peak score, peakcall.cpp:203-209),
+// organised around what made that path slow (profiles/r05/phases/: of its
+// 0.143 ms, 57 us were per-region load latency, 20 us the count pass
+// unrolled over 16 words whatever the region's length, 34 us the kurtosis):
+//  * a wave takes a run of consecutive regions -- one unit descriptor for
+//    most of them -- and the next region's count bytes arrive as 16-byte
+//    lane loads (one wave load per region) during the current region;
+//  * the bytes are staged in LDS and read back per 64-position word with a
+//    per-lane offset fixed for the region (rolled loops over its words);
+//  * pass 1 lists the hit positions as (offset, count) pairs in position
+//    order, so the kurtosis terms of pass 2 are formed 64 hits per
+//    instruction instead of 64 positions; the two sums then run in position
+//    order over LDS broadcasts (data.cpp:166-177).
+#pragma once
+
+namespace upk {
+
+constexpr int kS1Stage = 64 * 16;                    // staged region bytes: 64 16-byte pieces
+constexpr int kS1Words = kS1Stage / kWordBytes - 1;  // region words staged at once (63 at 2 bits)
+constexpr int kS1PkStage = 2 * ((kMaxBw + 64) / 64) * kWordBytes + 32;  // the peak window's bytes (2NH words)
+constexpr uint32_t kS1Pairs = 320;                   // hit pairs listed per region (more: per-word pass 2)
+constexpr int kS1WaveBytes = kS1Stage + kS1PkStage + (int)kS1Pairs * 8 + 64 * 16;
+constexpr size_t kStat1Lds = kKTab * sizeof(double) + 4 * (size_t)kS1WaveBytes;
+static_assert(kS1Stage % 16 == 0 && kS1PkStage % 16 == 0 && (kS1Pairs * 8) % 16 == 0, "LDS areas 16-byte aligned");
+
+// 16-byte pieces covering the field bytes of positions [first, last] (the
+// first byte rounded down to 16): lane l < n loads piece l
+struct Span {
+    int64_t base;  // first byte (16-aligned)
+    int n;         // pieces
+};
+__device__ __forceinline__ Span span_of(int64_t first_pos, int64_t last_pos) {
+    const int64_t b0 = fbyte(kPadPos + first_pos - 1) & ~(int64_t)15;
+    const int64_t b1 = fbyte(kPadPos + last_pos - 1);
+    return Span{b0, (int)((b1 - b0) / 16 + 1)};
+}
+__device__ __forceinline__ u32x4 span_load(gu8 *track, const Span &sp, int lane) {
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (lane < sp.n) v = *((gu32x4 *)(track + sp.base) + lane);
+    return v;
+}
+__device__ __forceinline__ bool piece_esc(const u32x4 &v) {
+    return (fbig32(v.x) | fbig32(v.y) | fbig32(v.z) | fbig32(v.w)) != 0u;
+}
+
+template <int NH>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) stats1_kernel(StatParams P) {
+    extern __shared__ double lds_[];
+    const int bw = P.bw;
+    const double *ktab = load_ktab(lds_, P.kern, bw);
+    constexpr int NWT = 2 * NH + 1;
+    constexpr int kPK = 2 * NH;  // peak window words (positions kpos - bw .. kpos + bw)
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    uint8_t *wb = (uint8_t *)(lds_ + kKTab) + (threadIdx.x >> 6) * kS1WaveBytes;
+    uint8_t *stg = wb;              // the region's count bytes
+    uint8_t *pstg = wb + kS1Stage;  // its peak window's bytes
+    uint2 *pairs = (uint2 *)(wb + kS1Stage + kS1PkStage);
+    double2 *terms = (double2 *)(wb + kS1Stage + kS1PkStage + kS1Pairs * 8);
+    const uint64_t nreg = *P.nreg < P.cap ? *P.nreg : P.cap;
+    uint64_t wm[NWT];
+#pragma unroll
+    for (int d = -NH; d <= NH; ++d) wm[d + NH] = win_mask(d, bw);
+    const int nc0 = P.nc[0];
+    const uint32_t trk = (uint32_t)nc0;  // (strand 0) * S + sample
+    const bool ctl0 = P.is_control[0] != 0;
+
+    // a run of consecutive regions per wave
+    const uint64_t per = (nreg + nwaves - 1) / nwaves;
+    const uint64_t rbeg = (uint64_t)wave * per < nreg ? (uint64_t)wave * per : nreg;
+    const uint64_t rend = rbeg + per < nreg ? rbeg + per : nreg;
+    auto desc_load = [&](uint64_t r) -> uint32_t {  // lanes 0..5: start, end, unit, peak, peak value
+        if (lane >= 6) return 0u;
+        const uint32_t *src = lane == 0   ? P.starts + r
+                              : lane == 1 ? P.ends + r
+                              : lane == 2 ? P.reg_unit + r
+                              : lane == 3 ? P.peak_pos + r
+                                          : (const uint32_t *)(P.peak_val + r) + (lane - 4);
+        return *src;
+    };
+    uint32_t ucur = 0xFFFFFFFFu;
+    UnitDesc U{};
+    gu8 *track = nullptr;
+    auto track_of = [&](uint32_t u) -> gu8 * {
+        if (u == ucur) return track;
+        const UnitDesc Un = P.units[u];
+        return (gu8 *)Un.base + (uint64_t)nc0 * Un.stride;
+    };
+    // the terms in terms[0, n) added in order to the two chains (wave-uniform
+    // LDS broadcasts, kTermBatch in flight)
+    auto chain = [&](int n, double &a, double &b) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int k = 0;
+        for (; k + kTermBatch <= n; k += kTermBatch) {
+            double2 v[kTermBatch];
+#pragma unroll
+            for (int i = 0; i < kTermBatch; ++i) v[i] = terms[k + i];
+#pragma unroll
+            for (int i = 0; i < kTermBatch; ++i) {
+                a = a + v[i].x;
+                b = b + v[i].y;
+            }
+        }
+        for (; k < n; ++k) {
+            const double2 v = terms[k];
+            a = a + v.x;
+            b = b + v.y;
+        }
+        __builtin_amdgcn_wave_barrier();  // terms reused
+    };
+    // compact this lane's term (when h) after the earlier lanes' into terms
+    auto compact = [&](bool h, double x, double y) -> int {
+        const uint64_t m = __ballot(h);
+        if (h) {
+            const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            terms[k] = make_double2(x, y);
+        }
+        return __builtin_popcountll(m);
+    };
+
+    uint32_t dsc = rbeg < rend ? desc_load(rbeg) : 0u;
+    u32x4 pv = {0u, 0u, 0u, 0u}, ppv = {0u, 0u, 0u, 0u};  // the next region's pieces (bytes, peak window)
+    bool pv_ok = false, ppv_ok = false;
+    for (uint64_t ri = rbeg; ri < rend; ++ri) {
+        const uint32_t left = rl_u(dsc, 0), right = rl_u(dsc, 1), u = rl_u(dsc, 2);
+        const uint64_t rn = ri + 1;
+        const uint32_t dsc_n = rn < rend ? desc_load(rn) : 0u;
+        if (u != ucur) {
+            U = P.units[u];
+            ucur = u;
+            track = (gu8 *)U.base + (uint64_t)nc0 * U.stride;
+        }
+        uint32_t kpos = rl_u(dsc, 3);
+        double kval = __longlong_as_double((long long)(((uint64_t)rl_u(dsc, 5) << 32) | rl_u(dsc, 4)));
+        const bool pre = kpos != 0;  // the peak window's bytes came with the descriptor's
+        if (kpos == 0) {
+            // the run crossed a strip edge: first maximum over its parts, in
+            // position order (as stats_kernel)
+            const uint32_t sa = U.strip0 + (left - 1) / kStrip, sb = U.strip0 + (right - 1) / kStrip;
+            for (uint32_t s = sa; s <= sb; ++s) {
+                const uint32_t sp0 = 1 + (s - U.strip0) * kStrip;
+                const bool prt = (s > sa || left == sp0) && s == sb && right < sp0 + kStrip - 1;
+                const uint64_t *e = P.spk + 4ull * s + (prt ? 0 : 2);
+                const double v = __longlong_as_double((long long)e[0]);
+                if (P.qmode) {  // Q keys: equal Q in two parts is a tie too
+                    const double fv = __builtin_floor(v), fk = __builtin_floor(kval);
+                    if (s == sa || fv > fk) {
+                        kval = v;
+                        kpos = (uint32_t)e[1];
+                    } else if (fv == fk) {
+                        kval = fk + 0.5;
+                    }
+                } else if (s == sa || v > kval) {
+                    kval = v;
+                    kpos = (uint32_t)e[1];
+                }
+            }
+        }
+        // a Q key marked +0.5 (the largest Q at two positions): the first
+        // maximum of the FP64 scores decides (the region's KDE below)
+        const bool kn = !(P.qmode && kval != __builtin_floor(kval));
+        const int nw = (int)((right - left) / 64u) + 1;
+        const bool staged = nw <= kS1Words;
+
+        // ---- the region's count bytes, staged in LDS ----
+        // lane's field of word w: byte off + kWordBytes * w, bits sh (the
+        // same for every word: a word is kWordBytes whole bytes)
+        const int64_t n0 = kPadPos + (int64_t)left - 1 + lane;
+        const uint32_t sh = fshift(n0);
+        bool esc = false;
+        int off = 0;
+        if (staged) {
+            const Span sp = span_of(left, right);
+            off = (int)(fbyte(n0) - sp.base);
+            const u32x4 v = pv_ok ? pv : span_load(track, sp, lane);
+            esc = __ballot(lane < sp.n && piece_esc(v)) != 0;
+            __builtin_amdgcn_wave_barrier();  // earlier readers of the stage are done
+            if (lane < sp.n) *(u32x4 *)(stg + 16 * lane) = v;
+        }
+        gu8 *tg = track + fbyte(n0);  // regions too long to stage read their bytes directly
+        const uint32_t lim = right - left;  // lane offsets past it hold no stored count
+        auto count_word = [&](int w) -> uint32_t {
+            const uint32_t o = 64u * (uint32_t)w + (uint32_t)lane;
+            if (o > lim) return 0u;
+            uint32_t c;
+            if (staged) {
+                c = ((uint32_t)stg[off + kWordBytes * w] >> sh) & kTMask;
+                if (esc && c == kEsc) c = ovf_lookup(U, trk, left + o);
+            } else {
+                c = ((uint32_t)tg[kWordBytes * w] >> sh) & kTMask;
+                if (c == kEsc) c = ovf_lookup(U, trk, left + o);
+            }
+            return c;
+        };
+        // the peak window (Q keys): lane t of word q holds position kpos - bw + 64q + t
+        bool pesc = false;
+        int poff = 0;
+        uint32_t psh = 0;
+        if (kn && P.qmode) {
+            const int64_t pn0 = kPadPos + (int64_t)kpos - bw - 1 + lane;
+            const Span psp = span_of((int64_t)kpos - bw, (int64_t)kpos - bw + 64 * kPK - 1);
+            poff = (int)(fbyte(pn0) - psp.base);
+            psh = fshift(pn0);
+            const u32x4 v = (pre && ppv_ok) ? ppv : span_load(track, psp, lane);
+            pesc = __ballot(lane < psp.n && piece_esc(v)) != 0;
+            if (lane < psp.n) *(u32x4 *)(pstg + 16 * lane) = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        // ---- the next region's bytes while this one is worked on ----
+        pv_ok = ppv_ok = false;
+        if (rn < rend) {
+            const uint32_t ln = rl_u(dsc_n, 0), rgn = rl_u(dsc_n, 1), un = rl_u(dsc_n, 2), kp = rl_u(dsc_n, 3);
+            gu8 *tn = track_of(un);
+            if ((rgn - ln) / 64u + 1 <= (uint32_t)kS1Words) {
+                pv = span_load(tn, span_of(ln, rgn), lane);
+                pv_ok = true;
+            }
+            if (P.qmode && kp != 0) {
+                ppv = span_load(tn, span_of((int64_t)kp - bw, (int64_t)kp - bw + 64 * kPK - 1), lane);
+                ppv_ok = true;
+            }
+        }
+
+        // ---- pass 1: exptSums, count and position moments; hit pairs ----
+        uint32_t bc = 0, bs = 0, np = 0;
+        for (int w = 0; w < nw; ++w) {
+            const uint32_t c = count_word(w);
+            const uint32_t key = (uint32_t)(uint16_t)(64 * w + lane);  // Q8: uint16 offsets
+            bc += c;
+            bs += c * key;
+            const uint64_t m = __ballot(c != 0u);
+            if (c != 0u && np <= kS1Pairs) {
+                const uint32_t k = np + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                if (k < kS1Pairs) pairs[k] = make_uint2(key, c);
+            }
+            np += (uint32_t)__builtin_popcountll(m);
+        }
+        const uint32_t count = wave_sum_u32(bc);
+        const uint32_t psum = wave_sum_u32(bs);
+        const uint32_t nonctl = ctl0 ? 0u : count;  // S == 1
+
+        // ---- pass 2: kurtosis (data.cpp:164-182; powi semantics) ----
+        const double x_bar = (double)psum / (double)count;
+        double sum2 = 0.0, sum4 = 0.0;
+        if (np <= kS1Pairs) {  // the terms of 64 hits per step
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t k0 = 0; k0 < np; k0 += 64) {
+                const uint32_t k = k0 + (uint32_t)lane;
+                if (k < np) {
+                    const uint2 pr = pairs[k];
+                    const double d = (double)pr.x - x_bar;
+                    const double d2 = d * d;
+                    terms[lane] = make_double2((double)pr.y * d2, (double)pr.y * (d2 * d2));
+                }
+                chain((int)(np - k0 < 64u ? np - k0 : 64u), sum2, sum4);
+            }
+        } else {  // many hits: per word, the positions holding a hit compacted
+            for (int w = 0; w < nw; ++w) {
+                const uint32_t c = count_word(w);
+                const double d = (double)(uint16_t)(64 * w + lane) - x_bar;
+                const double d2 = d * d;
+                const int n = compact(c != 0u, (double)c * d2, (double)c * (d2 * d2));
+                chain(n, sum2, sum4);
+            }
+        }
+        const double kurt = ((double)count - 1) * sum4 / (sum2 * sum2);
+
+        // ---- peak ----
+        double best = kval;
+        int64_t best_x = kpos;
+        if (kn && P.qmode) {
+            // score(kpos) as the reference sums it (peakcall.cpp:203-209): the
+            // hit at kpos - bw + t adds kernel[2bw - t] * countSum, in ascending t
+            double f = 0.0, zero = 0.0;
+#pragma unroll
+            for (int q = 0; q < kPK; ++q) {
+                const int t = 64 * q + lane;
+                uint32_t c = 0;
+                if (t <= 2 * bw) {
+                    c = ((uint32_t)pstg[poff + kWordBytes * q] >> psh) & kTMask;
+                    if (pesc && c == kEsc) c = ovf_lookup(U, trk, (uint32_t)((int64_t)kpos - bw + t));
+                }
+                const double kw = ktab[2 * bw - t];  // padded table: in range
+                const int n = compact(c != 0u, kw * (double)c, 0.0);
+                chain(n, f, zero);
+            }
+            best = f;
+        } else if (!kn) {
+            // tied keys: the region's KDE, first maximum of the FP64 scores
+            // (Region::addPos, data.cpp:98-101)
+            best = 0.0;
+            best_x = -1;
+            for (int64_t x0 = left; x0 <= (int64_t)right; x0 += 64) {
+                const int64_t x = x0 + lane;
+                uint32_t cf[NWT];
+                uint64_t hf[NWT];
+                load_words<NWT, 0>(cf, U, 1, 0, x0 - 64 * NH, lane, 1, P.nc, nullptr);
+#pragma unroll
+                for (int w = 0; w < NWT; ++w) hf[w] = __ballot(cf[w] != 0u);
+                const double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
+                if (x <= (int64_t)right && (best_x < 0 || f > best)) {
+                    best = f;
+                    best_x = x;
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const double ob = __shfl_xor(best, o);
+                const long long ox = __shfl_xor((long long)best_x, o);
+                if (ox >= 0 && (best_x < 0 || ob > best || (ob == best && ox < best_x))) {
+                    best = ob;
+                    best_x = ox;
+                }
+            }
+        }
+
+        // ---- processRegion filters (peakcall.cpp:33-53); strandCorr is NaN ----
+        const uint32_t n = right - left + 1;
+        bool acc = (double)nonctl >= P.hit_thr;
+        if (acc) acc = P.kurt_thr == 0 || (n > 1 && kurt <= P.kurt_thr);
+        if (acc) acc = P.corr_thr <= -1;
+        if (lane == 0) P.out_counts[ri] = count;  // exptSums[0]
+        if (lane < 7) {  // the 56-byte record as 7 words (one write burst)
+            uint64_t w;
+            switch (lane) {
+            case 0: w = (uint64_t)u | ((uint64_t)left << 32); break;
+            case 1: w = (uint64_t)right | ((uint64_t)(uint32_t)best_x << 32); break;
+            case 2: w = (uint64_t)count | ((uint64_t)nonctl << 32); break;
+            case 3: w = (uint64_t)(uint32_t)(acc ? 1 : 0) | ((uint64_t)UP_CLOSE_RULE << 32); break;
+            case 4: w = (uint64_t)__double_as_longlong(best); break;
+            case 5: w = (uint64_t)__double_as_longlong(kurt); break;
+            default: w = (uint64_t)__double_as_longlong(__builtin_nan("")); break;
+            }
+            ((uint64_t *)P.out)[ri * 7 + lane] = w;
+        }
+        dsc = dsc_n;
+    }
+}
+
+}  // namespace upk
