@@ -285,8 +285,8 @@ def main():
     # K1a algorithmic bytes per bp per strand per non-control sample: what
     # its stream reads -- the chunk-sum plane (1 byte per 16 bp) for one
     # directional track, else the TB-bit counts
-    dens = g.scan_density()  # bytes per 1,024 positions of one pooled track
-    alg_bytes = sum(lens[units[k][0]] * nstr * s_nc for k in mine) * dens // 1024
+    dens = g.scan_density()  # bytes per 1,024 positions of a unit
+    alg_bytes = sum(lens[units[k][0]] for k in mine) * dens // 1024
     copy_gbps = g.hbm_copy_gbps(1 << 30, 5)
 
     phase = {"allreduce": 0.0, "launch": 0.0, "wait": 0.0, "gather_merge": 0.0}
@@ -576,9 +576,9 @@ def main():
                          "kernel": "scan_kernel<..., kModeScreen> (K1a: stream + integer screen)",
                          "kernel_ms": round(k1a_ms, 4), "kernel_ms_max_rank": round(k1a_max, 4),
                          "bytes_per_launch": int(alg_bytes),
-                         "bytes_rule": (f"{dens / 1024} B per bp per strand per non-control sample (" +
-                                        ("chunk-sum plane: 1 byte per 16 positions" if dens * 8 != 1024 * TB
-                                         else f"{TB}-bit counts") + ")"),
+                         "bytes_rule": (f"{dens / 1024} B per bp of a unit (" +
+                                        ("chunk-sum plane: 1 byte per 16 positions of the pooled track"
+                                         if dens == 64 else f"{TB}-bit counts of every pooled track") + ")"),
                          "kernel_note": "mean K1a duration over the timed passes (HIP events on the pass "
                                         "stream); passes overlap, so K1a shares the GPU with earlier "
                                         "passes' K1b/K2/K3",
@@ -748,7 +748,7 @@ def shift_pipeline(args, W):
         ka.append(ga.timings()[0])
         kb.append(gb.timings()[0])
     dt = (time.perf_counter() - t0) / args.steps
-    alg = genome * 2 * ga.scan_density() // 1024  # K1a of each pass: both strands
+    alg = genome * ga.scan_density() // 1024  # K1a of each pass
     k1a = float(np.mean(ka + kb))
     res = {
         "metric": METRIC, "value": round(genome / dt / 1e9, 3), "unit": "Gbp/s", "n_gpus": 1,
@@ -763,7 +763,7 @@ def shift_pipeline(args, W):
                      "unit": "GB/s", "frac": round(alg / (k1a * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": None, "kernel": "scan_kernel<..., kModeScreen> (K1a), both passes",
                      "kernel_ms": round(k1a, 4), "bytes_per_launch": int(alg),
-                     "bytes_rule": f"{ga.scan_density() / 1024} B per bp per strand, both strands"},
+                     "bytes_rule": f"{ga.scan_density() / 1024} B per bp (K1a's stream)"},
     }
     print(json.dumps(res), flush=True)
     for g, _ in ctx:

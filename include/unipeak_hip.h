@@ -242,10 +242,11 @@ int up_shift_scan(up_ctx *ctx, const uint64_t *region_idx, size_t n,
 int up_shift_best(up_ctx *ctx, const uint64_t *region_idx, size_t n,
                   uint16_t max_shift, uint16_t *best_shift, double *best_corr);
 
-/* bytes the streaming scan (K1a) reads per 1,024 positions of one pooled
- * track under the current parameters (its algorithmic bytes):
- * 64 when it streams the chunk-sum plane (one directional pooled track,
- * bw <= 255), else 1024 * up_track_bits() / 8 */
+/* bytes the streaming scan (K1a) reads per 1,024 positions of a unit under
+ * the current parameters (its algorithmic bytes): 64 when it
+ * streams a chunk-sum plane (bw <= 255: the pooled track's own plane, or the
+ * unit's pooled plane of several samples / both strands), else
+ * 1024 * up_track_bits() / 8 per pooled track and strand */
 int up_scan_density(up_ctx *ctx, uint32_t *bytes_per_1024);
 /* device-side timings of the last up_run in ms: [0]=K1 scan, [1]=K2
  * segment, [2]=K3 stats, [3]=whole up_run wall, [4]=K1 launches */

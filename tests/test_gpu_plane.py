@@ -97,3 +97,31 @@ def test_plane_follows_scatter_between_passes(gpu_lib, oracle):
     ref, ref_sums = oracle.run_unit(bw, bg, p1, c1)
     compare(ref, ref_sums, regs, c)
     assert any(r["left"] <= 120_000 <= r["right"] for r in ref)
+
+
+def test_pooled_plane_follows_pooling_changes(gpu_lib, oracle):
+    """several samples screen on the unit's pooled plane (weighted by the
+    screen's sample weights, both strands of a nondirectional unit): it is
+    rebuilt when the control set or the coefficients change between passes
+    over the same tracks"""
+    rng = np.random.default_rng(11)
+    bw, bg, length, S = 50, 0.003, 160_000, 3
+    pos, cnt = random_unit(rng, length, bw, S=S)
+    settings = [dict(control=[0, 0, 1]), dict(control=[1, 0, 0]),
+                dict(control=[0, 0, 1], coeffs=[2.5, 0.4]), dict(control=[0, 0, 0])]
+    got = []
+    with gpu_lib.Lib(0) as g:
+        g.set_params(bw, S, bg, **settings[0])
+        u = g.add_unit(length)
+        for s in range(S):
+            m = cnt[:, s] != 0
+            g.scatter(u, 0, s, pos[m], cnt[m, s])
+        for kw in settings:
+            g.set_params(bw, S, bg, region_thr=25.0, kurt_thr=50.0, corr_thr=-1.0, hit_thr=10.0, **kw)
+            assert g.scan_density() == 64
+            n = g.run()
+            regs, c = g.regions(n)
+            got.append((regs.copy(), c.copy()))
+    for kw, (regs, c) in zip(settings, got):
+        ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, **kw)
+        compare(ref, ref_sums, regs, c)

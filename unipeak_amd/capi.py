@@ -335,7 +335,7 @@ class Lib:
         return v.value
 
     def scan_density(self):
-        """bytes K1a streams per 1,024 positions of one pooled track (up_scan_density)"""
+        """bytes K1a streams per 1,024 positions of a unit (up_scan_density)"""
         v = ctypes.c_uint32()
         _ck(self.L.up_scan_density(self.ctx, ctypes.byref(v)))
         return v.value

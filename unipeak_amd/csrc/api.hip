@@ -111,6 +111,7 @@ struct Unit {
     uint8_t *d_ovf_tiles = nullptr;  // [ntiles][kOvfBlk]
     bool ovf_dirty = false;
     bool cs_dirty = false;     // a track changed: rebuild its chunk-sum plane (csum_kernel)
+    bool pool_dirty = true;    // rebuild the unit's pooled plane (pool_kernel)
     uint32_t ovf_max = 0;          // largest escaped count of any track
 };
 
@@ -215,6 +216,7 @@ struct up_ctx {
     DevBuf<unsigned long long> d_dbg;
     std::vector<Unit> units;
     bool units_dirty = true;
+    std::vector<uint32_t> pool_sig;  // non-control samples + screen weights the pooled planes hold
     DevBuf<UnitDesc> d_units;
     uint32_t nstrips = 0;
     int bw_layout = -1;  // bw the strip layout was computed for
@@ -378,11 +380,13 @@ int up_track_bits(void) { return kTB; }
 // K1a's stream (scan_kernel kPlane): the chunk-sum plane for one pooled
 // directional track when the window reaches the neighbouring lanes only
 static bool plane_scan(const up_ctx *c);
+static int pool_mode(const up_ctx *c);
 
 int up_scan_density(up_ctx *c, uint32_t *b) {
     if (!c || !b) return UP_E_ARG;
     if (!c->have_params) return UP_E_STATE;
-    *b = plane_scan(c) ? 1024u / 16u : 1024u * (uint32_t)kTB / 8u;
+    *b = plane_scan(c) ? 1024u / 16u
+                       : 1024u * (uint32_t)kTB / 8u * (uint32_t)c->nc.size() * (c->p.nondir ? 2u : 1u);
     return UP_OK;
 }
 
@@ -579,6 +583,14 @@ int up_set_params(up_ctx *c, const up_params *p) {
         }
         HIPCHK(c->d_wscreen.ensure(w.size()));
         HIPCHK(hipMemcpy(c->d_wscreen.p, w.data(), w.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        // the pooled planes follow the pooling (samples and their weights)
+        std::vector<uint32_t> sig(c->nc.begin(), c->nc.end());
+        sig.insert(sig.end(), w.begin(), w.end());
+        if (sig != c->pool_sig) {
+            c->pool_sig = sig;
+            for (Unit &u : c->units) u.pool_dirty = true;
+            c->units_dirty = true;
+        }
         double kmax = 0.0;
         for (double v : c->kern) kmax = v > kmax ? v : kmax;
         const double wf = p->region_thr / (kmax * (1.0 + 1e-6));
@@ -684,8 +696,9 @@ int up_add_unit(up_ctx *c, uint32_t len, int32_t nstrands, int32_t buffer_id, ui
     u.nstrands = nstrands;
     u.buffer = buffer_id;
     u.stride = unit_stride(len);
-    // the tracks, then their chunk-sum planes (stride / 4 bytes each, kernels.h)
-    const size_t bytes = u.stride * (size_t)c->p.n_samples * nstrands / 4 * 5;
+    // the tracks, their chunk-sum planes (stride / 4 bytes each, kernels.h),
+    // the unit's pooled plane
+    const size_t bytes = u.stride * (size_t)c->p.n_samples * nstrands / 4 * 5 + u.stride / 4;
     u.ovf.resize((size_t)c->p.n_samples * nstrands);
     hipError_t e = hipMalloc(&u.dptr, bytes);
     if (e != hipSuccess) return UP_E_NOMEM;
@@ -751,7 +764,7 @@ static int pack_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample,
             for (auto v : e) m[(uint32_t)(v >> 32)] = (uint32_t)v;
         }
         u.ovf_dirty = true;
-        u.cs_dirty = true;
+        u.cs_dirty = u.pool_dirty = true;
         c->units_dirty = true;
         return UP_OK;
     }
@@ -796,7 +809,7 @@ int up_unit_scatter(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, s
             if (counts[i] >= kEsc) { m[pos[i]] = counts[i]; u.ovf_dirty = true; }
             else if (!m.empty() && m.erase(pos[i])) u.ovf_dirty = true;
         }
-        u.cs_dirty = true;  // the chunk sums change with any count
+        u.cs_dirty = u.pool_dirty = true;  // the chunk sums change with any count
         c->units_dirty = true;
     }
     // the caller's arrays are copied into the staging buffers before we
@@ -1120,6 +1133,19 @@ static int sync_units(up_ctx *c) {
         u.cs_dirty = false;
         planes = true;
     }
+    // pooled planes: several pooled tracks (or both strands) screen as one
+    if (kTB == 2 && (c->p.nondir || pool_mode(c) != 0)) {
+        for (size_t i = 0; i < c->units.size(); ++i) {
+            Unit &u = c->units[i];
+            if (!u.pool_dirty) continue;
+            const uint64_t n = u.stride / 4;
+            hipLaunchKernelGGL(pool_kernel, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 65536)), dim3(256), 0,
+                               c->stream, c->d_units.p, (uint32_t)i, (int)c->p.n_samples, (int)c->nc.size(),
+                               c->d_nc.p, c->d_wscreen.p);
+            u.pool_dirty = false;
+            planes = true;
+        }
+    }
     if (planes) {
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -1140,7 +1166,7 @@ static int pool_mode(const up_ctx *c) {
 }
 
 static bool plane_scan(const up_ctx *c) {
-    return kTB == 2 && pool_mode(c) == 0 && c->p.nondir == 0 && (c->p.bw + 64) / 64 <= 4;
+    return kTB == 2 && (c->p.bw + 64) / 64 <= 4;
 }
 
 static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps, uint32_t ovf_cap) {

@@ -42,12 +42,17 @@ constexpr int kPadBytes = 256;      // zero bytes before position 1 and after th
 constexpr int kPadPos = kPerByte * kPadBytes;  // the same padding in positions
 constexpr int kStripBytes = kStrip / kPerByte;  // one strip of one track
 constexpr int kMaxBw = 511;         // register-resident halo: NH <= 8 words (wider: the replay)
-// Chunk-sum plane (2-bit tracks): after a unit's tracks, one byte per track
+// Chunk-sum planes (2-bit tracks): after a unit's tracks, one byte per track
 // per 16-position chunk -- byte j = the tag sum of fields 16j .. 16j+15 (the
 // track's dword j), escaped fields at their overflow counts, saturated at 255
 // (>= 255 tags: unbounded for the screen).  Plane of track t at base +
-// ntracks * stride + t * (stride / 4); built by csum_kernel whenever a track
-// changes.  K1a's one-track screen streams it.
+// ntracks * stride + t * (stride / 4), built by csum_kernel whenever a track
+// changes; then the unit's pooled plane (base + ntracks * stride * 5 / 4):
+// per chunk the screen's weighted sum over the non-control samples (weights
+// ScanParams::wscreen) and both strands of a nondirectional unit, saturated
+// at 255 (pool_kernel, rebuilt when a track or the pooling changes).  K1a
+// streams the track's plane (one directional pooled track) or the pooled
+// plane.
 constexpr int kPlanePad = kPadPos / 16;      // chunks (bytes) before position 1
 constexpr int kPlaneStrip = kStrip / 16;     // chunks (bytes) of one strip
 // K1a screen: chunks of halo on each side -- kScrHalo places the halos in the

@@ -86,9 +86,12 @@ __device__ __forceinline__ gu8 *track_u8(const UnitDesc &U, int S, int strand, i
     return (gu8 *)U.base + ((uint64_t)strand * S + sample) * U.stride;
 }
 
-// a track's chunk-sum plane (kernels.h)
+// a track's chunk-sum plane, and the unit's pooled plane (kernels.h)
 __device__ __forceinline__ gu8 *plane_u8(const UnitDesc &U, int S, int strand, int sample) {
     return (gu8 *)U.base + (uint64_t)U.nstrands * S * U.stride + ((uint64_t)strand * S + sample) * (U.stride / 4);
+}
+__device__ __forceinline__ gu8 *pooled_u8(const UnitDesc &U, int S) {
+    return (gu8 *)U.base + (uint64_t)U.nstrands * S * U.stride / 4 * 5;
 }
 
 // byte and bit offset of field n (n = kPadPos + p - 1 for position p)
@@ -848,7 +851,8 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     // chunk-sum plane (kernels.h: one byte per 16 positions, escapes at their
     // counts) instead of its 2-bit fields -- a quarter of the bytes, no
     // per-dword sums and no escape tests
-    constexpr bool kPlane = MODE == kModeScreen && !PROF && POOL == 0 && !NONDIR && kTB == 2 && NH <= 4;
+    constexpr bool kPlane = MODE == kModeScreen && !PROF && kTB == 2 && NH <= 4;
+    constexpr bool kPooledPlane = NONDIR || POOL != 0;  // several tracks: the unit's pooled plane
     constexpr bool kCheap = MODE == kModeScreen && !PROF && POOL == 0 && !NONDIR && kTB == 2 && kPf && !kPlane;
     u32x4 pv[MODE == kModeScreen && !PROF ? kLoads : 1];
     u32x4 phv = {0u, 0u, 0u, 0u};
@@ -862,7 +866,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     auto pf_issue = [&](uint32_t strip_n, uint32_t cur_n, int st, int k) {
         const UnitDesc Un = units[cur_n];
         if constexpr (kPlane) {  // the strip's 1,024 chunk sums: 16 per lane; halos in lanes 0, 1
-            gu32x4 *pl = (gu32x4 *)(plane_u8(Un, S, st, ncs[k]) + kPlanePad +
+            gu32x4 *pl = (gu32x4 *)((kPooledPlane ? pooled_u8(Un, S) : plane_u8(Un, S, st, ncs[k])) + kPlanePad +
                                     (uint64_t)(strip_n - Un.strip0) * kPlaneStrip);
             pv[0] = __builtin_nontemporal_load(pl + lane);
             phv = u32x4{0u, 0u, 0u, 0u};
@@ -2021,6 +2025,23 @@ __global__ void __launch_bounds__(256) csum_kernel(const UnitDesc *units, uint32
             s = s - kEsc + (c < 255u ? c : 255u);
         }
         plane[(uint64_t)t * nd + j] = (uint8_t)(s < 255u ? s : 255u);
+    }
+}
+
+// the pooled plane of one unit (kernels.h): per chunk the weighted sum of
+// the non-control samples' planes over the unit's strands, saturated at 255
+__global__ void __launch_bounds__(256) pool_kernel(const UnitDesc *units, uint32_t unit, int S, int nnc,
+                                                   const int32_t *nc, const uint32_t *w) {
+    const UnitDesc U = units[unit];
+    const uint64_t nd = U.stride / 4;
+    const uint8_t *planes = (const uint8_t *)U.base + (uint64_t)U.nstrands * S * U.stride;
+    uint8_t *pooled = (uint8_t *)planes + (uint64_t)U.nstrands * S * nd;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t s = 0;
+        for (int st = 0; st < U.nstrands && s < 255u; ++st)
+            for (int k = 0; k < nnc && s < 255u; ++k)
+                s += w[k] * (uint32_t)planes[((uint64_t)st * S + nc[k]) * nd + j];  // w <= 4096: no wrap
+        pooled[j] = (uint8_t)(s < 255u ? s : 255u);
     }
 }
 
