@@ -853,6 +853,34 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     // per-dword sums and no escape tests
     constexpr bool kPlane = MODE == kModeScreen && !PROF && kTB == 2 && NH <= 4;
     constexpr bool kPooledPlane = NONDIR || POOL != 0;  // several tracks: the unit's pooled plane
+    // Plane path: each wave screens a run of consecutive strips -- they
+    // share a unit, so the next strips' plane addresses follow from a cursor
+    // without unit-table loads -- with the next two strips' loads in flight
+    uint32_t c_u = 0, c_s0 = 0, c_end = 0;     // unit of the strip being screened
+    uint32_t pc_u = 0, pc_s0 = 0, pc_end = 0;  // unit of the strip being prefetched
+    gu8 *pc_base = nullptr;
+    u32x4 phv2 = {0u, 0u, 0u, 0u};
+    if constexpr (kPlane) {
+        const uint32_t nsr = strip_end - strip_begin;
+        const uint32_t per = (nsr + nwaves - 1) / nwaves;
+        const uint32_t off = (uint64_t)wave * per < nsr ? wave * per : nsr;
+        it0 = strip_begin + off;
+        it_end = it0 + per < strip_end ? it0 + per : strip_end;
+        istep = 1;
+    }
+    auto pf_plane = [&](uint32_t strip_n, u32x4 &dv, u32x4 &dh) {
+        while (strip_n >= pc_end) {  // the strip's unit (first call: search)
+            pc_u = pc_end == 0 ? find_unit(units, P.nunits, strip_n) : pc_u + 1;
+            const UnitDesc Un = units[pc_u];
+            pc_s0 = Un.strip0;
+            pc_end = Un.strip0 + Un.nstrips;
+            pc_base = (kPooledPlane ? pooled_u8(Un, S) : plane_u8(Un, S, 0, ncs[0])) + kPlanePad;
+        }
+        gu32x4 *pl = (gu32x4 *)(pc_base + (uint64_t)(strip_n - pc_s0) * kPlaneStrip);
+        dv = __builtin_nontemporal_load(pl + lane);  // 16 chunk sums per lane
+        dh = u32x4{0u, 0u, 0u, 0u};
+        if (lane < 2) dh = pl[lane == 0 ? -1 : kPlaneStrip / 16];  // the halos' 16 chunks each side
+    };
     constexpr bool kCheap = MODE == kModeScreen && !PROF && POOL == 0 && !NONDIR && kTB == 2 && kPf && !kPlane;
     u32x4 pv[MODE == kModeScreen && !PROF ? kLoads : 1];
     u32x4 phv = {0u, 0u, 0u, 0u};
@@ -865,19 +893,6 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     uint32_t pf_escw = ~0u, pf_escb = 0;
     auto pf_issue = [&](uint32_t strip_n, uint32_t cur_n, int st, int k) {
         const UnitDesc Un = units[cur_n];
-        if constexpr (kPlane) {  // the strip's 1,024 chunk sums: 16 per lane; halos in lanes 0, 1
-            gu32x4 *pl = (gu32x4 *)((kPooledPlane ? pooled_u8(Un, S) : plane_u8(Un, S, st, ncs[k])) + kPlanePad +
-                                    (uint64_t)(strip_n - Un.strip0) * kPlaneStrip);
-            pv[0] = __builtin_nontemporal_load(pl + lane);
-            phv = u32x4{0u, 0u, 0u, 0u};
-            if (lane < 2) phv = pl[lane == 0 ? -1 : kPlaneStrip / 16];
-            pf_strip = strip_n;
-            pf_cur = cur_n;
-            pf_st = st;
-            pf_k = k;
-            pf_ok = true;
-            return;
-        }
         const int64_t q0 = 1 + (int64_t)(strip_n - Un.strip0) * kStrip;
         gu32x4 *t = (gu32x4 *)(track_u8(Un, S, st, ncs[k]) + fbyte(kPadPos + q0 - 1));
 #pragma unroll
@@ -896,7 +911,10 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         pf_k = k;
         pf_ok = true;
     };
-    if constexpr (MODE == kModeScreen && !PROF && kPf) {
+    if constexpr (kPlane) {
+        if (it0 < it_end) pf_plane(it0, pv[0], phv);
+        if (it0 + 1 < it_end) pf_plane(it0 + 1, pv[1], phv2);
+    } else if constexpr (MODE == kModeScreen && !PROF && kPf) {
         if (it0 < it_end) pf_issue(it0, find_unit(units, P.nunits, it0), 0, 0);
     }
     for (uint32_t it = it0; it < it_end; it += istep) {
@@ -925,23 +943,28 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             if (lane == 0) atomicAdd(&P.dbg[8 + __builtin_popcount(exact_blocks)], 1ull);  // blocks per item
 #endif
             if (cur == 0xFFFFu) cur = find_unit(units, P.nunits, strip);
+        } else if constexpr (kPlane) {
+            while (strip >= c_end) {
+                c_u = c_end == 0 ? find_unit(units, P.nunits, strip) : c_u + 1;
+                c_s0 = units[c_u].strip0;
+                c_end = c_s0 + units[c_u].nstrips;
+            }
+            cur = c_u;
         } else {
             if (!have) { cur = find_unit(units, P.nunits, strip); have = true; }
             while (strip >= units[cur].strip0 + units[cur].nstrips) ++cur;
         }
-        const UnitDesc U = units[cur];
-        const uint32_t local = strip - U.strip0;
+        const UnitDesc U = kPlane ? UnitDesc{} : (UnitDesc)units[cur];
+        const uint32_t local = kPlane ? strip - c_s0 : strip - U.strip0;
+        const uint32_t unstrips = kPlane ? c_end - c_s0 : U.nstrips;
         const int64_t p0 = 1 + (int64_t)local * kStrip;  // first position of the strip
 
         // ---- screen: which blocks can hold a flagged position ----
         if constexpr (kPlane) {
             const u32x4 v = pv[0], hv = phv;
-            pf_ok = false;
-            if (it + istep < it_end) {
-                uint32_t nc_ = cur;
-                while (it + istep >= units[nc_].strip0 + units[nc_].nstrips) ++nc_;
-                pf_issue(it + istep, nc_, 0, 0);
-            }
+            pv[0] = pv[1];
+            phv = phv2;
+            if (it + 2 < it_end) pf_plane(it + 2, pv[1], phv2);
             // chunks 16l .. 16l+15 of lane l (a 255: >= 255 tags, unbounded)
             uint32_t a[16];
             {
@@ -1296,7 +1319,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         }
         if constexpr (MODE == kModeScreen) {
             if (exact_blocks == 0) {  // no run can touch this strip
-                const uint64_t info = ((uint64_t)(local == 0) << 34) | ((uint64_t)(local + 1 == U.nstrips) << 35);
+                const uint64_t info = ((uint64_t)(local == 0) << 34) | ((uint64_t)(local + 1 == unstrips) << 35);
                 if (lane == 0) P.strip_info[strip] = info;
             } else {
                 // into this wave's stash: multi-block strips from its front,
@@ -1642,7 +1665,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         }
         const uint64_t info = (uint64_t)R_.ns | ((uint64_t)R_.ne << 16) | ((F0 & 1ull) << 32) |
                               ((uint64_t)open << 33) | ((uint64_t)(local == 0) << 34) |
-                              ((uint64_t)(local + 1 == U.nstrips) << 35) |
+                              ((uint64_t)(local + 1 == unstrips) << 35) |
                               ((uint64_t)(R_.slot != kInline) << 36);
         if (lane == 0) P.strip_info[strip] = info;
 #ifdef UPK_DEBUG_TIMES
