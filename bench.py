@@ -109,7 +109,7 @@ def load_table(names):
 def pmc_traffic(bytes_per_launch):
     """HBM bytes per K1a launch from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.py) when they were taken on this exact workload."""
-    for rnd in ("r04", "r03", "r02", "r01"):
+    for rnd in ("r05", "r04", "r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", rnd, "k1a_pmc_traffic.json")
         try:
             d = json.load(open(p))

@@ -173,10 +173,14 @@ int up_reset_units(up_ctx *ctx);
  * threshold <= 0 makes the leap branch of processPosition live (quirk Q11):
  * with non-negative scores every run of processed positions is a region,
  * found in parallel (K1q; records as UP_CLOSE_Q11 / UP_CLOSE_Q11_HEAD
- * describe), except when a unit processes position 1 (an add at <= bw + 1)
- * or a coefficient is negative.  Those, and bw > UP_MAX_PARALLEL_BW (511:
- * K1's register-resident halo of NH <= 8 64-position words), run the exact
- * state machine instead (K0 replay, sequential per buffer: exact, slow).
+ * describe).  A unit that processes position 1 (an add at <= bw + 1) adds a
+ * short exact replay (K0) around it, from the start of the buffer's
+ * previous unit's last run to the first clean leap past it; those records
+ * name their closing add in close_pos like the whole-buffer replay's.  A
+ * negative coefficient, the -w capture with such a unit, and bw >
+ * UP_MAX_PARALLEL_BW (511: K1's register-resident halo of NH <= 8
+ * 64-position words) run the exact state machine over every unit instead
+ * (K0 replay, sequential per buffer: exact, slow).
  * up_run_async refuses both (UP_E_UNSUPPORTED); up_unit_profile* refuse the
  * replay.  up_shift_scan correlates a replayed region's stored scores
  * (Region::scores), as strandCorr does.

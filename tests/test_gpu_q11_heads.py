@@ -1,0 +1,193 @@
+"""Threshold <= 0 with units that process position 1 (an add at <= bw + 1):
+K1q runs every unit in parallel and the exact replay (K0) covers only the
+chains around those units -- from the start of the buffer's previous unit's
+last run to the first leap past the head that closes the open region over a
+clean window (api.hip q11_finish, emulate.hip `q11`).  The
+reference semantics: misc/peakcall.cpp:55-86 (the leap branch), 164-168 (the
+open region relabelled by the next contig), 177-183 (quirk Q1's window).
+
+Every table byte-identical to the oracle CLI; the same tables again with
+UNIPEAK_Q11_HEADS=replay (round 4's whole-buffer replay); and the hg19-like
+case of VERDICT r4 item 4 (chr19-chr22 plus a chrM-like contig with tags at
+positions 3 and 40) timed against its -r 25 pass through the C API."""
+import os
+import time
+import zlib
+
+import numpy as np
+import pytest
+
+from tests.test_cli import BIN, compare_tool, gen_head_sample, gen_sample, run
+from tests.wig import write_contigs, write_wig
+
+pytestmark = pytest.mark.gpu
+
+SMALL = [("c0", 9000), ("c1", 4000), ("c2", 400), ("c3", 7000), ("c4", 5000), ("c5", 12_000)]
+
+CASES = [
+    # (name, bw, samples, args, tiny contigs: tags only at <= bw, Q1 leak)
+    ("dir_bw50", 50, 1, ["-f", "-r", "0"], ()),
+    ("dir_bw50_leaks", 50, 1, ["-f", "-r", "0"], ("c1", "c3")),
+    ("dir_bw50_leak_run", 50, 1, ["-f", "-r", "0"], ("c1", "c2", "c3")),
+    ("dir_bw20_negative_thr", 20, 1, ["-f", "-r", "-1", "-k", "0", "-t", "0"], ("c4",)),
+    ("dir_bw100_controls", 100, 2, ["-f", "-r", "0", "-e", "2"], ("c2",)),
+    ("dir_bw7_coeffs", 7, 3, ["-r", "0", "-e", "3", "-z", "0.5,2"], ("c1",)),
+    ("nondir_bw50_corr", 50, 1, ["-D", "-y", "-f", "-r", "0"], ("c2",)),
+    ("nondir_bw90_two", 90, 2, ["-D", "-f", "-r", "0"], ("c1", "c5")),
+    ("dir_bw255", 255, 1, ["-f", "-r", "0", "-k", "0"], ("c3",)),
+]
+
+
+def _inputs(tmp_path, name, bw, ns, tiny, contigs=SMALL):
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    ct = tmp_path / "contigs.txt"
+    write_contigs(ct, contigs)
+    files = []
+    for i in range(ns):
+        fwd, rev = gen_head_sample(rng, contigs, bw, tiny)
+        p = tmp_path / f"s{i}.wig"
+        write_wig(p, f"s{i}", fwd, rev)
+        files.append(str(p))
+    return str(ct), files
+
+
+def _same_as_whole_replay(tmp_path, args, ref_name):
+    """bin/regions with the whole-buffer replay forced: the same bytes"""
+    env = dict(os.environ, UNIPEAK_Q11_HEADS="replay")
+    out = tmp_path / "whole.txt"
+    import subprocess
+    r = subprocess.run([os.path.join(BIN, "regions")] + args + ["-o", str(out)], cwd=tmp_path,
+                       capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert out.read_bytes() == (tmp_path / ref_name).read_bytes()
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c[0])
+@pytest.mark.parametrize("thr_m", ["3000", "100000"])
+def test_q11_head_chains_cli(orc_bin, gpu_lib, tmp_path, case, thr_m):
+    name, bw, ns, args, tiny = case
+    ct, files = _inputs(tmp_path, name + thr_m, bw, ns, tiny)
+    full = ["-q", "-c", ct, "-b", str(bw), "-m", thr_m] + args + files
+    out = compare_tool(orc_bin, tmp_path, "regions", full)
+    assert out.count("\n") > 3
+    _same_as_whole_replay(tmp_path, full, "ref_out.txt")
+
+
+@pytest.mark.parametrize("order", ["head_first", "heads_adjacent", "head_last"])
+def test_q11_head_positions_in_buffer(orc_bin, gpu_lib, tmp_path, order):
+    """heads at the buffer's start (a chain from a fresh state), two heads in
+    a row (the second one's start point inside the first one's chain), and
+    at the buffer's end (the chain's open region is never closed)"""
+    contigs = {"head_first": [("h0", 3000), ("a", 20_000), ("b", 15_000)],
+               "heads_adjacent": [("a", 20_000), ("h0", 3000), ("h1", 5000), ("b", 15_000)],
+               "head_last": [("a", 20_000), ("b", 15_000), ("h0", 6000)]}[order]
+    rng = np.random.default_rng(zlib.crc32(order.encode()))
+    fwd, rev = gen_sample(rng, contigs, lo=60, n_cl=3, sd=40)
+    for d in (fwd, rev):
+        for cname, _ in contigs:
+            if cname.startswith("h"):
+                dense = dict(d.get(cname, []))
+                for p in (3, 40, 51):
+                    dense[p] = dense.get(p, 0) + 2
+                d[cname] = sorted(dense.items())
+    ct = tmp_path / "contigs.txt"
+    write_contigs(ct, contigs)
+    write_wig(tmp_path / "s0.wig", "s0", fwd, rev)
+    full = ["-q", "-c", str(ct), "-b", "50", "-m", "3000", "-f", "-r", "0", "s0.wig"]
+    compare_tool(orc_bin, tmp_path, "regions", full)
+    _same_as_whole_replay(tmp_path, full, "ref_out.txt")
+
+
+# ---- hg19-like contigs plus a chrM-like contig ----------
+
+HG = [("chr19", 59_128_983, 18), ("chr20", 63_025_520, 19), ("chrM", 16_571, 24),
+      ("chr21", 48_129_895, 20), ("chr22", 51_304_566, 21)]
+
+
+def _hg_tracks(oracle, contigs, seed, bw=50):
+    """per contig and strand the generator's (pos, cnt), chrM-like contigs
+    with extra tags at positions 3 and 40"""
+    out = {}
+    for name, L, ci in contigs:
+        for st in (0, 1):
+            pos, cnt = oracle.synth_track(seed, ci, st, False, L, bw, True)
+            if name == "chrM":
+                d = {int(p): int(c) for p, c in zip(pos, cnt)}
+                d[3] = d.get(3, 0) + 2
+                d[40] = d.get(40, 0) + 1
+                pos = np.array(sorted(d), np.uint32)
+                cnt = np.array([d[int(p)] for p in pos], np.uint32)
+            out[(name, st)] = (pos, cnt)
+    return out
+
+
+def _write_hg(path, oracle, contigs, tracks, name):
+    with open(path, "wb") as f:
+        total = sum(int(c.sum()) for _, c in tracks.values())
+        f.write(f"# original_file=synthetic\n# tags={total}\n".encode())
+        for st in (0, 1):
+            sign = "+" if st == 0 else "-"
+            f.write(f'track name="{name} {sign}" description="{name}" priority=3 visibility=full '
+                    'type=wiggle_0 alwaysZero=on color=0,0,255\n'.encode())
+            for cname, _, _ in contigs:
+                pos, cnt = tracks[(cname, st)]
+                if pos.size:
+                    f.write(f"variableStep chrom={cname}\n".encode())
+                    f.write(oracle.format_pairs(pos, cnt, st == 1))
+
+
+def test_q11_hg19_like_with_chrm_heads(orc_bin, gpu_lib, oracle, tmp_path):
+    """chr19-chr22 with a chrM-like contig between chr20 and chr21 carrying
+    tags at positions 3 and 40: -r 0 byte-identical to the oracle CLI"""
+    tracks = _hg_tracks(oracle, HG, 1000)
+    write_contigs(tmp_path / "contigs.txt", [(n, L) for n, L, _ in HG])
+    _write_hg(tmp_path / "s0.wig", oracle, HG, tracks, "s0")
+    out = compare_tool(orc_bin, tmp_path, "regions",
+                       ["-q", "-f", "-r", "0", "-c", "contigs.txt", "s0.wig"], "hg_r0.txt")
+    assert sum(1 for l in out.splitlines() if l.startswith("chrM:")) >= 1
+    assert out.count("\n") > 1000
+
+
+def test_q11_hg19_like_negative_coefficient_replays(orc_bin, gpu_lib, oracle, tmp_path):
+    """the same layout at a few Mbp per contig with two samples and a
+    negative -z coefficient (scores can go below 0: the whole-buffer replay)"""
+    small = [(n, min(L, 2_500_000), ci) for n, L, ci in HG]
+    write_contigs(tmp_path / "contigs.txt", [(n, L) for n, L, _ in small])
+    for i, seed in enumerate((1000, 1001)):
+        _write_hg(tmp_path / f"s{i}.wig", oracle, small, _hg_tracks(oracle, small, seed), f"s{i}")
+    out = compare_tool(orc_bin, tmp_path, "regions",
+                       ["-q", "-f", "-r", "0", "-z", "1.5,-0.25", "-c", "contigs.txt", "s0.wig", "s1.wig"],
+                       "hg_neg.txt")
+    assert out.count("\n") > 100
+
+
+def test_q11_hg19_like_time_against_r25(gpu_lib, oracle):
+    """the -r 0 pass (K1q + the chains around chrM) within 10x of the -r 25
+    pass over the same units, and its records equal to
+    the whole-buffer replay's"""
+    tracks = _hg_tracks(oracle, HG, 1000)
+    capi = gpu_lib
+
+    def timed(thr, reps=5):
+        with capi.Lib(0) as g:
+            g.set_params(50, 1, 0.003, region_thr=thr)
+            for b in (0, 1):
+                for name, L, _ in HG:
+                    u = g.add_unit(L, buffer_id=b)
+                    pos, cnt = tracks[(name, b)]
+                    g.scatter(u, 0, 0, pos, cnt)
+            g.run()  # warm-up
+            best = float("inf")
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                n = g.run()
+                best = min(best, time.perf_counter() - t0)
+            regs, _ = g.regions(n)
+            return best, regs.copy()
+
+    t25, _ = timed(25.0)
+    t0_, regs = timed(0.0)
+    assert (regs["close_pos"] < 0xFFFFFFFD).any()  # the replay closed some (chrM's chains)
+    assert (regs["close_pos"] >= 0xFFFFFFFD).any()  # and K1q the rest
+    print(f"-r 25 {t25 * 1e3:.2f} ms, -r 0 {t0_ * 1e3:.2f} ms ({t0_ / t25:.1f}x)")
+    assert t0_ <= 10 * t25, (t0_, t25)

@@ -4,8 +4,8 @@
   the leap position joins the region without setting its left end,
   misc/peakcall.cpp:76-78), so regions are not maximal runs of flags.  With
   non-negative scores every run of processed positions is a region, found in
-  parallel (K1q); a negative coefficient or a unit that
-  processes position 1 takes the exact replay below;
+  parallel (K1q); a negative coefficient takes the exact
+  replay below, a unit that processes position 1 a short chain of it;
 * kernel bandwidth > 511 -- wider than the scan's register-resident halo
   (NH <= 8 window words; round 3 stopped at 255):
   the exact state machine on the GPU over every unit (K0 replay,
@@ -171,8 +171,9 @@ def test_q11_dense_runs_and_spills(gpu_lib, oracle, bw):
     compare(ref, ref_sums, regs, gcnt)
 
 
-def test_q11_head_unit_takes_the_replay(gpu_lib, oracle):
-    """an add at <= bw + 1 processes position 1: the whole-buffer replay"""
+def test_q11_head_unit_takes_a_replay_chain(gpu_lib, oracle):
+    """an add at <= bw + 1 processes position 1: the exact replay covers the
+    unit's start up to its first clean leap, K1q the rest (test_gpu_q11_heads)"""
     rng = np.random.default_rng(813)
     length, bw, bg = 50_000, 50, 0.003
     pos, cnt = random_unit(rng, length, bw)
@@ -181,7 +182,8 @@ def test_q11_head_unit_takes_the_replay(gpu_lib, oracle):
     ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, region_thr=0.0)
     regs, gcnt = run_units(gpu_lib, bw, bg, [(length, pos, cnt, None)], region_thr=0.0)
     compare(ref, ref_sums, regs, gcnt)
-    assert np.all(regs["close_pos"] != 0xFFFFFFFE)
+    assert regs["close_pos"][0] != 0xFFFFFFFE  # the chain's record
+    assert np.all(regs["close_pos"][1:] == 0xFFFFFFFE)  # K1q's
 
 
 def test_q11_blocking_only_profile_allowed(gpu_lib, oracle):

@@ -24,6 +24,23 @@ def _stale(target, sources):
     return any(os.path.getmtime(s) > t for s in sources)
 
 
+def _includes(src, seen=None):
+    """src and the files it #includes with quotes, recursively (from its
+    own directory or include/)"""
+    import re
+    seen = set() if seen is None else seen
+    if src in seen or not os.path.exists(src):
+        return seen
+    seen.add(src)
+    for m in re.finditer(r'^\s*#\s*include\s+"([^"]+)"', open(src, errors="replace").read(), re.M):
+        for d in (os.path.dirname(src), os.path.join(ROOT, "include")):
+            f = os.path.join(d, m.group(1))
+            if os.path.exists(f):
+                _includes(f, seen)
+                break
+    return seen
+
+
 def _run(cmd, cwd=ROOT):
     print("+", " ".join(cmd), flush=True)
     subprocess.run(cmd, cwd=cwd, check=True)
@@ -45,13 +62,18 @@ def compile_lib(out, extra=(), jobs=None):
              ("tir", os.path.join(csrc, "tir.hip"), []),
              ("countmap", os.path.join(csrc, "countmap.hip"), [])] + [
         (f"nh{k}", os.path.join(csrc, "nh_tu.hip"), [f"-DUPK_NH_TU={k}"]) for k in range(1, 9)]
+    stamp = os.path.join(objdir, "flags.txt")  # objects built with other flags are stale
+    same = os.path.exists(stamp) and open(stamp).read() == " ".join(flags)
     def one(u):
         name, src, defs = u
         obj = os.path.join(objdir, name + ".o")
-        _run([HIPCC] + flags + defs + ["-c", "-o", obj, src])
+        if not same or _stale(obj, _includes(src)):
+            _run([HIPCC] + flags + defs + ["-c", "-o", obj, src])
         return obj
     with ThreadPoolExecutor(jobs or min(7, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(one, units))
+    with open(stamp, "w") as f:
+        f.write(" ".join(flags))
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
     return out
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <unordered_map>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -21,6 +22,7 @@
 #include "kernels.hip"  // device code shared with the per-NH units (nh_tu.hip)
 #include "stats1.hip"   // (its LDS size)
 #include "emulate.hip"
+#include "q11place.hip"
 
 namespace upk {
 // the templated K1 / K3 / K4 kernels live in four translation units, one per
@@ -269,7 +271,8 @@ struct up_ctx {
         uint64_t req_reg_cap = 0;    // record / overflow capacities: the caller's thread
         uint32_t req_ovf_cap = 0;    // grows them, the launcher thread only reads these
         int req_tl = 0;
-        bool req_q11 = false;        // K1q instead of K1a/K1x/K1b (threshold <= 0, run_q11)
+        bool req_q11 = false;
+        bool req_q11_place = false;  // the pass places its K1q records (q11_place)        // K1q instead of K1a/K1x/K1b (threshold <= 0, run_q11)
         bool lpending = false;       // queued for / being launched by the launcher thread
         int lrc = 0;                 // its launch result
         uint64_t cap = 0;            // reg_cap at launch
@@ -296,6 +299,7 @@ struct up_ctx {
     DevBuf<uint32_t> d_resync, d_emu_n, d_emu_err, d_emu_counts, d_ring_hits, d_reg_hit, d_reg_hits;
     DevBuf<int32_t> d_unit_buffer;
     DevBuf<uint32_t> d_gunits, d_goff;  // K0 chain groups (emulate_units)
+    DevBuf<uint32_t> d_gskip, d_gstop, d_emu_group;  // threshold <= 0 chains (Q11Chains)
     DevBuf<double> d_reg_f, d_reg_r;
     DevBuf<up_region> d_emu_out;
     DevBuf<double> d_ring_f, d_ring_r;   // K0 window in global memory (very wide kernels)
@@ -327,8 +331,20 @@ struct up_ctx {
     // and per host record the unit whose tracks hold its positions (a region
     // closed in the buffer's next unit keeps the previous unit's positions)
     bool q11_run = false;
-    std::vector<uint32_t> h_src_unit;
     DevBuf<uint32_t> d_q11_head;
+    // K1q records finished on the device (q11place.hip): K3's stage, the
+    // per-unit placement, the head chains' edits, and per placed record its
+    // stored positions and source unit (up_shift_scan); q11_rep: the
+    // replayed records among them (index, offset of their stored scores)
+    bool q11_place_in_pass = false;  // the pass places its records itself (no heads)
+    bool q11_placed = false;         // the current records are a placed K1q list
+    DevBuf<up_region> d_q11_stage;
+    DevBuf<uint32_t> d_q11_stage_cnt;
+    DevBuf<Q11Place> d_q11_tab;
+    DevBuf<uint64_t> d_q11_scr;
+    DevBuf<Q11Edit> d_q11_edit;
+    DevBuf<uint32_t> d_q11_st, d_q11_en, d_q11_src;
+    std::vector<std::pair<uint64_t, uint64_t>> q11_rep;
     std::vector<up_region> h_regions;
     std::vector<uint32_t> h_counts;
     std::vector<uint8_t> h_emulated;
@@ -502,6 +518,10 @@ void up_close(up_ctx *c) {
     c->d_sh_pref.release();
     c->d_pf_unit.release(); c->d_pf_event.release(); c->d_pf_pos.release(); c->d_pf_score.release();
     c->d_pf_n.release();
+    c->d_gunits.release(); c->d_goff.release(); c->d_gskip.release(); c->d_gstop.release();
+    c->d_emu_group.release(); c->d_q11_head.release();
+    c->d_q11_stage.release(); c->d_q11_stage_cnt.release(); c->d_q11_tab.release(); c->d_q11_scr.release();
+    c->d_q11_edit.release(); c->d_q11_st.release(); c->d_q11_en.release(); c->d_q11_src.release();
     for (int k = 0; k < kSlots; ++k) {
         c->hp_regions[k].release(); c->hp_counts[k].release(); c->hp_status[k].release(); c->hp_head[k].release();
         for (auto &e : c->pass[k].ev) (void)hipEventDestroy(e);
@@ -1323,6 +1343,16 @@ static bool q11_mode(const up_ctx *c) {
     return !off;
 }
 
+// UNIPEAK_Q11_HEADS=replay: units that process position 1 send the whole
+// context to the whole-buffer replay (round 4's rule; A/B and tests)
+static bool q11_whole_replay() {
+    static const bool on = [] {
+        const char *e = getenv("UNIPEAK_Q11_HEADS");
+        return e && std::strcmp(e, "replay") == 0;
+    }();
+    return on;
+}
+
 static bool replay_mode(const up_ctx *c) {
     return c->p.bw > kMaxBw || (!(c->p.region_thr > 0) && !q11_mode(c));
 }
@@ -1369,13 +1399,23 @@ static int launch_seg_count_head(up_ctx *c, int slot) {
     return UP_OK;
 }
 
+// threshold <= 0 chains for K0 (run_q11): group g = units gunits[goff[g] ..
+// goff[g + 1]) of one buffer, replayed from position gskip[g] of its first
+// unit; out: where each group stopped (unit, leap position; ~0: ran to its
+// end) and the group of each replayed record
+struct Q11Chains {
+    std::vector<uint32_t> gunits, goff{0}, gskip;
+    std::vector<uint32_t> gstop, rgroup;
+};
+
 // K0: run the exact state machine (emulate.hip) over the units flagged in
-// d_head (replay_all: over every unit, never resynced) -> its regions, their
-// exptSums and the per-unit resync positions.  Capacity of the region
-// record area and of one open region grow until the replay fits.
+// d_head (replay_all: over every unit, never resynced; q: the threshold <= 0
+// chains instead) -> its regions, their exptSums and the per-unit resync
+// positions.  Capacity of the region record area and of one open region
+// grow until the replay fits.
 static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std::vector<up_region> &emu,
                          std::vector<uint32_t> &ecnt,
-                         std::vector<uint32_t> &resync, std::vector<uint64_t> &soff) {
+                         std::vector<uint32_t> &resync, std::vector<uint64_t> &soff, Q11Chains *q = nullptr) {
     const uint32_t nu = (uint32_t)c->units.size();
     const int S = c->p.n_samples;
     const uint32_t W = 2u * c->p.bw + 1;
@@ -1388,7 +1428,7 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
     // (it cannot leave state behind), so independent head-hit units replay in
     // parallel instead of one wave walking the buffer
     std::vector<uint32_t> aligned(nu, 0);
-    if (!replay_all && nu) {
+    if (!replay_all && !q && nu) {
         HIPCHK(c->d_q11_head.ensure(nu));
         HIPCHK(hipMemsetAsync(c->d_q11_head.p, 0, nu * sizeof(uint32_t), c->stream));
         hipLaunchKernelGGL(unit_aligned_kernel, dim3(nu), dim3(256), 0, c->stream, c->d_units.p, S, (int)c->p.bw,
@@ -1411,16 +1451,27 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
         }
     }
     std::vector<uint32_t> gunits, goff{0};
-    for (const auto &g : groups) {
-        gunits.insert(gunits.end(), g.begin(), g.end());
-        goff.push_back((uint32_t)gunits.size());
+    if (q) {
+        gunits = q->gunits;
+        goff = q->goff;
+    } else {
+        for (const auto &g : groups) {
+            gunits.insert(gunits.end(), g.begin(), g.end());
+            goff.push_back((uint32_t)gunits.size());
+        }
     }
-    const uint32_t ngroups = (uint32_t)groups.size();
+    const uint32_t ngroups = (uint32_t)goff.size() - 1;
     HIPCHK(c->d_gunits.ensure(std::max<size_t>(gunits.size(), 1)));
     HIPCHK(c->d_goff.ensure(goff.size()));
     if (!gunits.empty())
         HIPCHK(hipMemcpy(c->d_gunits.p, gunits.data(), gunits.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_goff.p, goff.data(), goff.size() * 4, hipMemcpyHostToDevice));
+    if (q) {
+        if (q->gskip.size() != ngroups) return UP_E_INTERNAL;
+        HIPCHK(c->d_gskip.ensure(std::max(ngroups, 1u)));
+        HIPCHK(c->d_gstop.ensure(2 * std::max(ngroups, 1u)));
+        if (ngroups) HIPCHK(hipMemcpy(c->d_gskip.p, q->gskip.data(), ngroups * 4, hipMemcpyHostToDevice));
+    }
     HIPCHK(c->d_resync.ensure(nu));
     HIPCHK(c->d_emu_n.ensure(1));
     HIPCHK(c->d_emu_err.ensure(1));
@@ -1502,7 +1553,14 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
         E.out_score_off = c->d_emu_score_off.p;
         E.nscores = c->d_emu_nscores.p;
         E.scores_cap = c->d_emu_scores.n;
-        if (c->prof_capture) {
+        if (q) {
+            HIPCHK(c->d_emu_group.ensure(out_cap));
+            E.q11 = 1;
+            E.gskip = c->d_gskip.p;
+            E.gstop = c->d_gstop.p;
+            E.out_group = c->d_emu_group.p;
+        }
+        if (c->prof_capture && !q) {
             HIPCHK(c->d_pf_unit.ensure(c->pf_cap));
             HIPCHK(c->d_pf_event.ensure(c->pf_cap));
             HIPCHK(c->d_pf_pos.ensure(c->pf_cap));
@@ -1547,7 +1605,13 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
             continue;
         }
         c->h_resync = resync;
-        if (c->prof_capture) {  // the captured retirements, grouped by unit (emission order kept)
+        if (q) {
+            q->gstop.resize(2 * (size_t)ngroups);
+            q->rgroup.resize(nemu);
+            if (ngroups) HIPCHK(hipMemcpy(q->gstop.data(), c->d_gstop.p, 2 * ngroups * 4, hipMemcpyDeviceToHost));
+            if (nemu) HIPCHK(hipMemcpy(q->rgroup.data(), c->d_emu_group.p, nemu * 4, hipMemcpyDeviceToHost));
+        }
+        if (c->prof_capture && !q) {  // the captured retirements, grouped by unit (emission order kept)
             unsigned long long np = 0;
             HIPCHK(hipMemcpy(&np, c->d_pf_n.p, sizeof np, hipMemcpyDeviceToHost));
             std::vector<uint32_t> pu(np), pe(np), pp(np);
@@ -1695,6 +1759,42 @@ static void key_add(std::vector<uint8_t> &k, const T &v) {
 
 // K1x -> K1b -> K2a -> K2b -> K3 of a pass on ps.stream (the timing events
 // between them only at timing level 2, never while capturing)
+// a K1q pass's records in the reference's form (q11place.hip) on `st`: the
+// per-unit placement (with the head chains' edits, or none) and, if
+// `scatter`, the copy from K3's stage into the pass's record destination
+static int q11_place(up_ctx *c, int slot, hipStream_t st, const Q11Edit *d_edit, bool scatter) {
+    up_ctx::Pass &ps = c->pass[slot];
+    const uint32_t nu = (uint32_t)c->units.size();
+    HIPCHK(c->d_q11_tab.ensure(std::max(nu, 1u)));
+    HIPCHK(c->d_q11_scr.ensure(2 * (size_t)std::max(nu, 1u)));
+    up_region *out;
+    uint32_t *oc;
+    uint64_t dcap;
+    if (ps.target) {
+        out = (up_region *)(ps.target + 8);
+        oc = (uint32_t *)(ps.target + 8 + ps.target_cap * sizeof(up_region));
+        dcap = ps.target_cap;
+    } else {
+        out = c->hp_regions[slot].dev;
+        oc = c->hp_counts[slot].dev;
+        dcap = std::min<uint64_t>(c->hp_regions[slot].n, c->hp_counts[slot].n / (uint64_t)c->p.n_samples);
+    }
+    hipLaunchKernelGGL(q11_table_kernel, dim3(1), dim3(1024), 0, st, c->d_unit_buffer.p, nu, ps.d_runit.p,
+                       ps.d_starts.p, ps.d_nreg.p, d_edit, c->d_q11_tab.p, c->d_q11_scr.p, c->hp_status[slot].dev,
+                       (unsigned long long *)ps.target, dcap);
+    HIPCHK(hipGetLastError());
+    if (!scatter) return UP_OK;
+    HIPCHK(c->d_q11_st.ensure(dcap + 1));
+    HIPCHK(c->d_q11_en.ensure(dcap + 1));
+    HIPCHK(c->d_q11_src.ensure(dcap + 1));
+    const unsigned blocks = (unsigned)std::min<uint64_t>((ps.cap + 255) / 256 + 1, 4096);
+    hipLaunchKernelGGL(q11_scatter_kernel, dim3(blocks), dim3(256), 0, st, c->d_q11_stage.p,
+                       c->d_q11_stage_cnt.p, ps.d_nreg.p, (int)c->p.n_samples, c->d_q11_tab.p, out, oc, dcap,
+                       c->d_q11_st.p, c->d_q11_en.p, c->d_q11_src.p);
+    HIPCHK(hipGetLastError());
+    return UP_OK;
+}
+
 static int enqueue_rest(up_ctx *c, int slot, const ScanParams &SP, const StatParams &P, uint64_t cap,
                         uint32_t k1a_waves, uint32_t k1a_xcap, bool events) {
     up_ctx::Pass &ps = c->pass[slot];
@@ -1721,6 +1821,8 @@ static int enqueue_rest(up_ctx *c, int slot, const ScanParams &SP, const StatPar
     if (events) HIPCHK(hipEventRecord(ps.ev[3], ps.stream));
     dispatch_stats(c, ps.stream, P, std::max<uint64_t>(ps.req_last_nreg, 1024));
     HIPCHK(hipGetLastError());
+    if (ps.req_q11_place)
+        if (int r = q11_place(c, slot, ps.stream, nullptr, true)) return r;
     if (events) HIPCHK(hipEventRecord(ps.ev[4], ps.stream));
     return UP_OK;
 }
@@ -1841,6 +1943,12 @@ static int launch_pass(up_ctx *c, int slot) {
         P.peak_pos = nullptr;  // K3 runs its KDE for the peaks
         P.peak_val = nullptr;
         P.q11 = 1;
+        // K3 -> the device stage; q11place.hip places the records
+        HIPCHK(c->d_q11_stage.ensure(cap + 1));
+        HIPCHK(c->d_q11_stage_cnt.ensure((cap + 1) * S));
+        P.out = c->d_q11_stage.p;
+        P.out_counts = c->d_q11_stage_cnt.p;
+        P.cap = cap;
         const unsigned blocks = (unsigned)std::min<uint64_t>((ns + 3) / 4, 4096);
         hipLaunchKernelGGL(proc_runs_kernel, dim3(std::max(1u, blocks)), dim3(256), 0, s1, SP);
     } else {
@@ -1965,6 +2073,7 @@ int up_run_async(up_ctx *c) {
     ps.req_target_cap = c->target_cap;
     ps.req_tl = c->timing;
     ps.req_q11 = c->q11_run;
+    ps.req_q11_place = c->q11_run && c->q11_place_in_pass;
     ps.req_last_nreg = c->last_nreg;
     ps.req_reg_cap = c->reg_cap;
     ps.req_ovf_cap = c->ovf_cap;
@@ -1995,6 +2104,7 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
     c->ran = false;
     c->nreg = 0;
     c->host_regions = false;
+    c->q11_placed = false;
     c->cur_slot = slot;
     if (c->units.empty()) {
         ++c->seq_done;
@@ -2056,7 +2166,8 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
     }
     c->nreg = nreg;
     c->last_nreg = nreg;
-    int r = replay_head_hits(c, slot);
+    // (a K1q pass's head units take q11_finish's chains instead)
+    int r = ps.req_q11 ? UP_OK : replay_head_hits(c, slot);
     if (r) return fail(r);
     const int tl = ps.tl;
     float a = 0, b = 0, d = 0, x = 0;
@@ -2084,6 +2195,7 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
     c->ran = false;
     c->nreg = 0;
     c->host_regions = false;
+    c->q11_placed = false;
     c->h_regions.clear();
     c->h_counts.clear();
     c->h_emulated.clear();
@@ -2125,7 +2237,8 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
     return UP_OK;
 }
 
-// the records of a K1q pass -> the reference's regions (host list):
+// the records of a K1q pass -> the reference's regions, placed on the device
+// (q11place.hip; without heads already inside the pass):
 //  * every run [s, e] was reached by a leap: Region::left = s + 1, right =
 //    e + 1, peak = (first maximum over s + 1 .. e) + 1 (K3 skipped s), its
 //    statistics over s .. e as K3 computed them (peakcall.cpp:76-78,
@@ -2134,94 +2247,191 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
 //  * the last run of a unit is still open after its flush: the buffer's
 //    next unit relabels it (peakcall.cpp:164-168) and its first leap closes
 //    it -- the record moves there (UP_CLOSE_Q11_HEAD, positions still the
-//    previous unit's); the buffer's last unit's last run is never closed
-static int q11_finish(up_ctx *c) {
-    const up_ctx::Pass &ps = c->pass[c->cur_slot];
+//    previous unit's); the buffer's last unit's last run is never closed;
+//  * heads (units with an add at <= bw + 1, which process position 1 --
+//    continuing the open region across the unit boundary -- or land the
+//    misaligned window of quirk Q1): the exact replay (K0) covers each one
+//    from the start of the buffer's previous unit's last run (a leap: the
+//    window there holds only that add, so a fresh state is exact) to the
+//    first leap past the head that closes the open region over a clean
+//    window (Q11Chains); K1q's records before that leap and the moved one
+//    give way to the replay's, those from the leap on stay (Q11Edit).  A
+//    chain that reaches a later head's start point covers it too (that
+//    head's own chain is dropped).
+static int q11_finish(up_ctx *c, const std::vector<uint32_t> *heads) {
+    const int slot = c->cur_slot;
+    up_ctx::Pass &ps = c->pass[slot];
     const int S = c->p.n_samples;
     const uint32_t nu = (uint32_t)c->units.size();
-    const up_region *par = c->hp_regions[c->cur_slot].p;
-    const uint32_t *pcnt = c->hp_counts[c->cur_slot].p;
-    std::vector<up_region> dpar;
-    std::vector<uint32_t> dcnt;
-    if (ps.target && ps.target_hostp) {
-        par = (const up_region *)((const uint8_t *)ps.target_hostp + 8);
-        pcnt = (const uint32_t *)((const uint8_t *)ps.target_hostp + 8 + ps.target_cap * sizeof(up_region));
-    } else if (ps.target) {
-        dpar.resize(c->nreg);
-        dcnt.resize((size_t)c->nreg * S);
-        if (c->nreg) {
-            HIPCHK(hipMemcpy(dpar.data(), ps.target + 8, c->nreg * sizeof(up_region), hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(dcnt.data(), ps.target + 8 + ps.target_cap * sizeof(up_region),
-                             dcnt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-        }
-        par = dpar.data();
-        pcnt = dcnt.data();
-    }
-    std::vector<uint64_t> first(nu + 1, c->nreg);  // records of unit u: [first[u], first[u + 1])
-    for (uint64_t i = c->nreg; i-- > 0;) first[par[i].unit] = i;
-    for (uint32_t u = nu; u-- > 0;) first[u] = std::min(first[u], first[u + 1]);
-    std::vector<int64_t> moved_in(nu, -1);  // the record a unit closes for its buffer's previous unit
-    int64_t prev[2] = {-1, -1};
-    for (uint32_t u = 0; u < nu; ++u) {
-        if (first[u] == first[u + 1]) continue;  // no adds: no relabel (add() never ran)
-        const int b = c->units[u].buffer;
-        if (prev[b] >= 0) moved_in[u] = (int64_t)first[prev[b] + 1] - 1;
-        prev[b] = u;
-    }
-    c->h_regions.clear();
-    c->h_counts.clear();
-    c->h_emulated.clear();
-    c->h_score_off.clear();
-    c->h_src_unit.clear();
-    auto push = [&](uint64_t i, uint32_t unit, uint32_t close) {
-        up_region r = par[i];
-        c->h_src_unit.push_back(r.unit);
-        r.left += 1;
-        r.right += 1;
-        r.peak += 1;
-        r.unit = unit;
-        r.close_pos = close;
-        c->h_regions.push_back(r);
-        c->h_counts.insert(c->h_counts.end(), pcnt + i * S, pcnt + (i + 1) * S);
-        c->h_emulated.push_back(2);
-        c->h_score_off.push_back(~0ull);
-    };
-    for (uint32_t u = 0; u < nu; ++u) {
-        if (moved_in[u] >= 0) push((uint64_t)moved_in[u], u, UP_CLOSE_Q11_HEAD);
-        for (uint64_t i = first[u]; i + 1 < first[u + 1]; ++i) push(i, u, UP_CLOSE_Q11);
-    }
+    c->host_regions = false;
+    c->q11_placed = true;
+    c->q11_rep.clear();
     c->h_resync.assign(nu, 0);
     c->h_pf_off.assign(nu + 1, 0);
-    return publish_host_regions(c, ps);
+    const unsigned long long *st = c->hp_status[slot].p;
+    if (!heads) {  // placed inside the pass
+        c->nreg = st[3] ? st[3] - 1 : 0;
+        return UP_OK;
+    }
+    // each unit's K1q records (the placement table without edits)
+    HIPCHK(hipStreamSynchronize(ps.stream));
+    if (int r = q11_place(c, slot, c->stream, nullptr, false)) return r;
+    std::vector<Q11Place> tab(nu);
+    HIPCHK(hipMemcpyAsync(tab.data(), c->d_q11_tab.p, nu * sizeof(Q11Place), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    // the chains: one per head, from the start of the buffer's previous unit
+    // with records' last run (its raw start s: the add at s + bw begins it)
+    struct G { int b; uint32_t k0; uint64_t s; };  // buffer, start index in its order, run start (0: fresh)
+    std::vector<G> gs;
+    Q11Chains q;
+    std::vector<uint32_t> order[2];
+    for (uint32_t u = 0; u < nu; ++u) order[c->units[u].buffer].push_back(u);
+    for (int b = 0; b < 2; ++b) {
+        const std::vector<uint32_t> &o = order[b];
+        int64_t pw = -1;  // the previous unit with records (index into o)
+        for (uint32_t k = 0; k < o.size(); ++k) {
+            const uint32_t u = o[k];
+            if ((*heads)[u]) {
+                G g{b, k, 0};
+                uint32_t skip = 1;
+                if (pw >= 0) {
+                    const uint32_t pu = o[(size_t)pw];
+                    uint32_t s0 = 0;
+                    HIPCHK(hipMemcpy(&s0, ps.d_starts.p + tab[pu].first + tab[pu].cnt - 1, 4, hipMemcpyDeviceToHost));
+                    g.k0 = (uint32_t)pw;
+                    g.s = s0;
+                    skip = (uint32_t)(g.s + c->p.bw);
+                }
+                q.gunits.insert(q.gunits.end(), o.begin() + g.k0, o.end());
+                q.goff.push_back((uint32_t)q.gunits.size());
+                q.gskip.push_back(skip);
+                gs.push_back(g);
+            }
+            if (tab[u].cnt) pw = k;
+        }
+    }
+    std::vector<up_region> emu;
+    std::vector<uint32_t> ecnt, resync;
+    std::vector<uint64_t> soff;
+    if (int r = emulate_units(c, c->d_q11_head.p, true, emu, ecnt, resync, soff, &q)) return r;
+    c->h_resync.assign(nu, 0);
+    // keep a chain unless an earlier kept chain of its buffer reached past
+    // its start point; the edits of the kept ones
+    std::vector<Q11Edit> ed(nu, Q11Edit{0u, 0xFFFFFFFFu, 0u, 0u});
+    std::vector<uint8_t> kept(gs.size(), 0);
+    int64_t last[2] = {-1, -1};
+    for (size_t g = 0; g < gs.size(); ++g) {
+        const G &G_ = gs[g];
+        const std::vector<uint32_t> &o = order[G_.b];
+        if (last[G_.b] >= 0) {
+            const size_t l = (size_t)last[G_.b];
+            if (q.gstop[2 * l] == ~0u) continue;  // ran to the buffer's end
+            const uint32_t sk = (uint32_t)(std::find(o.begin(), o.end(), q.gstop[2 * l]) - o.begin());
+            if (sk > G_.k0 || (sk == G_.k0 && q.gstop[2 * l + 1] > G_.s)) continue;  // covered
+        }
+        kept[g] = 1;
+        last[G_.b] = (int64_t)g;
+        const bool stopped = q.gstop[2 * g] != ~0u;
+        const uint32_t sk = stopped ? (uint32_t)(std::find(o.begin(), o.end(), q.gstop[2 * g]) - o.begin())
+                                    : (uint32_t)o.size();
+        uint32_t k = G_.k0;
+        if (G_.s) ed[o[k++]].hi = (uint32_t)G_.s;
+        for (; k < sk; ++k) ed[o[k]].flags |= kQ11Full;
+        if (stopped) {
+            ed[q.gstop[2 * g]].lo = q.gstop[2 * g + 1];
+            ed[q.gstop[2 * g]].flags |= kQ11NoMove;
+        }
+    }
+    // the kept chains' records per unit, in emission order
+    std::vector<std::vector<uint32_t>> rep(nu);
+    for (uint32_t i = 0; i < emu.size(); ++i)
+        if (kept[q.rgroup[i]]) rep[emu[i].unit].push_back(i);
+    for (uint32_t u = 0; u < nu; ++u) ed[u].nrep = (uint32_t)rep[u].size();
+    HIPCHK(c->d_q11_edit.ensure(std::max(nu, 1u)));
+    HIPCHK(hipMemcpy(c->d_q11_edit.p, ed.data(), nu * sizeof(Q11Edit), hipMemcpyHostToDevice));
+    // place K1q's records around the replayed ones (growing the pinned
+    // record area when the replay adds more than K1q dropped)
+    uint64_t total = 0;
+    for (int attempt = 0;; ++attempt) {
+        if (int r = q11_place(c, slot, c->stream, c->d_q11_edit.p, true)) return r;
+        HIPCHK(hipStreamSynchronize(c->stream));
+        total = st[3] ? st[3] - 1 : 0;
+        const uint64_t dcap = ps.target ? ps.target_cap
+                                        : std::min<uint64_t>(c->hp_regions[slot].n, c->hp_counts[slot].n / (uint64_t)S);
+        if (total <= dcap) break;
+        if (ps.target || attempt) return UP_E_NOMEM;
+        HIPCHK(c->hp_regions[slot].ensure(total + 1));
+        HIPCHK(c->hp_counts[slot].ensure((total + 1) * S));
+        st = c->hp_status[slot].p;
+    }
+    // the replayed records into their slots: after the unit's moved-in one
+    std::vector<uint64_t> scr(2 * (size_t)nu);
+    HIPCHK(hipMemcpy(scr.data(), c->d_q11_scr.p, scr.size() * 8, hipMemcpyDeviceToHost));
+    for (uint32_t u = 0; u < nu; ++u) {
+        uint64_t d = scr[2 * u] + (scr[2 * u + 1] & 1u);
+        for (uint32_t i : rep[u]) {
+            const up_region &r = emu[i];
+            const uint32_t *k = ecnt.data() + (size_t)i * S;
+            if (ps.target && ps.target_hostp) {
+                uint8_t *h = (uint8_t *)ps.target_hostp;
+                std::memcpy(h + 8 + d * sizeof(up_region), &r, sizeof r);
+                std::memcpy(h + 8 + ps.target_cap * sizeof(up_region) + d * S * 4, k, S * 4);
+            } else if (ps.target) {
+                HIPCHK(hipMemcpy(ps.target + 8 + d * sizeof(up_region), &r, sizeof r, hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(ps.target + 8 + ps.target_cap * sizeof(up_region) + d * S * 4, k, S * 4,
+                                 hipMemcpyHostToDevice));
+            } else {
+                c->hp_regions[slot].p[d] = r;
+                std::memcpy(c->hp_counts[slot].p + d * S, k, S * 4);
+            }
+            const uint32_t sh[3] = {r.left, r.right, r.unit};  // (stored scores: the extent only)
+            HIPCHK(hipMemcpy(c->d_q11_st.p + d, &sh[0], 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->d_q11_en.p + d, &sh[1], 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->d_q11_src.p + d, &sh[2], 4, hipMemcpyHostToDevice));
+            c->q11_rep.push_back({d, soff[i]});
+            ++d;
+        }
+    }
+    c->nreg = total;
+    return UP_OK;
 }
 
 static int run_replay(up_ctx *c, uint64_t *n_regions);
 
-// threshold <= 0 (q11_mode): one K1q pass, unless a unit processes position
-// 1 (an add at <= bw + 1), which the whole-buffer replay handles
+// threshold <= 0 (q11_mode): one K1q pass; units that process position 1
+// (an add at <= bw + 1) add the chains of the exact replay around them
+// (q11_finish).  With the -w capture on, the whole-buffer replay instead.
 static int run_q11(up_ctx *c, uint64_t *n_regions) {
     HIPCHK(hipSetDevice(c->dev));
     int r = sync_units(c);
     if (r) return r;
     const uint32_t nu = (uint32_t)c->units.size();
+    std::vector<uint32_t> f(nu, 0);
+    bool any = false;
     if (nu) {
         HIPCHK(c->d_q11_head.ensure(nu));
         HIPCHK(hipMemsetAsync(c->d_q11_head.p, 0, nu * sizeof(uint32_t), c->stream));
         hipLaunchKernelGGL(q11_head_kernel, dim3(nu), dim3(256), 0, c->stream, c->d_units.p,
                            (int)c->p.n_samples, (int)c->p.bw, c->d_q11_head.p);
         HIPCHK(hipGetLastError());
-        std::vector<uint32_t> f(nu);
         HIPCHK(hipMemcpyAsync(f.data(), c->d_q11_head.p, nu * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        for (uint32_t v : f)
-            if (v) return run_replay(c, n_regions);
+        for (uint32_t v : f) any |= v != 0;
+        if (any && (c->prof_capture || q11_whole_replay())) return run_replay(c, n_regions);
+        std::vector<int32_t> ub(nu);  // the placement's buffer column
+        for (uint32_t i = 0; i < nu; ++i) ub[i] = c->units[i].buffer;
+        HIPCHK(c->d_unit_buffer.ensure(nu));
+        HIPCHK(hipMemcpy(c->d_unit_buffer.p, ub.data(), nu * sizeof(int32_t), hipMemcpyHostToDevice));
     }
     c->q11_run = true;
+    c->q11_place_in_pass = !any;
     r = up_run_async(c);
     if (!r) r = up_run_wait(c, nullptr);
     c->q11_run = false;
     if (r) return r;
-    if ((r = q11_finish(c))) return r;
+    const auto t0 = std::chrono::steady_clock::now();
+    if ((r = q11_finish(c, any ? &f : nullptr))) return r;
+    c->times[3] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (n_regions) *n_regions = c->nreg;
     return UP_OK;
 }
@@ -2344,17 +2554,29 @@ static int shift_run(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shif
     HIPCHK(hipSetDevice(c->dev));
     up_ctx::Pass &ps = c->pass[c->cur_slot];  // the last completed pass's region lists
     std::vector<uint32_t> st(c->nreg), en(c->nreg);
-    if (c->host_regions) {
+    std::unordered_map<uint64_t, uint64_t> qrep;  // placed K1q list: its replayed records
+    if (c->q11_placed) {
+        // K1q records: their stored positions left - 1 .. right - 1 of their
+        // source unit, as q11_scatter_kernel wrote them
+        for (const auto &e : c->q11_rep) qrep[e.first] = e.second;
+        if (c->nreg) {
+            HIPCHK(hipMemcpy(st.data(), c->d_q11_st.p, c->nreg * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(en.data(), c->d_q11_en.p, c->nreg * 4, hipMemcpyDeviceToHost));
+        }
+        HIPCHK(ps.d_starts.ensure(c->nreg + 1));
+        HIPCHK(ps.d_ends.ensure(c->nreg + 1));
+        HIPCHK(ps.d_runit.ensure(c->nreg + 1));
+        HIPCHK(hipMemcpy(ps.d_starts.p, c->d_q11_st.p, c->nreg * 4, hipMemcpyDeviceToDevice));
+        HIPCHK(hipMemcpy(ps.d_ends.p, c->d_q11_en.p, c->nreg * 4, hipMemcpyDeviceToDevice));
+        HIPCHK(hipMemcpy(ps.d_runit.p, c->d_q11_src.p, c->nreg * 4, hipMemcpyDeviceToDevice));
+    } else if (c->host_regions) {
         // replayed (Q1) regions carry state-machine scores the dense KDE
         // cannot reproduce; refuse rather than return something else
         std::vector<uint32_t> un(c->nreg);
         for (uint64_t i = 0; i < c->nreg; ++i) {
-            // K1q records (h_emulated 2): positions left - 1 .. right - 1 of
-            // their source unit
-            const bool q = c->h_emulated[i] == 2;
-            st[i] = c->h_regions[i].left - (q ? 1u : 0u);
-            en[i] = c->h_regions[i].right - (q ? 1u : 0u);
-            un[i] = q ? c->h_src_unit[i] : c->h_regions[i].unit;
+            st[i] = c->h_regions[i].left;
+            en[i] = c->h_regions[i].right;
+            un[i] = c->h_regions[i].unit;
         }
         // replayed regions (Q1 heads, whole-buffer replay) correlate the
         // scores the state machine stored (Region::scores), copied below
@@ -2376,7 +2598,8 @@ static int shift_run(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shif
     for (size_t j = 0; j < n; ++j) {
         if (idx[j] >= c->nreg) return UP_E_ARG;
         const uint64_t len = (uint64_t)en[idx[j]] - st[idx[j]] + 1;
-        pref[j] = c->host_regions && c->h_emulated[idx[j]] == 1 ? 1 : 0;
+        pref[j] = c->q11_placed ? (qrep.count(idx[j]) ? 1 : 0)
+                                : (c->host_regions && c->h_emulated[idx[j]] == 1 ? 1 : 0);
         if (pref[j] || len > (uint64_t)kShiftLds) {
             off[j] = tot;
             tot += 2ull * len;
@@ -2397,7 +2620,7 @@ static int shift_run(up_ctx *c, const uint64_t *idx, size_t n, uint16_t max_shif
     HIPCHK(hipMemcpyAsync(d_off, off.data(), n * 8, hipMemcpyHostToDevice, c->stream));
     for (size_t j = 0; j < n; ++j) {
         if (!pref[j]) continue;
-        const uint64_t so = c->h_score_off[idx[j]];
+        const uint64_t so = c->q11_placed ? qrep[idx[j]] : c->h_score_off[idx[j]];
         if (so == ~0ull) return UP_E_INTERNAL;
         const uint64_t len = (uint64_t)en[idx[j]] - st[idx[j]] + 1;
         HIPCHK(hipMemcpyAsync(d_slab + off[j], c->d_emu_scores.p + so, 2 * len * sizeof(double),

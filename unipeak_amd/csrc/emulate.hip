@@ -77,6 +77,18 @@ struct EmuParams {
     double *prof_score;
     unsigned long long *nprof;
     uint64_t prof_cap;
+    // threshold <= 0 chains (run_q11): group g replays from its first unit
+    // (its adds at >= gskip[g]: the start of that unit's last run) with a
+    // fresh state, and stops after the first leap it processes -- outside
+    // that first unit -- that closes the open region with a clean window
+    // (no Q1 leftovers, every add aligned since the last full drain): from
+    // there on K1q's records hold.  gstop[2g] / [2g + 1] = (unit, leap
+    // position) or ~0 when the group ran to its end; out_group[slot] = the
+    // group of each record
+    int32_t q11;
+    const uint32_t *gskip;
+    uint32_t *gstop;
+    uint32_t *out_group;
 };
 
 constexpr uint32_t kFlushEvent = 0xFFFFFFFFu;
@@ -100,6 +112,10 @@ struct EmuState {
     bool aligned;
     uint64_t horizon;     // positions <= horizon may hold misaligned leftovers
     bool resynced;
+    // q11 chains: the window holds only aligned adds since a full drain (or
+    // a clean unit start); a leap may end the chain; where it did; the group
+    bool clean, may_stop;
+    uint32_t stop_pos, group;
 };
 
 __device__ static bool any_at(const EmuParams &P, uint32_t u, int strand, int s, uint64_t p) {
@@ -176,6 +192,7 @@ __device__ static void emu_region(const EmuParams &P, EmuState &E) {
             atomicOr(P.err, 8u);
         }
     }
+    if (keep && P.out_group) P.out_group[slot] = E.group;
     if (keep) {
         up_region &o = P.out[slot];
         o.unit = E.cur_unit;
@@ -226,6 +243,9 @@ __device__ static void emu_process(const EmuParams &P, EmuState &E, uint32_t pos
     const double f = E.rf[cell], r = E.rr[cell];
     const int hc = E.rhas[cell] ? cell : -1;
     const double score = f + r;
+    // q11 chain end: a leap that closes the open region (left set, or
+    // nothing open) over a clean window
+    const bool stop = P.q11 && E.may_stop && pos != E.last_pos + 1 && E.clean && (E.left != 0 || E.n == 0);
     if (pos == E.last_pos + 1) {
         if (E.left != 0) {
             if (score >= P.region_thr) emu_addpos(P, E, hc, f, r);
@@ -252,6 +272,10 @@ __device__ static void emu_process(const EmuParams &P, EmuState &E, uint32_t pos
     E.last_pos = pos;
     // resync: aligned, leftovers retired, nothing open
     if (!P.replay_all && E.aligned && (uint64_t)pos > E.horizon && E.n == 0) E.resynced = true;
+    if (stop) {
+        E.resynced = true;
+        E.stop_pos = pos;
+    }
 }
 
 // ProfileBuffer::add (peakcall.cpp:161-222) without the contig switch
@@ -270,6 +294,9 @@ __device__ static void emu_add(const EmuParams &P, EmuState &E, const uint32_t *
                 E.head = (E.head + 1) % E.W;
             }
         }
+        if (E.buffer_pos > (uint32_t)P.bw && n_static == E.W) E.clean = true;  // every cell retired
+    } else if (pos <= (uint32_t)P.bw) {
+        E.clean = false;  // quirk Q1: the unit's first add lands misaligned
     }
     if (E.resynced) return;
     double cs = 0.0;
@@ -329,10 +356,19 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
 
     for (uint32_t g = blockIdx.x; g < P.ngroups; g += gridDim.x) {
     bool in_chain = false;
+    if (P.q11 && lane == 0) {
+        P.gstop[2 * g] = 0xFFFFFFFFu;
+        P.gstop[2 * g + 1] = 0xFFFFFFFFu;
+        E.group = g;
+        E.clean = true;
+    }
     for (uint32_t gk = P.goff[g]; gk < P.goff[g + 1]; ++gk) {
         const uint32_t u = P.gunits[gk];
+        // q11 chains start at their group's first unit and end for good
+        const bool q11_first = P.q11 && gk == P.goff[g];
+        if (P.q11 && !in_chain && !q11_first) break;
         if (!in_chain) {
-            if (!P.unit_head[u]) continue;
+            if (!q11_first && !P.unit_head[u]) continue;
             // chain start: fresh buffer state (the previous unit ended clean)
             if (lane == 0) {
                 for (uint32_t j = 0; j < E.W; ++j) { rf[j] = 0.0; rr[j] = 0.0; rhas[j] = 0; }
@@ -353,13 +389,15 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
             E.aligned = false;
             E.horizon = ~0ull;
             E.resynced = false;
+            E.may_stop = !(q11_first && P.gskip[g] > 1);  // not inside the start unit's last run
         }
         const UnitDesc U = P.units[u];
         const int nstr = U.nstrands;
+        const uint64_t from = q11_first ? P.gskip[g] : 1;
         if (lane == 0) stop_flag = 0;
         __syncthreads();
         // walk the unit's add() positions in order, 64 at a time
-        for (uint64_t base = 1; base <= U.len && !stop_flag; base += 64) {
+        for (uint64_t base = from; base <= U.len && !stop_flag; base += 64) {
             const uint64_t p = base + lane;
             uint32_t any0 = 0, any1 = 0;
             if (p <= U.len) {
@@ -404,12 +442,20 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
                 E.buffer_pos = 0;
                 E.last_pos = 0;
                 P.resync[u] = 0xFFFFFFFFu;
-                bool clean = E.n == 0;
-                for (uint32_t j = 0; j < E.W && clean; ++j)
-                    clean = rf[j] == 0.0 && rr[j] == 0.0 && !rhas[j];
-                stop_flag = clean ? 1 : 0;
+                bool win = true;
+                for (uint32_t j = 0; j < E.W && win; ++j)
+                    win = rf[j] == 0.0 && rr[j] == 0.0 && !rhas[j];
+                E.clean = win;
+                // a q11 chain carries its open region on: only a leap ends it
+                stop_flag = !P.q11 && win && E.n == 0 ? 1 : 0;
             }
-            if (E.resynced) stop_flag = 1;
+            if (E.resynced) {
+                stop_flag = 1;
+                if (P.q11) {
+                    P.gstop[2 * g] = u;
+                    P.gstop[2 * g + 1] = E.stop_pos;
+                }
+            }
         }
         __syncthreads();
         if (stop_flag) in_chain = false;

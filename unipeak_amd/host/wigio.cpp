@@ -576,11 +576,11 @@ bool WigStream::decode_rest(std::vector<Tag> &out, unsigned threads) {
     // (A) serially: text lines through parse(), runs of other lines cut out
     // as segments with the state they start in
     struct Seg {
-        const LexedFile::Chunk *ch;
-        size_t b, e;
+        const LexedFile::Chunk *ch = nullptr;
+        size_t b = 0, e = 0;
         Align state;
-        int format;
-        size_t at;  // insertion point in out (records before it come first)
+        int format = 0;
+        size_t at = 0;  // insertion point in out (records before it come first)
         std::vector<Tag> tags;
         uint64_t total = 0, oob = 0, confident = 0;
     };
