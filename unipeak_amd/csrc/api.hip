@@ -1477,7 +1477,7 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
     HIPCHK(c->d_emu_err.ensure(1));
     // the window in LDS when it fits (64 KiB), else in global scratch
     const size_t ring_bytes = (size_t)W * (2 * sizeof(double) + 1);
-    const bool ring_lds = ring_bytes <= 65536 - 64;
+    const bool ring_lds = ring_bytes + sizeof(EmuLds) <= 65536 - 64;
     for (int attempt = 0;; ++attempt) {
         if (attempt == 6) return UP_E_NOMEM;
         const uint32_t reg_cap = c->emu_reg_cap, out_cap = c->emu_out_cap;

@@ -16,8 +16,11 @@
 // no region is open -- and records the resync position X: regions of that
 // unit starting at or after X come from K1-K3 unchanged, earlier ones from
 // here.  A chain that ends a unit dirty continues into the buffer's next unit.
-// Lane 0 runs the state machine; the wave scans for adds 64 positions at a
-// time.  Everything is sequential FP64 in the reference's order.
+// The wave runs the state machine in lockstep (identical state in every
+// lane): the window update of an add, the per-sample work and a region's
+// statistics are split over the lanes, every FP64 sum keeps the reference's
+// order (per-lane terms staged in LDS, added up in position order), and the
+// wave scans for adds 64 positions at a time.
 
 namespace upk {
 
@@ -122,82 +125,156 @@ __device__ static bool any_at(const EmuParams &P, uint32_t u, int strand, int s,
     return fld_at(track_u8(P.units[u], P.S, strand, s), (int64_t)p) != 0;
 }
 
+// Every lane of the wave runs the state machine on identical copies of
+// EmuState (wave-uniform control flow); the loops over the window, the
+// samples and a region's positions are split over the lanes, and every sum
+// whose order the reference fixes is added up in that order from a stage of
+// 64 per-lane terms in LDS (each lane reads the same broadcast values, so the
+// copies stay identical).  Stores and atomics of a single value go through
+// lane 0.
+struct EmuLds {
+    uint32_t counts[256];   // the current add's counts per sample
+    double t0[64], t1[64], t2[64];
+};
+
+__device__ __forceinline__ void emu_sync() { __syncthreads(); }  // one wave per workgroup
+
+// the 64 staged terms of a chunk of `m` positions, added in position order
+__device__ __forceinline__ double emu_add_terms(double acc, const double *t, int m) {
+    for (int k = 0; k < m; ++k) acc = acc + t[k];
+    return acc;
+}
+
+__device__ __forceinline__ uint32_t emu_wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+
 // processRegion (peakcall.cpp:33-53) + Region statistics, appended to out
-__device__ static void emu_region(const EmuParams &P, EmuState &E) {
+__device__ static void emu_region(const EmuParams &P, EmuState &E, EmuLds &L) {
     const int S = P.S;
-    uint32_t slot = atomicAdd(P.nout, 1u);
-    uint32_t sums_local[1];
-    (void)sums_local;
+    const int lane = threadIdx.x;
+    emu_sync();  // the region's positions and hit vectors, stored by other lanes
+    uint32_t slot = 0;
+    if (lane == 0) slot = atomicAdd(P.nout, 1u);
+    slot = (uint32_t)__shfl((int)slot, 0);
     const bool keep = slot < P.out_cap;
-    if (!keep) atomicOr(P.err, 2u);
+    if (!keep && lane == 0) atomicOr(P.err, 2u);
+    const uint32_t n = E.n;
+    // exptSums per sample (integer sums: any order)
     uint32_t nonctl = 0, total = 0;
     for (int s = 0; s < S; ++s) {
-        uint32_t acc = 0;
-        for (uint32_t i = 0; i < E.n; ++i)
-            if (E.ghit[i] != 0xFFFFFFFFu) acc += E.ghits[(uint64_t)E.ghit[i] * S + s];
+        uint32_t part = 0;
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t h = E.ghit[i];
+            if (h != 0xFFFFFFFFu) part += E.ghits[(uint64_t)h * S + s];
+        }
+        const uint32_t acc = emu_wave_sum(part);
         if (!P.is_control[s]) nonctl += acc;
         total += acc;
-        if (keep) P.out_counts[(uint64_t)slot * S + s] = acc;
+        if (keep && lane == (s & 63)) P.out_counts[(uint64_t)slot * S + s] = acc;
     }
-    // posMean / posKurtosis with a UShort position index (data.cpp:133-182)
-    uint32_t count = 0, psum = 0;
-    uint16_t pos = 0;
-    for (uint32_t i = 0; i < E.n; ++i, ++pos)
-        if (E.ghit[i] != 0xFFFFFFFFu) {
-            uint32_t pc = 0;
-            for (int s = 0; s < S; ++s) pc += E.ghits[(uint64_t)E.ghit[i] * S + s];
-            count += pc;
-            psum += pc * (uint32_t)pos;
-        }
+    // posMean / posKurtosis with a UShort position index (data.cpp:133-182):
+    // count and psum are integer sums; sum2 and sum4 in position order
+    auto pooled = [&](uint32_t i) -> uint32_t {
+        const uint32_t h = E.ghit[i];
+        if (h == 0xFFFFFFFFu) return 0u;
+        uint32_t pc = 0;
+        for (int s = 0; s < S; ++s) pc += E.ghits[(uint64_t)h * S + s];
+        return pc;
+    };
+    uint32_t cpart = 0, ppart = 0;
+    for (uint32_t i = lane; i < n; i += 64) {
+        const uint32_t pc = pooled(i);
+        cpart += pc;
+        ppart += pc * (uint32_t)(uint16_t)i;
+    }
+    const uint32_t count = emu_wave_sum(cpart), psum = emu_wave_sum(ppart);
     const double x_bar = (double)psum / (double)count;
     double sum2 = 0.0, sum4 = 0.0;
-    pos = 0;
-    for (uint32_t i = 0; i < E.n; ++i, ++pos)
-        if (E.ghit[i] != 0xFFFFFFFFu) {
-            uint32_t pc = 0;
-            for (int s = 0; s < S; ++s) pc += E.ghits[(uint64_t)E.ghit[i] * S + s];
-            const double d = (double)pos - x_bar;
-            const double d2 = d * d;
-            sum2 = sum2 + (double)pc * d2;
-            sum4 = sum4 + (double)pc * (d2 * d2);
+    for (uint32_t b = 0; b < n; b += 64) {
+        const uint32_t i = b + lane;
+        double a2 = 0.0, a4 = 0.0;
+        if (i < n) {
+            const uint32_t pc = pooled(i);
+            if (pc != 0u || E.ghit[i] != 0xFFFFFFFFu) {  // a stored hit (exptSums may be 0)
+                const double d = (double)(uint16_t)i - x_bar;
+                const double d2 = d * d;
+                a2 = (double)pc * d2;
+                a4 = (double)pc * (d2 * d2);
+            }
         }
+        L.t0[lane] = a2;
+        L.t1[lane] = a4;
+        emu_sync();
+        const int m = n - b < 64 ? (int)(n - b) : 64;
+        // positions without a stored hit add nothing in the reference; a
+        // +0.0 here leaves the (non-negative) sums as they are
+        sum2 = emu_add_terms(sum2, L.t0, m);
+        sum4 = emu_add_terms(sum4, L.t1, m);
+        emu_sync();
+    }
     const double kurt = ((double)count - 1) * sum4 / (sum2 * sum2);
     double corr = __builtin_nan("");
-    if (P.want_corr && E.n > 3) {
-        const uint32_t m = E.n;
+    if (P.want_corr && n > 3) {
         double s1 = 0.0, s2 = 0.0;
-        for (uint32_t i = 0; i < m; ++i) s1 = s1 + E.gf[i];
-        for (uint32_t i = 0; i < m; ++i) s2 = s2 + E.gr[i];
-        const double m1 = s1 / (double)m, m2 = s2 / (double)m;
+        for (uint32_t b = 0; b < n; b += 64) {
+            const uint32_t i = b + lane;
+            L.t0[lane] = i < n ? E.gf[i] : 0.0;
+            L.t1[lane] = i < n ? E.gr[i] : 0.0;
+            emu_sync();
+            const int m = n - b < 64 ? (int)(n - b) : 64;
+            s1 = emu_add_terms(s1, L.t0, m);
+            s2 = emu_add_terms(s2, L.t1, m);
+            emu_sync();
+        }
+        const double m1 = s1 / (double)n, m2 = s2 / (double)n;
         double q1 = 0.0, q2 = 0.0, q3 = 0.0;
-        for (uint32_t i = 0; i < m; ++i) { const double d = E.gf[i] - m1; q1 = q1 + d * d; }
-        for (uint32_t i = 0; i < m; ++i) { const double d = E.gr[i] - m2; q2 = q2 + d * d; }
-        const double sd1 = sqrt(q1 / ((double)m - 1)), sd2 = sqrt(q2 / ((double)m - 1));
-        for (uint32_t i = 0; i < m; ++i) q3 = q3 + (E.gf[i] - m1) * (E.gr[i] - m2);
-        corr = q3 / (((double)m - 1) * sd1 * sd2);
+        for (uint32_t b = 0; b < n; b += 64) {
+            const uint32_t i = b + lane;
+            double d1 = 0.0, d2 = 0.0;
+            if (i < n) {
+                d1 = E.gf[i] - m1;
+                d2 = E.gr[i] - m2;
+            }
+            L.t0[lane] = d1 * d1;
+            L.t1[lane] = d2 * d2;
+            L.t2[lane] = d1 * d2;
+            emu_sync();
+            const int m = n - b < 64 ? (int)(n - b) : 64;
+            q1 = emu_add_terms(q1, L.t0, m);
+            q2 = emu_add_terms(q2, L.t1, m);
+            q3 = emu_add_terms(q3, L.t2, m);
+            emu_sync();
+        }
+        const double sd1 = sqrt(q1 / ((double)n - 1)), sd2 = sqrt(q2 / ((double)n - 1));
+        corr = q3 / (((double)n - 1) * sd1 * sd2);
     }
     bool acc = (double)nonctl >= P.hit_thr;
-    if (acc) acc = P.kurt_thr == 0 || (E.n > 1 && kurt <= P.kurt_thr);
+    if (acc) acc = P.kurt_thr == 0 || (n > 1 && kurt <= P.kurt_thr);
     if (acc) acc = P.corr_thr <= -1 || corr >= P.corr_thr;
     if (keep && P.out_scores) {
-        const unsigned long long off = atomicAdd(P.nscores, 2ull * E.n);
-        if (off + 2ull * E.n <= P.scores_cap) {
-            for (uint32_t i = 0; i < E.n; ++i) {
+        unsigned long long off = 0;
+        if (lane == 0) off = atomicAdd(P.nscores, 2ull * n);
+        off = (unsigned long long)__shfl((long long)off, 0);
+        if (off + 2ull * n <= P.scores_cap) {
+            for (uint32_t i = lane; i < n; i += 64) {
                 P.out_scores[off + i] = E.gf[i];
-                P.out_scores[off + E.n + i] = E.gr[i];
+                P.out_scores[off + n + i] = E.gr[i];
             }
-            P.out_score_off[slot] = off;
-        } else {
+            if (lane == 0) P.out_score_off[slot] = off;
+        } else if (lane == 0) {
             P.out_score_off[slot] = ~0ull;
             atomicOr(P.err, 8u);
         }
     }
-    if (keep && P.out_group) P.out_group[slot] = E.group;
-    if (keep) {
+    if (keep && lane == 0) {
+        if (P.out_group) P.out_group[slot] = E.group;
         up_region &o = P.out[slot];
         o.unit = E.cur_unit;
         o.left = E.left;
-        o.right = E.left + E.n - 1;
+        o.right = E.left + n - 1;
         o.peak = E.peak_pos;
         o.sum = total;
         o.nonctl_sum = nonctl;
@@ -216,18 +293,20 @@ __device__ static void emu_region(const EmuParams &P, EmuState &E) {
 
 // Region::addPos (data.cpp:92-102); hits (cell index or none) are copied
 __device__ static void emu_addpos(const EmuParams &P, EmuState &E, int cell, double f, double r) {
+    const int lane = threadIdx.x;
     if (E.n >= P.reg_cap) {
-        atomicOr(P.err, 1u);
+        if (lane == 0) atomicOr(P.err, 1u);
         return;
     }
-    E.gf[E.n] = f;
-    E.gr[E.n] = r;
+    if (lane == 0) {
+        E.gf[E.n] = f;
+        E.gr[E.n] = r;
+        E.ghit[E.n] = cell >= 0 ? E.nhits : 0xFFFFFFFFu;
+    }
     if (cell >= 0) {
         const uint32_t h = E.nhits++;
-        for (int s = 0; s < P.S; ++s) E.ghits[(uint64_t)h * P.S + s] = E.rhits[(uint64_t)cell * P.S + s];
-        E.ghit[E.n] = h;
-    } else {
-        E.ghit[E.n] = 0xFFFFFFFFu;
+        // lane s % 64 wrote the cell's count of sample s (emu_add)
+        for (int s = lane; s < P.S; s += 64) E.ghits[(uint64_t)h * P.S + s] = E.rhits[(uint64_t)cell * P.S + s];
     }
     E.n++;
     const double score = f + r;
@@ -238,8 +317,9 @@ __device__ static void emu_addpos(const EmuParams &P, EmuState &E, int cell, dou
 }
 
 // processPosition (peakcall.cpp:55-86) of the front cell
-__device__ static void emu_process(const EmuParams &P, EmuState &E, uint32_t pos, int cell) {
-    if (!(pos > E.last_pos)) atomicOr(P.err, 4u);
+__device__ static void emu_process(const EmuParams &P, EmuState &E, EmuLds &L, uint32_t pos, int cell) {
+    const int lane = threadIdx.x;
+    if (!(pos > E.last_pos) && lane == 0) atomicOr(P.err, 4u);
     const double f = E.rf[cell], r = E.rr[cell];
     const int hc = E.rhas[cell] ? cell : -1;
     const double score = f + r;
@@ -249,16 +329,16 @@ __device__ static void emu_process(const EmuParams &P, EmuState &E, uint32_t pos
     if (pos == E.last_pos + 1) {
         if (E.left != 0) {
             if (score >= P.region_thr) emu_addpos(P, E, hc, f, r);
-            else emu_region(P, E);
+            else emu_region(P, E, L);
         } else if (score >= P.region_thr) {
             E.left = pos;
             emu_addpos(P, E, hc, f, r);
         }
     } else {
-        if (E.left != 0) emu_region(P, E);
+        if (E.left != 0) emu_region(P, E, L);
         if (score >= P.region_thr) emu_addpos(P, E, hc, f, r);
     }
-    if (P.prof_score && score != 0.0) {  // profileOut_->write(PosScore(...)), peakcall.cpp:80-83
+    if (P.prof_score && score != 0.0 && lane == 0) {  // profileOut_->write(PosScore(...)), peakcall.cpp:80-83
         const unsigned long long k = atomicAdd(P.nprof, 1ull);
         if (k < P.prof_cap) {
             P.prof_unit[k] = E.cur_unit;
@@ -278,19 +358,23 @@ __device__ static void emu_process(const EmuParams &P, EmuState &E, uint32_t pos
     }
 }
 
-// ProfileBuffer::add (peakcall.cpp:161-222) without the contig switch
-__device__ static void emu_add(const EmuParams &P, EmuState &E, const uint32_t *counts,
-                               uint32_t pos, bool forward) {
+// ProfileBuffer::add (peakcall.cpp:161-222) without the contig switch; the
+// add's counts are in L.counts (with_counts) -- none for a flush
+__device__ static void emu_add(const EmuParams &P, EmuState &E, EmuLds &L, bool with_counts, uint32_t pos,
+                               bool forward) {
+    const int lane = threadIdx.x;
     uint16_t n_static = (uint16_t)E.W;
     if (pos <= E.buffer_pos + 2u * (uint32_t)P.bw) n_static = (uint16_t)(pos - E.buffer_pos);
     if (E.buffer_pos != 0) {
         for (uint16_t i = 0; i < n_static && !E.resynced; ++i) {
             if (E.buffer_pos + i > (uint32_t)P.bw) {
                 const int cell = (int)E.head;
-                emu_process(P, E, E.buffer_pos + i - P.bw, cell);
-                E.rf[cell] = 0.0;
-                E.rr[cell] = 0.0;
-                E.rhas[cell] = 0;
+                emu_process(P, E, L, E.buffer_pos + i - P.bw, cell);
+                if (lane == 0) {
+                    E.rf[cell] = 0.0;
+                    E.rr[cell] = 0.0;
+                    E.rhas[cell] = 0;
+                }
                 E.head = (E.head + 1) % E.W;
             }
         }
@@ -300,38 +384,42 @@ __device__ static void emu_add(const EmuParams &P, EmuState &E, const uint32_t *
     }
     if (E.resynced) return;
     double cs = 0.0;
-    if (counts) {
+    if (with_counts) {  // countSum in the reference's sample order (uniform: LDS broadcasts)
         if (P.ncoef == 0) {
             for (int s = 0; s < P.S; ++s)
-                if (!P.is_control[s]) cs = cs + (double)counts[s];
+                if (!P.is_control[s]) cs = cs + (double)L.counts[s];
         } else {
             int k = 0;
             for (int s = 0; s < P.S && k < P.ncoef; ++s)
-                if (!P.is_control[s]) { cs = cs + (double)counts[s] * P.coef[k]; ++k; }
+                if (!P.is_control[s]) { cs = cs + (double)L.counts[s] * P.coef[k]; ++k; }
             for (int s = 0; s < P.S; ++s)
-                if (!P.is_control[s]) cs = cs + (double)counts[s];
+                if (!P.is_control[s]) cs = cs + (double)L.counts[s];
         }
     }
+    emu_sync();  // the retired cells' clears before the window's update
     if (cs != 0.0) {
-        for (uint32_t j = 0; j < E.W; ++j) {
+        // each cell gains its kernel term once per add: split over the lanes
+        for (uint32_t j = lane; j < E.W; j += 64) {
             const uint32_t c = (E.head + j) % E.W;
             if (forward) E.rf[c] = E.rf[c] + P.kern[j] * cs;
             else E.rr[c] = E.rr[c] + P.kern[j] * cs;
         }
         const uint32_t c = (E.head + P.bw) % E.W;
-        if (E.rhas[c]) {
-            for (int s = 0; s < P.S; ++s) E.rhits[(uint64_t)c * P.S + s] += counts[s];
-        } else {
-            for (int s = 0; s < P.S; ++s) E.rhits[(uint64_t)c * P.S + s] = counts[s];
-            E.rhas[c] = 1;
+        const bool had = E.rhas[c] != 0;
+        for (int s = lane; s < P.S; s += 64) {
+            if (had) E.rhits[(uint64_t)c * P.S + s] += L.counts[s];
+            else E.rhits[(uint64_t)c * P.S + s] = L.counts[s];
         }
+        emu_sync();  // every lane has read rhas[c]
+        if (lane == 0) E.rhas[c] = 1;
+        emu_sync();  // the window as the next retirements read it
     }
     E.buffer_pos = pos;
 }
 
 __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
     extern __shared__ double emu_lds[];  // the window when P.ring_lds: rf[W], rr[W], rhas[W]
-    __shared__ int stop_flag;
+    __shared__ EmuLds L;
     const int lane = threadIdx.x;
     const int buffer = blockIdx.x;  // scratch slot
     const int S = P.S;
@@ -353,12 +441,18 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
     E.gr = P.reg_r + (uint64_t)buffer * P.reg_cap;
     E.ghit = P.reg_hit + (uint64_t)buffer * P.reg_cap;
     E.ghits = P.reg_hits + (uint64_t)buffer * P.reg_cap * S;
+    E.group = 0;
+    E.clean = true;
+    E.may_stop = true;
+    E.stop_pos = 0;
 
     for (uint32_t g = blockIdx.x; g < P.ngroups; g += gridDim.x) {
     bool in_chain = false;
-    if (P.q11 && lane == 0) {
-        P.gstop[2 * g] = 0xFFFFFFFFu;
-        P.gstop[2 * g + 1] = 0xFFFFFFFFu;
+    if (P.q11) {
+        if (lane == 0) {
+            P.gstop[2 * g] = 0xFFFFFFFFu;
+            P.gstop[2 * g + 1] = 0xFFFFFFFFu;
+        }
         E.group = g;
         E.clean = true;
     }
@@ -370,34 +464,29 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
         if (!in_chain) {
             if (!q11_first && !P.unit_head[u]) continue;
             // chain start: fresh buffer state (the previous unit ended clean)
-            if (lane == 0) {
-                for (uint32_t j = 0; j < E.W; ++j) { rf[j] = 0.0; rr[j] = 0.0; rhas[j] = 0; }
-                E.head = 0;
-                E.buffer_pos = 0;
-                E.last_pos = 0;
-                E.left = 0;
-                E.n = 0;
-                E.nhits = 0;
-                E.peak_pos = 0;
-                E.peak_score = 0.0;
-            }
+            for (uint32_t j = lane; j < E.W; j += 64) { rf[j] = 0.0; rr[j] = 0.0; rhas[j] = 0; }
+            emu_sync();
+            E.head = 0;
+            E.buffer_pos = 0;
+            E.last_pos = 0;
+            E.left = 0;
+            E.n = 0;
+            E.nhits = 0;
+            E.peak_pos = 0;
+            E.peak_score = 0.0;
             in_chain = true;
         }
-        uint32_t nadd = 0;  // add() calls of this unit so far (lane 0)
-        if (lane == 0) {
-            E.cur_unit = u;  // contig switch relabels the open region (peakcall.cpp:164-168)
-            E.aligned = false;
-            E.horizon = ~0ull;
-            E.resynced = false;
-            E.may_stop = !(q11_first && P.gskip[g] > 1);  // not inside the start unit's last run
-        }
+        uint32_t nadd = 0;  // add() calls of this unit so far
+        E.cur_unit = u;  // contig switch relabels the open region (peakcall.cpp:164-168)
+        E.aligned = false;
+        E.horizon = ~0ull;
+        E.resynced = false;
+        E.may_stop = !(q11_first && P.gskip[g] > 1);  // not inside the start unit's last run
         const UnitDesc U = P.units[u];
         const int nstr = U.nstrands;
         const uint64_t from = q11_first ? P.gskip[g] : 1;
-        if (lane == 0) stop_flag = 0;
-        __syncthreads();
         // walk the unit's add() positions in order, 64 at a time
-        for (uint64_t base = from; base <= U.len && !stop_flag; base += 64) {
+        for (uint64_t base = from; base <= U.len && !E.resynced; base += 64) {
             const uint64_t p = base + lane;
             uint32_t any0 = 0, any1 = 0;
             if (p <= U.len) {
@@ -408,58 +497,54 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
             }
             const uint64_t m0 = __ballot(any0 != 0), m1 = __ballot(any1 != 0);
             uint64_t m = m0 | m1;
-            if (lane == 0) {
-                while (m && !E.resynced) {
-                    const int b = __builtin_ctzll(m);
-                    m &= m - 1;
-                    const uint32_t pos = (uint32_t)(base + b);
-                    for (int st = 0; st < 2 && !E.resynced; ++st) {
-                        if (!(((st ? m1 : m0) >> b) & 1)) continue;
-                        uint32_t counts[256];
-                        for (int s = 0; s < S; ++s) counts[s] = count_at(U, S, nstr == 2 ? st : 0, s, pos);
-                        E.close_pos = pos;
-                        E.ev = nadd++;
-                        const bool first_aligned = !E.aligned && pos > (uint32_t)P.bw;
-                        emu_add(P, E, counts, pos, nstr == 2 ? st == 0 : P.unit_buffer[u] == 0);
-                        if (first_aligned) {
-                            E.aligned = true;
-                            E.horizon = (uint64_t)pos + P.bw;
-                        }
+            while (m && !E.resynced) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1;
+                const uint32_t pos = (uint32_t)(base + b);
+                for (int st = 0; st < 2 && !E.resynced; ++st) {
+                    if (!(((st ? m1 : m0) >> b) & 1)) continue;
+                    for (int s = lane; s < S; s += 64) L.counts[s] = count_at(U, S, nstr == 2 ? st : 0, s, pos);
+                    emu_sync();
+                    E.close_pos = pos;
+                    E.ev = nadd++;
+                    const bool first_aligned = !E.aligned && pos > (uint32_t)P.bw;
+                    emu_add(P, E, L, true, pos, nstr == 2 ? st == 0 : P.unit_buffer[u] == 0);
+                    if (first_aligned) {
+                        E.aligned = true;
+                        E.horizon = (uint64_t)pos + P.bw;
                     }
-                }
-                if (E.resynced) stop_flag = 1;
-            }
-            __syncthreads();
-        }
-        if (lane == 0) {
-            if (E.resynced) {
-                P.resync[u] = E.last_pos + 1;
-            } else {
-                // explicit flushContig() at the end of the unit's pass
-                E.close_pos = 0;
-                E.ev = kFlushEvent;
-                emu_add(P, E, nullptr, E.buffer_pos + E.W, true);
-                E.buffer_pos = 0;
-                E.last_pos = 0;
-                P.resync[u] = 0xFFFFFFFFu;
-                bool win = true;
-                for (uint32_t j = 0; j < E.W && win; ++j)
-                    win = rf[j] == 0.0 && rr[j] == 0.0 && !rhas[j];
-                E.clean = win;
-                // a q11 chain carries its open region on: only a leap ends it
-                stop_flag = !P.q11 && win && E.n == 0 ? 1 : 0;
-            }
-            if (E.resynced) {
-                stop_flag = 1;
-                if (P.q11) {
-                    P.gstop[2 * g] = u;
-                    P.gstop[2 * g + 1] = E.stop_pos;
+                    emu_sync();  // L.counts is rewritten by the next add
                 }
             }
         }
-        __syncthreads();
-        if (stop_flag) in_chain = false;
-        __syncthreads();
+        bool stop = false;
+        if (E.resynced) {
+            if (lane == 0) P.resync[u] = E.last_pos + 1;
+        } else {
+            // explicit flushContig() at the end of the unit's pass
+            E.close_pos = 0;
+            E.ev = kFlushEvent;
+            emu_add(P, E, L, false, E.buffer_pos + E.W, true);
+            E.buffer_pos = 0;
+            E.last_pos = 0;
+            if (lane == 0) P.resync[u] = 0xFFFFFFFFu;
+            emu_sync();
+            bool dirty = false;
+            for (uint32_t j = lane; j < E.W; j += 64) dirty |= rf[j] != 0.0 || rr[j] != 0.0 || rhas[j] != 0;
+            const bool win = __ballot(dirty) == 0;
+            E.clean = win;
+            // a q11 chain carries its open region on: only a leap ends it
+            stop = !P.q11 && win && E.n == 0;
+        }
+        if (E.resynced) {
+            stop = true;
+            if (P.q11 && lane == 0) {
+                P.gstop[2 * g] = u;
+                P.gstop[2 * g + 1] = E.stop_pos;
+            }
+        }
+        if (stop) in_chain = false;
+        emu_sync();
     }
     }  // groups
 }
