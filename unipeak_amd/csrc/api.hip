@@ -111,6 +111,7 @@ struct Unit {
     uint32_t *d_ovf_off = nullptr; // [ntracks + 1]
     uint32_t *d_ovf_tidx = nullptr;  // [ntracks][nblk] escape tile per block (kNoTile: none)
     uint8_t *d_ovf_tiles = nullptr;  // [ntiles][kOvfBlk]
+    uint8_t *d_pct = nullptr;        // pooled count track (POOL 1; UnitDesc::pct)
     bool ovf_dirty = false;
     bool cs_dirty = false;     // a track changed: rebuild its chunk-sum plane (csum_kernel)
     bool pool_dirty = true;    // rebuild the unit's pooled plane (pool_kernel)
@@ -488,6 +489,7 @@ static void free_units(up_ctx *c) {
         if (u.d_ovf_off) (void)hipFree(u.d_ovf_off);
         if (u.d_ovf_tidx) (void)hipFree(u.d_ovf_tidx);
         if (u.d_ovf_tiles) (void)hipFree(u.d_ovf_tiles);
+        if (u.d_pct) (void)hipFree(u.d_pct);
     }
     c->units.clear();
     c->units_dirty = true;
@@ -1107,11 +1109,30 @@ static int sync_units(up_ctx *c) {
         }
         d[i] = UnitDesc{(uint64_t)(uintptr_t)u.dptr, u.stride, u.len, u.strip0, u.nstrips, u.nstrands,
                         (uint64_t)(uintptr_t)u.d_ovf, (uint64_t)(uintptr_t)u.d_ovf_off,
-                        (uint64_t)(uintptr_t)u.d_ovf_tidx, (uint64_t)(uintptr_t)u.d_ovf_tiles};
+                        (uint64_t)(uintptr_t)u.d_ovf_tidx, (uint64_t)(uintptr_t)u.d_ovf_tiles, 0};
     }
     c->nstrips = strip;
     c->ovf_max_all = 0;
     for (const Unit &u : c->units) c->ovf_max_all = std::max(c->ovf_max_all, u.ovf_max);
+    // pooled count tracks while several samples pool in uint32 (POOL 1):
+    // K1b, K3 and K4 read one byte track instead of every pooled sample's
+    // (UNIPEAK_PCT=0: off, the per-sample path)
+    static const bool pct_on = [] {
+        const char *e = getenv("UNIPEAK_PCT");
+        return !(e && *e == '0');
+    }();
+    const bool want_pct = pct_on && kTB == 2 && pool_mode(c) == 1;
+    for (size_t i = 0; i < c->units.size(); ++i) {
+        Unit &u = c->units[i];
+        if (want_pct && !u.d_pct) {
+            HIPCHK(hipMalloc(&u.d_pct, (size_t)u.nstrands * kPerByte * u.stride));
+            u.pool_dirty = true;
+        } else if (!want_pct && u.d_pct) {
+            (void)hipFree(u.d_pct);
+            u.d_pct = nullptr;
+        }
+        d[i].pct = (uint64_t)(uintptr_t)u.d_pct;
+    }
     {
         // escape bitmap: bit (strip) of row (strand * S + sample) is set when
         // a block of the strip, or the block either side (the screen's halos,
@@ -1162,6 +1183,10 @@ static int sync_units(up_ctx *c) {
             hipLaunchKernelGGL(pool_kernel, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 65536)), dim3(256), 0,
                                c->stream, c->d_units.p, (uint32_t)i, (int)c->p.n_samples, (int)c->nc.size(),
                                c->d_nc.p, c->d_wscreen.p);
+            if (u.d_pct)
+                hipLaunchKernelGGL(pct_kernel, dim3((unsigned)std::min<uint64_t>((n * u.nstrands + 255) / 256, 65536)),
+                                   dim3(256), 0, c->stream, c->d_units.p, (uint32_t)i, (int)c->p.n_samples,
+                                   (int)c->nc.size(), c->d_nc.p);
             u.pool_dirty = false;
             planes = true;
         }

@@ -94,6 +94,10 @@ struct UnitDesc {
     uint64_t ovf_tidx;  // uint32[ntracks][nblk]: escape tile of block b (kNoTile: none)
     uint64_t ovf_tiles; // uint8[ntiles][kOvfBlk]: min(count, 255) of every escaped position
                         // of the tile's block (255: the entries hold it)
+    uint64_t pct;       // pooled count track (several pooled samples, POOL 1) or 0:
+                        // uint8[nstrands][kPerByte * stride], byte n = field n of the 2-bit
+                        // tracks, min(sum of the pooled samples' counts, 255) -- 255: sum
+                        // the samples (pct_kernel, rebuilt with the pooled plane)
 };
 constexpr uint32_t kNoTile = 0xFFFFFFFFu;
 

@@ -205,6 +205,28 @@ __device__ __forceinline__ uint32_t count_at(const UnitDesc &U, int S, int stran
     return b == kEsc ? ovf_lookup(U, (uint32_t)(strand * S + sample), (uint32_t)p) : b;
 }
 
+// pooled counts of N words from the unit's pooled count track (POOL 1): one
+// coalesced byte load per word; a saturated byte (255) is summed from the
+// samples' tracks in the reference's sample order (exact in uint32)
+template <int N>
+__device__ __forceinline__ void pct_words(uint32_t (&c)[N], const UnitDesc &U, int S, int strand, int64_t x0,
+                                          int lane, int nnc, const int32_t *nc) {
+    gu8 *t = (gu8 *)U.pct + (uint64_t)strand * ((uint64_t)kPerByte * U.stride) + (kPadPos + x0 - 1 + lane);
+#pragma unroll
+    for (int w = 0; w < N; ++w) c[w] = t[64 * w];
+    uint32_t m = 0;
+#pragma unroll
+    for (int w = 0; w < N; ++w) m |= (c[w] == 255u ? 1u : 0u) << w;
+    while (m) {
+        const int w = __builtin_ctz(m);
+        m &= m - 1;
+        uint32_t v = 0;
+        for (int k = 0; k < nnc; ++k) v += count_at(U, S, strand, nc[k], x0 + 64 * w + lane);
+#pragma unroll
+        for (int q = 0; q < N; ++q) c[q] = q == w ? v : c[q];
+    }
+}
+
 // ---- pooled count (ProfileBuffer::add countSum, peakcall.cpp:186-200) ----
 // POOL 0: one non-control sample, no coefficients; 1: several, unscaled;
 // 2: scaled by coefficients plus the unscaled second loop (quirk Q5).
@@ -227,6 +249,10 @@ __device__ __forceinline__ void load_words(WinT<POOL> (&cs)[N], const UnitDesc &
     };
     if constexpr (POOL == 0) {
         fetch(0);
+#pragma unroll
+        for (int w = 0; w < N; ++w) cs[w] = c[w];
+    } else if (POOL == 1 && U.pct) {
+        pct_words<N>(c, U, S, strand, x0, lane, nnc, nc);
 #pragma unroll
         for (int w = 0; w < N; ++w) cs[w] = c[w];
     } else {
@@ -340,6 +366,11 @@ __device__ __forceinline__ void load_words_staged(WinT<POOL> (&cs)[N], const Uni
         for (int w = 0; w < N; ++w) c[w] = ((uint32_t)stage[kWordBytes * w + fbyte(lane)] >> sh) & kTMask;
         // most windows hold no escape: one ballot instead of N per-word tests
         if (__ballot(eb != 0u)) resolve_escapes<N>(c, U, (uint32_t)(strand * S + nc[0]), x0, lane);
+#pragma unroll
+        for (int w = 0; w < N; ++w) cs[w] = c[w];
+    } else if (POOL == 1 && U.pct) {
+        uint32_t c[N];
+        pct_words<N>(c, U, S, strand, x0, lane, nnc, nc);
 #pragma unroll
         for (int w = 0; w < N; ++w) cs[w] = c[w];
     } else {
@@ -2065,6 +2096,45 @@ __global__ void __launch_bounds__(256) pool_kernel(const UnitDesc *units, uint32
             for (int k = 0; k < nnc && s < 255u; ++k)
                 s += w[k] * (uint32_t)planes[((uint64_t)st * S + nc[k]) * nd + j];  // w <= 4096: no wrap
         pooled[j] = (uint8_t)(s < 255u ? s : 255u);
+    }
+}
+
+// the pooled count track of one unit (UnitDesc::pct): one thread per track
+// dword (16 positions) and strand, the pooled samples' fields summed (escapes
+// at their counts), saturated at 255
+__global__ void __launch_bounds__(256) pct_kernel(const UnitDesc *units, uint32_t unit, int S, int nnc,
+                                                  const int32_t *nc) {
+    const UnitDesc U = units[unit];
+    const uint64_t nd = U.stride / 4;  // dwords per track
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nd * (uint64_t)U.nstrands;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const int st = (int)(i / nd);
+        const uint64_t j = i - (uint64_t)st * nd;
+        uint32_t sum[16];
+#pragma unroll
+        for (int f = 0; f < 16; ++f) sum[f] = 0;
+        for (int k = 0; k < nnc; ++k) {
+            const uint32_t d = ((const uint32_t *)((const uint8_t *)U.base + ((uint64_t)st * S + nc[k]) * U.stride))[j];
+            if (!d) continue;
+#pragma unroll
+            for (int f = 0; f < 16; ++f) {
+                uint32_t v = (d >> (2 * f)) & 3u;
+                if (v == kEsc) {
+                    const int64_t p = (int64_t)(16 * j) + f - kPadPos + 1;
+                    v = ovf_lookup(U, (uint32_t)(st * S + nc[k]), (uint32_t)p);
+                }
+                sum[f] += v;
+            }
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            o[q] = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) o[q] |= (sum[4 * q + b] < 255u ? sum[4 * q + b] : 255u) << (8 * b);
+        }
+        uint4 *dst = (uint4 *)((uint8_t *)U.pct + (uint64_t)st * (4 * U.stride) + 16 * j);
+        *dst = make_uint4(o[0], o[1], o[2], o[3]);
     }
 }
 
