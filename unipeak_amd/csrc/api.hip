@@ -398,6 +398,7 @@ int up_track_bits(void) { return kTB; }
 // directional track when the window reaches the neighbouring lanes only
 static bool plane_scan(const up_ctx *c);
 static int pool_mode(const up_ctx *c);
+static bool pct_mode(const up_ctx *c);
 
 int up_scan_density(up_ctx *c, uint32_t *b) {
     if (!c || !b) return UP_E_ARG;
@@ -690,8 +691,16 @@ static bool q_mode(const up_ctx *c) {
     // samples + 1 control: K1b 2.07 -> 1.64 ms but K3 0.82 -> 1.08-1.23 ms,
     // 541 -> 515-525 Gbp/s) -- unless K3 runs its own KDE anyway (-D with
     // the strand correlation), where the keys are K1b's gain only
+    // (round 5, with the pooled count track, UNIPEAK_Q_POOLED=1: K3 scores
+    // the pooled peak from one byte per window position, but configs[3]
+    // still lost -- K1b 1.16 -> 1.13 ms, K3 0.54 -> 1.03 ms, 1,828 -> 1,458
+    // Gbp/s same box, profiles/r05/pct/ -- so the keys stay off)
     const bool k3_kde = c->p.nondir && (c->p.want_corr || c->p.corr_thr > -1);
-    if (c->nc.size() > 1 && !k3_kde) return false;
+    static const bool q_pooled = [] {
+        const char *e = getenv("UNIPEAK_Q_POOLED");
+        return e && *e == '1';
+    }();
+    if (c->nc.size() > 1 && !k3_kde && !(q_pooled && pct_mode(c))) return false;
     const int bw = c->p.bw;
     const double cmax = (double)std::max<uint32_t>(kEsc - 1, c->ovf_max_all) * (double)c->nc.size() *
                         (c->p.nondir ? 2.0 : 1.0);
@@ -1116,12 +1125,7 @@ static int sync_units(up_ctx *c) {
     for (const Unit &u : c->units) c->ovf_max_all = std::max(c->ovf_max_all, u.ovf_max);
     // pooled count tracks while several samples pool in uint32 (POOL 1):
     // K1b, K3 and K4 read one byte track instead of every pooled sample's
-    // (UNIPEAK_PCT=0: off, the per-sample path)
-    static const bool pct_on = [] {
-        const char *e = getenv("UNIPEAK_PCT");
-        return !(e && *e == '0');
-    }();
-    const bool want_pct = pct_on && kTB == 2 && pool_mode(c) == 1;
+    const bool want_pct = pct_mode(c);
     for (size_t i = 0; i < c->units.size(); ++i) {
         Unit &u = c->units[i];
         if (want_pct && !u.d_pct) {
@@ -1208,6 +1212,16 @@ static int pool_mode(const up_ctx *c) {
     if (c->nc.size() == 1) return 0;
     const double cmax = (double)std::max<uint32_t>(kEsc - 1, c->ovf_max_all) * (double)c->nc.size();
     return cmax < 4294967296.0 ? 1 : 2;
+}
+
+// pooled count tracks (UnitDesc::pct) for this pooling; UNIPEAK_PCT=0: off
+// (every pooled sample's track, as before round 5)
+static bool pct_mode(const up_ctx *c) {
+    static const bool on = [] {
+        const char *e = getenv("UNIPEAK_PCT");
+        return !(e && *e == '0');
+    }();
+    return on && kTB == 2 && pool_mode(c) == 1;
 }
 
 static bool plane_scan(const up_ctx *c) {

@@ -2322,11 +2322,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
         // the peak's FP64 score: the pooled counts of its window (2NH words
         // from kpos - bw, lane = offset t), fetched now and summed after the
         // region's counts
-        // (several pooled samples use Q keys only with -D -y, where K3 runs
-        // its own KDE: the peak code exists for one pooled sample only)
-        constexpr int kPK = POOL == 0 ? 2 * NH : 1;
+        // (several pooled samples without coefficients: their pooled count
+        // words, one byte each from the pooled count track)
+        constexpr int kPK = POOL != 2 ? 2 * NH : 1;
         WinT<POOL> pkf[kPK], pkr[NONDIR ? kPK : 1];
-        if (POOL == 0 && kn && P.qmode) {
+        if (POOL != 2 && kn && P.qmode) {
             if (kPrefetch && pk_pre && pk_pos == kpos) {  // fetched during the previous region
                 const uint32_t sh = fshift(kPadPos + (int64_t)kpos - bw - 1 + lane);
                 uint32_t c[kPrefetch ? 2 * NH : 1];
@@ -2499,7 +2499,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 sum_acc += pc * (uint32_t)(uint16_t)(x - left);
             }
         }
-        if (POOL == 0 && kn && P.qmode) {
+        if (POOL != 2 && kn && P.qmode) {
             // score(kpos) as the reference sums it (peakcall.cpp:203-209):
             // the hit at kpos - bw + t adds kernel[2bw - t] * countSum, in
             // ascending t; each lane forms its products, the hits' products
