@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Time the exact whole-buffer replay against the parallel
 scan on one contig of the synthetic genome: `-r 25` (parallel scan), `-r 0`
-(quirk Q11 live: replay), `-b 150` (parallel, NH = 3) and `-b 300` (replay,
-wider than the register halo).  Blocking up_run, both directional buffers of
+(quirk Q11 live: K1q), `-b 150` / `-b 300` / `-b 511` (parallel, NH = 3 / 5 /
+8) and `-b 600` / `-b 2000` (the whole-buffer replay: wider than the
+register halo).  Blocking up_run, both directional buffers of
 the contig, one line of JSON per configuration.
 
 usage: python tools/replay_probe.py [CONTIG (default chr21)]"""
@@ -23,13 +24,15 @@ def main():
             if l.strip() and not l.startswith("#")]
     ci = [r[0] for r in rows].index(name)
     L = int(rows[ci][1])
-    for bw, thr in ((50, 25.0), (50, 0.0), (150, 25.0), (300, 25.0), (511, 25.0), (300, 0.0)):
+    for bw, thr in ((50, 25.0), (50, 0.0), (150, 25.0), (300, 25.0), (511, 25.0), (300, 0.0),
+                    (600, 25.0), (2000, 25.0)):
         with capi.Lib(0) as g:
             g.set_params(bw, 1, 0.0029, region_thr=thr)
             for buf in (0, 1):
                 u = g.add_unit(L, buffer_id=buf)
                 g.synth(u, 0, 0, 1000, ci, buf, nondir=False, peaks=True)
-            g.run()  # warm-up (allocations, replay capacities)
+            if bw <= 511:
+                g.run()  # warm-up (allocations; the replay grows its capacities itself)
             t0 = time.perf_counter()
             n = g.run()
             dt = time.perf_counter() - t0

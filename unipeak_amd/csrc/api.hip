@@ -326,6 +326,10 @@ struct up_ctx {
     std::vector<uint64_t> h_score_off;   // per host region: offset in d_emu_scores or ~0
     DevBuf<uint8_t> d_ring_has;
     uint32_t emu_reg_cap = 1u << 18;     // K0: positions of one open region
+    uint32_t emu_chain_reg_cap = 1u << 14;  // the same for chains (many slots at once)
+    uint32_t seg_cap = 1u << 20;         // segmented replay: run starts
+    DevBuf<unsigned long long> d_seg;
+    DevBuf<uint32_t> d_seg_n, d_gbeg, d_gend;
     uint32_t emu_out_cap = 1u << 16;     // K0: region records
     bool host_regions = false;  // merged list lives on the host
     // threshold <= 0 through K1q (run_q11): the blocking pass in progress,
@@ -523,6 +527,7 @@ void up_close(up_ctx *c) {
     c->d_pf_n.release();
     c->d_gunits.release(); c->d_goff.release(); c->d_gskip.release(); c->d_gstop.release();
     c->d_emu_group.release(); c->d_q11_head.release();
+    c->d_seg.release(); c->d_seg_n.release(); c->d_gbeg.release(); c->d_gend.release();
     c->d_q11_stage.release(); c->d_q11_stage_cnt.release(); c->d_q11_tab.release(); c->d_q11_scr.release();
     c->d_q11_edit.release(); c->d_q11_st.release(); c->d_q11_en.release(); c->d_q11_src.release();
     for (int k = 0; k < kSlots; ++k) {
@@ -1444,6 +1449,7 @@ static int launch_seg_count_head(up_ctx *c, int slot) {
 // end) and the group of each replayed record
 struct Q11Chains {
     std::vector<uint32_t> gunits, goff{0}, gskip;
+    std::vector<uint32_t> gbeg, gend;  // instead of goff: ranges of gunits (segmented replay)
     std::vector<uint32_t> gstop, rgroup;
 };
 
@@ -1499,7 +1505,8 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
             goff.push_back((uint32_t)gunits.size());
         }
     }
-    const uint32_t ngroups = (uint32_t)goff.size() - 1;
+    const bool ranges = q && !q->gbeg.empty();
+    const uint32_t ngroups = ranges ? (uint32_t)q->gbeg.size() : (uint32_t)goff.size() - 1;
     HIPCHK(c->d_gunits.ensure(std::max<size_t>(gunits.size(), 1)));
     HIPCHK(c->d_goff.ensure(goff.size()));
     if (!gunits.empty())
@@ -1507,6 +1514,12 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
     HIPCHK(hipMemcpy(c->d_goff.p, goff.data(), goff.size() * 4, hipMemcpyHostToDevice));
     if (q) {
         if (q->gskip.size() != ngroups) return UP_E_INTERNAL;
+        if (ranges) {
+            HIPCHK(c->d_gbeg.ensure(ngroups));
+            HIPCHK(c->d_gend.ensure(ngroups));
+            HIPCHK(hipMemcpy(c->d_gbeg.p, q->gbeg.data(), ngroups * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->d_gend.p, q->gend.data(), ngroups * 4, hipMemcpyHostToDevice));
+        }
         HIPCHK(c->d_gskip.ensure(std::max(ngroups, 1u)));
         HIPCHK(c->d_gstop.ensure(2 * std::max(ngroups, 1u)));
         if (ngroups) HIPCHK(hipMemcpy(c->d_gskip.p, q->gskip.data(), ngroups * 4, hipMemcpyHostToDevice));
@@ -1519,12 +1532,14 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
     const bool ring_lds = ring_bytes + sizeof(EmuLds) <= 65536 - 64;
     for (int attempt = 0;; ++attempt) {
         if (attempt == 6) return UP_E_NOMEM;
-        const uint32_t reg_cap = c->emu_reg_cap, out_cap = c->emu_out_cap;
+        uint32_t &reg_cap_ref = q ? c->emu_chain_reg_cap : c->emu_reg_cap;
+        const uint32_t reg_cap = reg_cap_ref, out_cap = c->emu_out_cap;
         // workgroups (scratch slots): every group at once, within ~1 GiB of scratch
         const uint64_t slot_bytes = (uint64_t)W * S * 4 + (uint64_t)reg_cap * (8 + 8 + 4 + 4ull * S) +
                                     (ring_lds ? 0 : (uint64_t)W * 17);
         const uint32_t nslots = (uint32_t)std::max<uint64_t>(
-            1, std::min<uint64_t>({(uint64_t)std::max(ngroups, 1u), 256, (1ull << 30) / std::max<uint64_t>(slot_bytes, 1)}));
+            1, std::min<uint64_t>({(uint64_t)std::max(ngroups, 1u), q ? 2048u : 256u,
+                                   (1ull << 30) / std::max<uint64_t>(slot_bytes, 1)}));
         HIPCHK(c->d_ring_hits.ensure((uint64_t)nslots * W * S));
         if (!ring_lds) {
             HIPCHK(c->d_ring_f.ensure((uint64_t)nslots * W));
@@ -1598,6 +1613,10 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
             E.gskip = c->d_gskip.p;
             E.gstop = c->d_gstop.p;
             E.out_group = c->d_emu_group.p;
+            if (ranges) {
+                E.gbeg = c->d_gbeg.p;
+                E.gend = c->d_gend.p;
+            }
         }
         if (c->prof_capture && !q) {
             HIPCHK(c->d_pf_unit.ensure(c->pf_cap));
@@ -1634,7 +1653,7 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
         }
         if (err & 11u) {  // 1: a region longer than reg_cap positions, 2: more than out_cap
                           // regions, 8: the region-score slab is full
-            if (err & 1u) c->emu_reg_cap *= 4;
+            if (err & 1u) reg_cap_ref *= 4;
             if (err & 2u) c->emu_out_cap = std::max<uint32_t>(c->emu_out_cap * 4, nemu + nemu / 4);
             if (err & 8u) {
                 unsigned long long used = 0;
@@ -2227,7 +2246,93 @@ int up_run_wait(up_ctx *c, uint64_t *n_regions) {
     return UP_OK;
 }
 
-// every unit through K0, never resynced (replay_mode configurations)
+// The segmented replay (round 5): configurations outside the parallel scan
+// still replay every position exactly, but as independent chains, one from
+// each run start (leap_adds_kernel: an add with no add in the 2bw + 1
+// positions before it, where the window has drained and a fresh state is
+// the true one), each stopping at the first leap past its start that closes
+// the open region over a clean window (the q11 chains' rule).  A chain that
+// reaches past the next chain's start (an unclean window: quirk Q1 leftovers,
+// a region carried across a unit boundary) covers it, and that chain is
+// dropped.  Records: the kept chains', unit-major, in emission order.
+static int replay_segments(up_ctx *c, std::vector<up_region> &emu, std::vector<uint32_t> &ecnt,
+                           std::vector<uint64_t> &soff, std::vector<uint32_t> &keep) {
+    const uint32_t nu = (uint32_t)c->units.size();
+    const int S = c->p.n_samples;
+    const int bw = c->p.bw;
+    std::vector<unsigned long long> starts;
+    for (int attempt = 0;; ++attempt) {
+        HIPCHK(c->d_seg.ensure(c->seg_cap));
+        HIPCHK(c->d_seg_n.ensure(1));
+        HIPCHK(hipMemsetAsync(c->d_seg_n.p, 0, 4, c->stream));
+        const unsigned blocks = std::max(1u, std::min<uint32_t>((c->nstrips + 3) / 4, 4096));
+        hipLaunchKernelGGL(leap_adds_kernel, dim3(blocks), dim3(256), 0, c->stream, c->d_units.p, nu, c->nstrips,
+                           S, bw, c->d_seg.p, c->d_seg_n.p, c->seg_cap);
+        HIPCHK(hipGetLastError());
+        uint32_t n = 0;
+        HIPCHK(hipMemcpyAsync(&n, c->d_seg_n.p, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (n > c->seg_cap) {
+            if (attempt) return UP_E_INTERNAL;
+            c->seg_cap = n + n / 4 + 1024;
+            continue;
+        }
+        starts.resize(n);
+        if (n) HIPCHK(hipMemcpy(starts.data(), c->d_seg.p, (size_t)n * 8, hipMemcpyDeviceToHost));
+        break;
+    }
+    std::sort(starts.begin(), starts.end());  // (unit, position)
+    std::vector<uint32_t> order[2], at(nu);
+    for (uint32_t u = 0; u < nu; ++u) {
+        at[u] = (uint32_t)order[c->units[u].buffer].size();
+        order[c->units[u].buffer].push_back(u);
+    }
+    Q11Chains q;
+    uint32_t base[2];
+    for (int b = 0; b < 2; ++b) {
+        base[b] = (uint32_t)q.gunits.size();
+        q.gunits.insert(q.gunits.end(), order[b].begin(), order[b].end());
+    }
+    struct G { int b; uint32_t k0; int64_t s; };
+    std::vector<G> gs;
+    gs.reserve(starts.size());
+    for (unsigned long long e : starts) {
+        const uint32_t u = (uint32_t)(e >> 32), a = (uint32_t)e;
+        const int b = c->units[u].buffer;
+        q.gbeg.push_back(base[b] + at[u]);
+        q.gend.push_back(base[b] + (uint32_t)order[b].size());
+        q.gskip.push_back(a);
+        gs.push_back(G{b, at[u], (int64_t)a - bw});
+    }
+    std::vector<uint32_t> resync;
+    up_ctx::Pass &p0 = c->pass[0];
+    if (int r = emulate_units(c, p0.d_head.p, true, emu, ecnt, resync, soff, &q)) return r;
+    std::vector<uint8_t> kept(gs.size(), 0);
+    int64_t last[2] = {-1, -1};
+    for (size_t g = 0; g < gs.size(); ++g) {
+        const G &G_ = gs[g];
+        if (last[G_.b] >= 0) {
+            const size_t l = (size_t)last[G_.b];
+            if (q.gstop[2 * l] == ~0u) continue;  // ran to the buffer's end
+            const uint32_t sk = at[q.gstop[2 * l]];
+            if (sk > G_.k0 || (sk == G_.k0 && (int64_t)q.gstop[2 * l + 1] > G_.s)) continue;  // covered
+        }
+        kept[g] = 1;
+        last[G_.b] = (int64_t)g;
+    }
+    keep.clear();
+    for (uint32_t i = 0; i < emu.size(); ++i)
+        if (kept[q.rgroup[i]]) keep.push_back(i);
+    std::stable_sort(keep.begin(), keep.end(), [&](uint32_t x, uint32_t y) {
+        if (emu[x].unit != emu[y].unit) return emu[x].unit < emu[y].unit;
+        return q.rgroup[x] < q.rgroup[y];
+    });
+    return UP_OK;
+}
+
+// every unit through K0 (replay_mode configurations): the segmented replay,
+// or -- with the -w capture on (its retirements must keep each unit's add
+// order) or UNIPEAK_REPLAY_WHOLE=1 -- one chain per buffer, never resynced
 static int run_replay(up_ctx *c, uint64_t *n_regions) {
     const auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipSetDevice(c->dev));
@@ -2255,12 +2360,22 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
         std::vector<up_region> emu;
         std::vector<uint32_t> ecnt, resync;
         std::vector<uint64_t> soff;
-        if ((r = emulate_units(c, p0.d_head.p, true, emu, ecnt, resync, soff))) return r;
+        std::vector<uint32_t> order;
+        static const bool whole = [] {
+            const char *e = getenv("UNIPEAK_REPLAY_WHOLE");
+            return e && *e == '1';
+        }();
+        if (!c->prof_capture && kTB == 2 && !whole) {
+            if ((r = replay_segments(c, emu, ecnt, soff, order))) return r;
+            c->h_resync.assign(nu, 0);
+        } else {
+            if ((r = emulate_units(c, p0.d_head.p, true, emu, ecnt, resync, soff))) return r;
+            order.resize(emu.size());
+            for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
+            std::stable_sort(order.begin(), order.end(),
+                             [&](uint32_t a, uint32_t b) { return emu[a].unit < emu[b].unit; });
+        }
         const int S = c->p.n_samples;
-        std::vector<uint32_t> order(emu.size());
-        for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
-        std::stable_sort(order.begin(), order.end(),
-                         [&](uint32_t a, uint32_t b) { return emu[a].unit < emu[b].unit; });
         for (uint32_t i : order) {
             c->h_regions.push_back(emu[i]);
             c->h_counts.insert(c->h_counts.end(), ecnt.begin() + (size_t)i * S, ecnt.begin() + (size_t)(i + 1) * S);

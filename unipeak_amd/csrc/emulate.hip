@@ -92,6 +92,9 @@ struct EmuParams {
     const uint32_t *gskip;
     uint32_t *gstop;
     uint32_t *out_group;
+    // chains as ranges of one buffer's unit list (segmented replay): group g
+    // walks gunits[gbeg[g] .. gend[g]) -- null: goff's ranges
+    const uint32_t *gbeg, *gend;
 };
 
 constexpr uint32_t kFlushEvent = 0xFFFFFFFFu;
@@ -338,7 +341,7 @@ __device__ static void emu_process(const EmuParams &P, EmuState &E, EmuLds &L, u
         if (E.left != 0) emu_region(P, E, L);
         if (score >= P.region_thr) emu_addpos(P, E, hc, f, r);
     }
-    if (P.prof_score && score != 0.0 && lane == 0) {  // profileOut_->write(PosScore(...)), peakcall.cpp:80-83
+    if (P.prof_score && score != 0.0 && !stop && lane == 0) {  // profileOut_->write(PosScore(...)), peakcall.cpp:80-83
         const unsigned long long k = atomicAdd(P.nprof, 1ull);
         if (k < P.prof_cap) {
             P.prof_unit[k] = E.cur_unit;
@@ -356,6 +359,7 @@ __device__ static void emu_process(const EmuParams &P, EmuState &E, EmuLds &L, u
         E.resynced = true;
         E.stop_pos = pos;
     }
+    E.may_stop = true;  // (a chain's own first position is a leap from its fresh state)
 }
 
 // ProfileBuffer::add (peakcall.cpp:161-222) without the contig switch; the
@@ -456,10 +460,11 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
         E.group = g;
         E.clean = true;
     }
-    for (uint32_t gk = P.goff[g]; gk < P.goff[g + 1]; ++gk) {
+    const uint32_t gk0 = P.gbeg ? P.gbeg[g] : P.goff[g], gk1 = P.gbeg ? P.gend[g] : P.goff[g + 1];
+    for (uint32_t gk = gk0; gk < gk1; ++gk) {
         const uint32_t u = P.gunits[gk];
         // q11 chains start at their group's first unit and end for good
-        const bool q11_first = P.q11 && gk == P.goff[g];
+        const bool q11_first = P.q11 && gk == gk0;
         if (P.q11 && !in_chain && !q11_first) break;
         if (!in_chain) {
             if (!q11_first && !P.unit_head[u]) continue;
@@ -474,6 +479,7 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
             E.nhits = 0;
             E.peak_pos = 0;
             E.peak_score = 0.0;
+            E.may_stop = false;
             in_chain = true;
         }
         uint32_t nadd = 0;  // add() calls of this unit so far
@@ -481,7 +487,6 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
         E.aligned = false;
         E.horizon = ~0ull;
         E.resynced = false;
-        E.may_stop = !(q11_first && P.gskip[g] > 1);  // not inside the start unit's last run
         const UnitDesc U = P.units[u];
         const int nstr = U.nstrands;
         const uint64_t from = q11_first ? P.gskip[g] : 1;
@@ -547,6 +552,89 @@ __global__ void __launch_bounds__(64) emulate_kernel(EmuParams P) {
         emu_sync();
     }
     }  // groups
+}
+
+// Run starts of every unit for the segmented replay: the adds a with no add
+// in [a - 2bw - 1, a - 1] of the same unit (any track: every sample, both
+// strands).  At such an add the window drains completely, so a replay that
+// starts there from a fresh state is exact from its first retirement on
+// (api.hip run_replay).  One wave per strip: presence words of the strip, the
+// last add before it searched backwards (up to 2bw + 1 positions), previous
+// adds by prefix-max scans; the starts are appended as (unit << 32 | pos).
+__global__ void __launch_bounds__(256) leap_adds_kernel(const UnitDesc *units, uint32_t nunits,
+                                                        uint32_t nstrips, int S, int bw,
+                                                        unsigned long long *out, uint32_t *count,
+                                                        uint32_t cap) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    const int64_t gap = 2 * (int64_t)bw + 1;
+    constexpr int64_t kNone = -((int64_t)1 << 40);
+    for (uint32_t strip = wave; strip < nstrips; strip += nwaves) {
+        const uint32_t u = find_unit(units, nunits, strip);
+        const UnitDesc U = units[u];
+        const int64_t p0 = 1 + (int64_t)(strip - U.strip0) * kStrip;
+        if (p0 > (int64_t)U.len) continue;
+        auto word_bits = [&](int64_t wbase) -> uint64_t {  // adds at wbase .. wbase + 63 (within 1..len)
+            uint64_t m = 0;
+            if (wbase + 63 < 1 || wbase > (int64_t)U.len) return 0;
+            for (int st = 0; st < U.nstrands; ++st)
+                for (int k = 0; k < S; ++k) {
+                    const int64_t n0 = kPadPos + wbase - 1;
+                    gu8 *t = track_u8(U, S, st, k) + fbyte(n0);
+                    const uint32_t sh = fshift(n0);
+                    // 64 fields from 16 bytes (aligned: wbase - 1 is a multiple of 64)
+                    const u32x4 x = *(gu32x4 *)t;
+                    (void)sh;
+                    m |= nz_bits64(x);
+                }
+            if (wbase < 1) m &= ~0ull << (1 - wbase);
+            if (wbase + 63 > (int64_t)U.len) m &= (U.len - wbase + 1) >= 64 ? ~0ull : ((1ull << (U.len - wbase + 1)) - 1);
+            return m;
+        };
+        // the last add before the strip, within gap positions of it
+        int64_t carry = kNone;
+        for (int64_t back = 0; back < gap; back += 64 * 64) {
+            const int64_t wb = p0 - 64 - back - 64 * lane;  // lane's word, going backwards
+            uint64_t m = 0;
+            if (wb + 63 >= p0 - gap && wb + 63 >= 1) m = word_bits(wb);
+            int64_t v = m ? wb + 63 - __builtin_clzll(m) : kNone;
+            if (v < p0 - gap) v = kNone;
+            for (int o = 32; o > 0; o >>= 1) {
+                const int64_t y = __shfl_xor((long long)v, o);
+                v = y > v ? y : v;
+            }
+            if (v != kNone) { carry = v; break; }
+        }
+        for (int r = 0; r < kStripWords / 64; ++r) {
+            const int64_t wbase = p0 + 64 * (64 * r + lane);
+            const uint64_t m = word_bits(wbase);
+            // previous add before this lane's word: carry, or the highest add
+            // of the earlier words of this round (exclusive prefix max)
+            int64_t v = m ? wbase + 63 - __builtin_clzll(m) : kNone;
+            int64_t inc = v;
+            for (int d = 1; d < 64; d <<= 1) {
+                const int64_t y = __shfl_up((long long)inc, d);
+                if (lane >= d && y > inc) inc = y;
+            }
+            int64_t prev = __shfl_up((long long)inc, 1);
+            if (lane == 0) prev = kNone;
+            prev = prev > carry ? prev : carry;
+            uint64_t mm = m;
+            while (mm) {
+                const int b = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                const int64_t a = wbase + b;
+                if (prev == kNone || a - prev > gap) {
+                    const uint32_t k = atomicAdd(count, 1u);
+                    if (k < cap) out[k] = ((unsigned long long)u << 32) | (uint32_t)a;
+                }
+                prev = a;
+            }
+            const int64_t top = __shfl((long long)inc, 63);
+            carry = top > carry ? top : carry;
+        }
+    }
 }
 
 // a unit with an add() past bw cannot end its pass dirty (quirk Q1 leaks
