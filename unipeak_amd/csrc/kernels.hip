@@ -2202,6 +2202,68 @@ __device__ __forceinline__ void region_words(WinT<POOL> (&cs)[2 * NH + 1], uint6
     for (int w = 0; w < 2 * NH + 1; ++w) hm[w] = __ballot(nz(cs[w]));
 }
 
+// sum of one track's counts over positions [left, right]: the chunk-sum plane
+// for whole chunks (a saturated 255 and the two partial chunks at the ends
+// from the track's dword, escapes at their overflow counts)
+__device__ __forceinline__ uint32_t track_range_sum(const UnitDesc &U, int S, int st, int smp, uint32_t left,
+                                                    uint32_t right) {
+    gu32 *tw = (gu32 *)track_u8(U, S, st, smp);
+    gu8 *pl = plane_u8(U, S, st, smp);
+    const uint32_t track = (uint32_t)(st * S + smp);
+    const int64_t n0 = kPadPos + (int64_t)left - 1, n1 = kPadPos + (int64_t)right - 1;
+    const int64_t j0 = n0 >> 4, j1 = n1 >> 4;
+    auto dsum = [&](int64_t j, int f0, int f1) -> uint32_t {  // fields f0..f1 of dword j
+        const uint32_t mask = (f1 - f0 == 15) ? ~0u : (((1u << (2 * (f1 - f0 + 1))) - 1u) << (2 * f0));
+        const uint32_t d = tw[j] & mask;
+        uint32_t sum = fsum32(d, 0u);  // an escaped field counts kEsc here
+        uint32_t e = fbig32(d);
+        while (e) {
+            const int b = __builtin_ctz(e);
+            e &= e - 1u;
+            const int64_t p = 16 * j + b / 2 - kPadPos + 1;
+            sum += ovf_lookup(U, track, (uint32_t)p) - kEsc;
+        }
+        return sum;
+    };
+    if (j0 == j1) return dsum(j0, (int)(n0 & 15), (int)(n1 & 15));
+    uint32_t sum = dsum(j0, (int)(n0 & 15), 15) + dsum(j1, 0, (int)(n1 & 15));
+#pragma unroll 4
+    for (int64_t j = j0 + 1; j < j1; ++j) {
+        const uint32_t b = pl[j];
+        sum += b == 255u ? dsum(j, 0, 15) : b;
+    }
+    return sum;
+}
+
+// exptSums of the non-control samples over a region: every tag of a
+// non-control sample is a pooled hit, so its exptSum is its track's range
+// sum (one lane per (strand, sample) track; sc: 256 words of the wave's LDS)
+template <bool NONDIR>
+__device__ __forceinline__ void nc_range_sums(uint32_t (&esum)[4], const UnitDesc &U, const StatParams &P,
+                                              uint32_t left, uint32_t right, int lane, uint32_t *sc) {
+    const int S = P.S, nnc = P.nnc;
+    constexpr int NSTR = NONDIR ? 2 : 1;
+    __builtin_amdgcn_wave_barrier();  // earlier readers of the area are done
+    for (int i = lane; i < S; i += 64) sc[i] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int t = lane; t < nnc * NSTR; t += 64) {
+        const int st = t >= nnc ? 1 : 0;
+        const int smp = P.nc[t - st * nnc];
+        atomicAdd(&sc[smp], track_range_sum(U, S, st, smp, left, right));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int smp = 64 * q + lane;
+        if (smp < S && !P.is_control[smp]) esum[q] += sc[smp];
+    }
+    __builtin_amdgcn_wave_barrier();  // the area is reused
+}
+
 // K3's occupancy: 5 waves per EU, i.e. <= 96 VGPRs (one directional
 // sample: a 40-byte spill), so two K3 waves fit beside K1a's three per SIMD.
 // Same-box A/B (profiles/r04/k1b_dead/, k3_all/): configs[1] K3 alone 0.160
@@ -2228,6 +2290,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
 #pragma unroll
     for (int d = -NH; d <= NH; ++d) wm[d + NH] = win_mask(d, bw);
     const int S = P.S;  // <= 256 (checked by the host)
+    // several samples, integer pooling: the non-control samples' exptSums are
+    // range sums of their chunk-sum planes (nc_range_sums), the pooled count
+    // of a hit is the window word's own value
+    constexpr bool kRS = kTB == 2 && POOL != 2;
 
     // per-wave cache of the pass-1 hit totals pc (pass 2 reads them back)
     uint32_t *pcache = (uint32_t *)(lds_ + kKTab) + (threadIdx.x >> 6) * (kStatCache * 64);
@@ -2342,7 +2408,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 load_words<kPK, POOL>(pkr, U, S, 1, (int64_t)kpos - bw, lane, P.nnc, P.nc, P.coef);
         }
         int blk = 0;
-        bool counted = false;
+        bool counted = false, staged = false;
         if constexpr (POOL == 0) {
             // one pooled sample: the region's count bytes (<= kStatCache
             // words) are fetched with all loads in flight at once, then
@@ -2441,6 +2507,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                     const bool h0 = valid && pf != 0u;
                     const bool h1 = NONDIR && valid && pr != 0u;
                     uint32_t pc = 0;
+                    // (every sample from the stage: cheaper here than the
+                    // plane range sums -- configs[3] K3 0.53 vs 0.73 ms)
                     for (int s = 0; s < S; ++s) {
                         uint32_t c = h0 ? fld(s) : 0u;
                         if constexpr (NONDIR) c += h1 ? fld(S + s) : 0u;
@@ -2460,6 +2528,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 }
                 __builtin_amdgcn_wave_barrier();  // terms reused below
                 counted = true;
+                staged = true;
             }
         }
         if (kn && !counted) {
@@ -2478,6 +2547,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                     if (h0) pc += (uint32_t)c0[0];
                     if (h1) pc += (uint32_t)c1[0];
                     esum1 += pc;
+                } else if (kRS) {  // (as in the scoring loop below)
+                    if (h0) pc += (uint32_t)c0[0];
+                    if (h1) pc += (uint32_t)c1[0];
+                    for (int s = 0; s < S && P.nnc < S; ++s) {
+                        if (!P.is_control[s]) continue;
+                        uint32_t c = 0;
+                        if (h0) c += count_at(U, S, 0, s, x);
+                        if (h1) c += count_at(U, S, 1, s, x);
+                        pc += c;
+                        const uint32_t t = wave_sum_u32(c);
+                        if (lane == (s & 63)) {
+                            const int slot = s >> 6;
+                            esum[0] += slot == 0 ? t : 0u;
+                            esum[1] += slot == 1 ? t : 0u;
+                            esum[2] += slot == 2 ? t : 0u;
+                            esum[3] += slot == 3 ? t : 0u;
+                        }
+                    }
                 } else {
                     for (int s = 0; s < S; ++s) {
                         uint32_t c = 0;
@@ -2625,6 +2712,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                     if (NONDIR && sr_hit) pc += (uint32_t)cr[NONDIR ? NH : 0];
                 }
                 esum1 += pc;
+            } else if (kRS) {
+                // the pooled non-control count is the word's own centre
+                // value; control samples per word (their exptSums count
+                // pooled hits only); the non-controls' exptSums come from
+                // the plane range sums after the pass (nc_range_sums)
+                if (valid) {
+                    if (sf_hit) pc += (uint32_t)cf[NH];
+                    if (NONDIR && sr_hit) pc += (uint32_t)cr[NONDIR ? NH : 0];
+                }
+                for (int s = 0; s < S && P.nnc < S; ++s) {
+                    if (!P.is_control[s]) continue;
+                    uint32_t c = 0;
+                    if (valid) {
+                        if (sf_hit) c += count_at(U, S, 0, s, x);
+                        if (NONDIR && sr_hit) c += count_at(U, S, 1, s, x);
+                    }
+                    pc += c;
+                    const uint32_t t = wave_sum_u32(c);
+                    if (lane == (s & 63)) {
+                        const int slot = s >> 6;
+                        esum[0] += slot == 0 ? t : 0u;
+                        esum[1] += slot == 1 ? t : 0u;
+                        esum[2] += slot == 2 ? t : 0u;
+                        esum[3] += slot == 3 ? t : 0u;
+                    }
+                }
             } else {
                 for (int s = 0; s < S; ++s) {
                     uint32_t c = 0;
@@ -2658,6 +2771,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
             }
         }
         }  // !kn
+        if (kRS && S > 1 && !staged) nc_range_sums<NONDIR>(esum, U, P, left, right, lane, (uint32_t *)terms);
         if (POOL == 0 && S == 1) {
             const uint32_t t = wave_sum_u32(esum1);
             esum[0] = lane == 0 ? t : 0u;
