@@ -107,10 +107,11 @@ def test_replay_multi_sample_control_and_coeffs(gpu_lib, oracle):
 
 
 def test_replay_refuses_pipelined_and_profile(gpu_lib):
-    """bw > 511 (kMaxBw): outside the parallel scan, the whole-buffer replay"""
+    """bw > 511 (kMaxBw) on a nondirectional unit: outside the parallel scans
+    (K1 and the directional K1w), the segmented replay"""
     capi = gpu_lib
     with capi.Lib(0) as g:
-        g.set_params(600, 1, 0.003)
+        g.set_params(600, 1, 0.003, nondir=True)
         u = g.add_unit(10_000)
         g.scatter(u, 0, 0, np.array([5000], np.uint32), np.array([3], np.uint32))
         assert g.run() >= 0

@@ -38,7 +38,7 @@ def main():
             dt = time.perf_counter() - t0
             regs, _ = g.regions(n)
             print(json.dumps({"contig": name, "bp": L, "bw": bw, "region_thr": thr,
-                              "path": "replay" if bw > 511 else ("K1q" if thr <= 0 else "scan"), "ms": round(dt * 1e3, 3),
+                              "path": ("wide" if thr > 0 else "replay") if bw > 511 else ("K1q" if thr <= 0 else "scan"), "ms": round(dt * 1e3, 3),
                               "gbps": round(L / dt / 1e9, 3), "candidates": int(n),
                               "accepted": int(regs["accepted"].sum())}), flush=True)
 

@@ -23,6 +23,7 @@
 #include "stats1.hip"   // (its LDS size)
 #include "emulate.hip"
 #include "q11place.hip"
+#include "wide.hip"
 
 namespace upk {
 // the templated K1 / K3 / K4 kernels live in four translation units, one per
@@ -690,7 +691,7 @@ static void set_q_params(up_ctx *c) {
 // 2^32 for the largest possible window, and distinct Q ordering the FP64
 // scores: alpha (Q+1)(1 - delta) > alpha Q (1 + delta) for every Q <= Qmax
 static bool q_mode(const up_ctx *c) {
-    if (!c->q_ok || !c->coef.empty() || c->nc.empty()) return false;
+    if (!c->q_ok || !c->coef.empty() || c->nc.empty() || c->p.bw > kMaxBw) return false;
     // several pooled samples: K3 would score each peak from every sample's
     // window bytes, which cost more than the keys save in K1b (hg19, 8
     // samples + 1 control: K1b 2.07 -> 1.64 ms but K3 0.82 -> 1.08-1.23 ms,
@@ -717,7 +718,9 @@ static bool q_mode(const up_ctx *c) {
 // len+bw (Q16), rounded to whole strips, two positions per byte, with
 // kPadBytes zero bytes on both sides
 static uint64_t unit_stride(uint32_t len) {
-    const uint64_t dom = (uint64_t)len + kMaxBw + 1;
+    // (the domain of the widest UShort kernel: K1w and K3 read windows up to
+    // len + bw, bw <= 65535)
+    const uint64_t dom = (uint64_t)len + 65536;
     const uint64_t strips = (dom + kStrip - 1) / kStrip;
     return (uint64_t)kPadBytes + strips * kStripBytes + kPadBytes;
 }
@@ -1069,7 +1072,7 @@ static int sync_units(up_ctx *c) {
     for (size_t i = 0; i < c->units.size(); ++i) {
         Unit &u = c->units[i];
         // strips only serve the parallel scan (bw <= kMaxBw; wider kernels replay)
-        const uint64_t dom = (uint64_t)u.len + std::min<int>(c->p.bw, kMaxBw);
+        const uint64_t dom = (uint64_t)u.len + (uint32_t)c->p.bw;
         u.nstrips = (uint32_t)((dom + kStrip - 1) / kStrip);
         u.strip0 = strip;
         strip += u.nstrips;
@@ -1397,8 +1400,19 @@ static bool q11_whole_replay() {
     return on;
 }
 
+// K1w (wide.hip) for kernels wider than K1's halo: directional units, a
+// threshold > 0, no -w capture (its retirements come from the replay);
+// UNIPEAK_WIDE=0: the replay instead
+static bool wide_mode(const up_ctx *c) {
+    static const bool on = [] {
+        const char *e = getenv("UNIPEAK_WIDE");
+        return !(e && *e == '0');
+    }();
+    return on && c->p.bw > kMaxBw && kTB == 2 && c->p.region_thr > 0 && !c->p.nondir && !c->prof_capture;
+}
+
 static bool replay_mode(const up_ctx *c) {
-    return c->p.bw > kMaxBw || (!(c->p.region_thr > 0) && !q11_mode(c));
+    return (c->p.bw > kMaxBw && !wide_mode(c)) || (!(c->p.region_thr > 0) && !q11_mode(c));
 }
 
 static int check_params(up_ctx *c) {
@@ -1414,6 +1428,7 @@ static int check_runnable(up_ctx *c, bool profile = false) {
     int r = check_params(c);
     if (r) return r;
     if (replay_mode(c)) return UP_E_UNSUPPORTED;
+    if (profile && c->p.bw > kMaxBw) return UP_E_UNSUPPORTED;  // (the dense profile's window is K1's)
     return q11_mode(c) && !c->q11_run && !profile ? UP_E_UNSUPPORTED : UP_OK;
 }
 
@@ -1858,7 +1873,7 @@ static int enqueue_rest(up_ctx *c, int slot, const ScanParams &SP, const StatPar
     up_ctx::Pass &ps = c->pass[slot];
     const uint32_t ns = c->nstrips;
     const uint32_t nsb = (ns + kSegBlock - 1) / kSegBlock;
-    if (!ps.req_q11) {  // (K1q wrote every strip's runs itself)
+    if (!ps.req_q11 && c->p.bw <= kMaxBw) {  // (K1q and K1w wrote every strip's runs themselves)
         if (k1a_waves) {  // K1x: list the stashed work-list entries for K1b
             hipLaunchKernelGGL(xref_kernel, dim3(1), dim3(1024), 0, ps.stream, ps.d_xwcount.p, k1a_waves,
                                k1a_xcap, ps.d_xref.p, ps.d_xcount.p);
@@ -2010,7 +2025,16 @@ static int launch_pass(up_ctx *c, int slot) {
         const unsigned blocks = (unsigned)std::min<uint64_t>((ns + 3) / 4, 4096);
         hipLaunchKernelGGL(proc_runs_kernel, dim3(std::max(1u, blocks)), dim3(256), 0, s1, SP);
     } else {
-        dispatch_scan<false, kModeScreen>(c, s1, SP, 0, ns);   // K1a: stream + screen
+        if (c->p.bw > kMaxBw) {  // K1w: screen + exact in one (wide.hip)
+            graph = false;
+            const unsigned blocks = std::max(1u, std::min<uint32_t>(ns, 8192));
+            const int pm = pool_mode(c);
+            if (pm == 0) hipLaunchKernelGGL(wide_kernel<0>, dim3(blocks), dim3(64), 0, s1, SP);
+            else if (pm == 1) hipLaunchKernelGGL(wide_kernel<1>, dim3(blocks), dim3(64), 0, s1, SP);
+            else hipLaunchKernelGGL(wide_kernel<2>, dim3(blocks), dim3(64), 0, s1, SP);
+        } else {
+            dispatch_scan<false, kModeScreen>(c, s1, SP, 0, ns);   // K1a: stream + screen
+        }
     }
     HIPCHK(hipGetLastError());
     hipEvent_t k1a_end = ps.k1a_end;  // a timed pass's end-of-K1a event serves as well
