@@ -176,14 +176,17 @@ int up_reset_units(up_ctx *ctx);
  * describe).  A unit that processes position 1 (an add at <= bw + 1) adds a
  * short exact replay (K0) around it, from the start of the buffer's
  * previous unit's last run to the first clean leap past it; those records
- * name their closing add in close_pos like the whole-buffer replay's.  A
- * negative coefficient, the -w capture with such a unit, and bw >
- * UP_MAX_PARALLEL_BW (511: K1's register-resident halo of NH <= 8
- * 64-position words) run the exact state machine over every unit instead
- * (K0 replay, sequential per buffer: exact, slow).
- * up_run_async refuses both (UP_E_UNSUPPORTED); up_unit_profile* refuse the
- * replay.  up_shift_scan correlates a replayed region's stored scores
- * (Region::scores), as strandCorr does.
+ * name their closing add in close_pos like the whole-buffer replay's.
+ * bw > UP_MAX_PARALLEL_BW (511: K1's register-resident halo of NH <= 8
+ * 64-position words) on directional units with a threshold > 0 runs K1w,
+ * the parallel scan for wide kernels (up to 65535; pipelined like K1; no
+ * dense profile).  A negative coefficient at a threshold <= 0, the -w
+ * capture with a head unit or with bw > 511, and bw > 511 on nondirectional
+ * units or at a threshold <= 0 run the exact state machine over every unit
+ * instead (K0, as independent chains from every run start: exact, far
+ * slower than the scans); up_run_async refuses those (UP_E_UNSUPPORTED),
+ * up_unit_profile* refuse them and bw > 511.  up_shift_scan correlates a
+ * replayed region's stored scores (Region::scores), as strandCorr does.
  * With a threshold <= 0 the last region of a unit is still open after its
  * flush and is closed in the buffer's next unit (UP_CLOSE_Q11_HEAD); the
  * last region of a buffer's last unit in the context is never closed (the
