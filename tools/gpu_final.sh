@@ -31,6 +31,10 @@ tests)
     timeout -k 10 300 python bench.py --bw $b --steps 20 --warmup 2 --no-cpu-baseline > "$F/bench_bw$b.json" 2> "$F/bench_bw$b.err" || { tail -3 "$F/bench_bw$b.err"; exit 1; }
     line "$F/bench_bw$b.json" bw$b
   done
+  # the paths outside K1: wide kernels, the replay, -r 0 with heads
+  timeout -k 10 300 python tools/replay_probe.py chr21 > "$F/replay_probe_chr21.jsonl" 2> "$F/replay_probe.err" || exit 1
+  timeout -k 10 300 python tools/q11_heads_probe.py > "$F/q11_heads_probe.json" 2> "$F/q11_heads_probe.err" || exit 1
+  cat "$F/q11_heads_probe.json"
   ;;
 prof)
   cd /tmp && export TMPDIR=/tmp
