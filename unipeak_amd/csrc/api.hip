@@ -344,6 +344,10 @@ struct up_ctx {
     // replayed records among them (index, offset of their stored scores)
     bool q11_place_in_pass = false;  // the pass places its records itself (no heads)
     bool q11_placed = false;         // the current records are a placed K1q list
+    // K0 chain groups: per unit, an add past bw (unit_aligned_kernel), kept
+    // while the unit layout and the tracks are unchanged (sync_units clears it)
+    std::vector<uint32_t> aligned_cache;
+    bool aligned_valid = false;
     DevBuf<up_region> d_q11_stage;
     DevBuf<uint32_t> d_q11_stage_cnt;
     DevBuf<Q11Place> d_q11_tab;
@@ -1067,6 +1071,7 @@ int up_unit_last_add(up_ctx *c, uint32_t unit, uint32_t *last) {
 
 static int sync_units(up_ctx *c) {
     if (!c->units_dirty && c->bw_layout == c->p.bw) return UP_OK;
+    c->aligned_valid = false;
     std::vector<UnitDesc> d(c->units.size());
     uint32_t strip = 0;
     for (size_t i = 0; i < c->units.size(); ++i) {
@@ -1488,7 +1493,9 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
     // (it cannot leave state behind), so independent head-hit units replay in
     // parallel instead of one wave walking the buffer
     std::vector<uint32_t> aligned(nu, 0);
-    if (!replay_all && !q && nu) {
+    if (!replay_all && !q && nu && c->aligned_valid && c->aligned_cache.size() == nu) {
+        aligned = c->aligned_cache;  // (a function of the tracks and bw: once per layout)
+    } else if (!replay_all && !q && nu) {
         HIPCHK(c->d_q11_head.ensure(nu));
         HIPCHK(hipMemsetAsync(c->d_q11_head.p, 0, nu * sizeof(uint32_t), c->stream));
         hipLaunchKernelGGL(unit_aligned_kernel, dim3(nu), dim3(256), 0, c->stream, c->d_units.p, S, (int)c->p.bw,
@@ -1496,6 +1503,8 @@ static int emulate_units(up_ctx *c, const uint32_t *d_head, bool replay_all, std
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(aligned.data(), c->d_q11_head.p, nu * 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
+        c->aligned_cache = aligned;
+        c->aligned_valid = true;
     }
     std::vector<std::vector<uint32_t>> groups;
     {
@@ -1789,37 +1798,51 @@ static int replay_head_hits(up_ctx *c, int slot) {
         par = dpar.data();
         pcnt = dcnt.data();
     }
-    // merge: unit-major; within a unit the replayed regions, then the
-    // parallel ones that start at or after the resync position
-    std::vector<std::pair<uint64_t, int64_t>> keys;  // (unit<<32 | order, +par idx / -emu idx-1)
-    for (uint32_t i = 0; i < nemu; ++i) keys.push_back({((uint64_t)emu[i].unit << 32) | i, -(int64_t)i - 1});
-    for (uint64_t i = 0; i < c->nreg; ++i) {
-        const uint32_t x = resync[par[i].unit];
-        if (x != 0 && par[i].left < x) continue;
-        keys.push_back({((uint64_t)par[i].unit << 32) | (0x80000000u + par[i].left / 2), (int64_t)i});
-    }
-    std::stable_sort(keys.begin(), keys.end(),
-                     [](const std::pair<uint64_t, int64_t> &a, const std::pair<uint64_t, int64_t> &b) {
-                         return (a.first >> 32) < (b.first >> 32);
-                     });
+    // merge, unit-major: within a unit the replayed regions (emission
+    // order), then the parallel ones that start at or after the resync
+    // position.  The parallel records are unit-major already (K2's order):
+    // one linear pass, the untouched runs of records copied in bulk
+    std::vector<uint32_t> eorder(nemu);
+    for (uint32_t i = 0; i < nemu; ++i) eorder[i] = i;
+    std::stable_sort(eorder.begin(), eorder.end(), [&](uint32_t a, uint32_t b) { return emu[a].unit < emu[b].unit; });
     c->h_regions.clear();
     c->h_counts.clear();
     c->h_emulated.clear();
     c->h_score_off.clear();
-    for (auto &k : keys) {
-        if (k.second < 0) {
-            const uint32_t i = (uint32_t)(-k.second - 1);
+    c->h_regions.reserve(c->nreg + nemu);
+    c->h_counts.reserve((c->nreg + nemu) * (size_t)S);
+    c->h_emulated.reserve(c->nreg + nemu);
+    c->h_score_off.reserve(c->nreg + nemu);
+    auto push_par = [&](uint64_t a, uint64_t b) {  // par records [a, b)
+        if (a >= b) return;
+        c->h_regions.insert(c->h_regions.end(), par + a, par + b);
+        c->h_counts.insert(c->h_counts.end(), pcnt + a * S, pcnt + b * S);
+        c->h_emulated.insert(c->h_emulated.end(), b - a, 0);
+        c->h_score_off.insert(c->h_score_off.end(), b - a, ~0ull);
+    };
+    uint32_t ei = 0;
+    uint64_t pi = 0;
+    while (ei < nemu || pi < c->nreg) {
+        // the next unit holding a record of either list
+        const uint32_t ue = ei < nemu ? emu[eorder[ei]].unit : ~0u;
+        const uint32_t up = pi < c->nreg ? par[pi].unit : ~0u;
+        const uint32_t u = ue < up ? ue : up;
+        for (; ei < nemu && emu[eorder[ei]].unit == u; ++ei) {
+            const uint32_t i = eorder[ei];
             c->h_regions.push_back(emu[i]);
             c->h_counts.insert(c->h_counts.end(), ecnt.begin() + (size_t)i * S, ecnt.begin() + (size_t)(i + 1) * S);
             c->h_emulated.push_back(1);
             c->h_score_off.push_back(soff[i]);
-        } else {
-            const uint64_t i = (uint64_t)k.second;
-            c->h_regions.push_back(par[i]);
-            c->h_counts.insert(c->h_counts.end(), pcnt + i * S, pcnt + (i + 1) * S);
-            c->h_emulated.push_back(0);
-            c->h_score_off.push_back(~0ull);
         }
+        const uint32_t x = u < resync.size() ? resync[u] : 0u;
+        uint64_t run = pi;  // start of the current run of kept records
+        for (; pi < c->nreg && par[pi].unit == u; ++pi) {
+            if (x != 0 && par[pi].left < x) {
+                push_par(run, pi);
+                run = pi + 1;
+            }
+        }
+        push_par(run, pi);
     }
     return publish_host_regions(c, ps);
 }
