@@ -23,7 +23,7 @@ tests)
   timeout -k 10 400 python bench.py > "$F/bench.json" 2> "$F/bench.err" || { tail -5 "$F/bench.err"; exit 1; }
   line "$F/bench.json" hg19-dir1
   for w in hg19-nondir1 hg19-8s1c hg19-shift hg19mm9-32rep hg19mm9-32s; do
-    st=20; case $w in hg19mm9*) st=5;; hg19-shift) st=10;; esac
+    st=20; case $w in hg19-shift) st=10;; esac
     timeout -k 10 400 python bench.py --workload $w --steps $st --warmup 2 --no-cpu-baseline > "$F/bench_$w.json" 2> "$F/bench_$w.err" || { tail -3 "$F/bench_$w.err"; exit 1; }
     line "$F/bench_$w.json" $w
   done

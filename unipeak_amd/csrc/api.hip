@@ -2585,14 +2585,16 @@ static int q11_finish(up_ctx *c, const std::vector<uint32_t> *heads) {
                 c->hp_regions[slot].p[d] = r;
                 std::memcpy(c->hp_counts[slot].p + d * S, k, S * 4);
             }
-            const uint32_t sh[3] = {r.left, r.right, r.unit};  // (stored scores: the extent only)
-            HIPCHK(hipMemcpy(c->d_q11_st.p + d, &sh[0], 4, hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(c->d_q11_en.p + d, &sh[1], 4, hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(c->d_q11_src.p + d, &sh[2], 4, hipMemcpyHostToDevice));
+            // (stored scores: only the extent matters) -- async fills, no
+            // round trip per record
+            HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(c->d_q11_st.p + d), r.left, 1, c->stream));
+            HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(c->d_q11_en.p + d), r.right, 1, c->stream));
+            HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(c->d_q11_src.p + d), r.unit, 1, c->stream));
             c->q11_rep.push_back({d, soff[i]});
             ++d;
         }
     }
+    HIPCHK(hipStreamSynchronize(c->stream));
     c->nreg = total;
     return UP_OK;
 }
