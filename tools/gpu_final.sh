@@ -3,6 +3,7 @@
 # gpurun_out/<tag>/; the first failure ends the stage):
 #   tools/gpu_final.sh TAG tests   every GPU test, smoke, the default bench line
 #                                  (CPU baselines), the other BASELINE workloads
+#   tools/gpu_final.sh TAG bench   the bench lines and probes alone
 #   tools/gpu_final.sh TAG prof    rocprofv3 kernel stats of the default bench,
 #                                  K1a PMC traffic (FETCH_SIZE / WRITE_SIZE passes,
 #                                  gfx950-corrected), SQ counter passes
@@ -20,6 +21,8 @@ tests)
   tail -1 "$F/pytest.log"
   timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$F/smoke.log" 2>&1 || { cat "$F/smoke.log"; exit 1; }
   cat "$F/smoke.log"
+  ;&
+bench)
   timeout -k 10 400 python bench.py > "$F/bench.json" 2> "$F/bench.err" || { tail -5 "$F/bench.err"; exit 1; }
   line "$F/bench.json" hg19-dir1
   for w in hg19-nondir1 hg19-8s1c hg19-shift hg19mm9-32rep hg19mm9-32s; do
