@@ -471,10 +471,18 @@ int up_open(int hip_device, up_ctx **out) {
     if (const char *e = getenv("UNIPEAK_K3_ONE")) c->k3_one = atoi(e) != 0;
     if (const char *e = getenv("UNIPEAK_CHAINS")) c->n_chain = std::min(4, std::max(1, atoi(e)));
     if (const char *e = getenv("UNIPEAK_LAUNCHER")) c->use_launcher = e[0] != '0';
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     {
         int least = 0, greatest = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        // the context stream (track writes, the K0 head replays between
+        // pipelined passes) at high priority: K0's few latency-bound waves
+        // are dispatched ahead of the in-flight passes' queued K1b/K3 blocks
+        // (configs[4], same box, three alternating pairs: 1.52-1.63 vs
+        // 1.65-1.67 ms/step, profiles/r05/ctx_prio.txt); UNIPEAK_CTX_PRIO=0:
+        // normal priority
+        const char *ep = getenv("UNIPEAK_CTX_PRIO");
+        HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking,
+                                           (ep && ep[0] == '0') ? least : greatest));
         const char *e = getenv("UNIPEAK_K1A_PRIO");  // A/B: 0 = normal priority
         HIPCHK(hipStreamCreateWithPriority(&c->k1a_stream, hipStreamNonBlocking,
                                            (e && e[0] == '0') ? least : greatest));
