@@ -49,7 +49,11 @@ sys.path.insert(0, ROOT)
 # RCCL's: more hardware queues than HIP's default 4, so no stream of a pass
 # shares an in-order queue with another (read at HIP initialisation)
 # (the configs[2] pipeline holds two contexts: twice the streams)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "12" if "hg19-shift" in sys.argv else "8")
+# Set explicitly (a box that exports HIP's default 4 would otherwise keep it,
+# and the five streams would share four in-order queues); UNIPEAK_HWQ
+# overrides; both values go into the bench line (hw_queues)
+HWQ_INHERITED = os.environ.get("GPU_MAX_HW_QUEUES")
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("UNIPEAK_HWQ") or ("12" if "hg19-shift" in sys.argv else "8")
 
 from unipeak_amd import capi, shard  # noqa: E402
 
@@ -109,7 +113,7 @@ def load_table(names):
 def pmc_traffic(bytes_per_launch):
     """HBM bytes per K1a launch from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.py) when they were taken on this exact workload."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06",):  # (earlier rounds' files measured other K1a builds)
         p = os.path.join(ROOT, "profiles", rnd, "k1a_pmc_traffic.json")
         try:
             d = json.load(open(p))
@@ -282,12 +286,18 @@ def main():
                     local_tags += g2.tag_total(u, st, smp)
         g2.close()
     gen_s = time.time() - t_gen
-    # K1a algorithmic bytes per bp per strand per non-control sample: what
-    # its stream reads -- the chunk-sum plane (1 byte per 16 bp) for one
-    # directional track, else the TB-bit counts
-    dens = g.scan_density()  # bytes per 1,024 positions of a unit
-    alg_bytes = sum(lens[units[k][0]] for k in mine) * dens // 1024
+    mine_bp = sum(lens[units[k][0]] for k in mine)
     copy_gbps = g.hbm_copy_gbps(1 << 30, 5)
+    # legs (DESIGN.md §3 "Index policy", §7): "cold" -- every pass reads only
+    # the packed 2-bit tracks, no derived index survives between passes
+    # (UP_INDEX_NEVER): the reference's one pass per run, the headline value;
+    # "warm" -- the chunk-sum plane / pooled planes / pooled count tracks are
+    # built once (untimed) and reused, a parameter sweep's re-scan (value_warm)
+    legs = os.environ.get("UNIPEAK_BENCH_LEGS", "cold,warm").split(",")
+    policy_of = {"cold": capi.INDEX_NEVER, "warm": capi.INDEX_ALWAYS}
+    if not legs or any(x not in policy_of for x in legs):
+        raise SystemExit(f"UNIPEAK_BENCH_LEGS={os.environ.get('UNIPEAK_BENCH_LEGS')}: cold and/or warm")
+    g.set_index_policy(policy_of[legs[0]])
 
     phase = {"allreduce": 0.0, "launch": 0.0, "wait": 0.0, "gather_merge": 0.0}
     sub = {"submit": 0.0, "target": 0.0, "run_async": 0.0}  # parts of "launch"
@@ -468,81 +478,124 @@ def main():
         if comm is not None:
             comm.dist.barrier()
 
-    g.set_timing(2)  # warm-up passes report every phase
-    for _ in range(args.warmup):
-        step()
-    drain()
-    warm = [float(x) for x in done_times[-1]] if done_times else [0.0] * 5
-    if rank == 0 and done_times:
-        tt = done_times[-1]
-        print(f"[bench] warmup: K1 {tt[0]:.3f} ms (exact part {tt[4]:.3f}), K2 {tt[1]:.3f} ms, "
-              f"K3 {tt[2]:.3f} ms, pass wall {tt[3]:.3f} ms", file=sys.stderr, flush=True)
-    g.set_timing(1)  # timed passes: HIP events around K1a only
-    timed[0] = True
-    for k in phase:
-        phase[k] = 0.0
-    for k in sub:
-        sub[k] = 0.0
-    done_times.clear()
-    bbase[0] += it[0]
-    it[0] = 0
-    barrier()
-    if comm is not None:
-        comm.torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    final = drain()  # inside the timed region: the last step's records reach rank 0
-    barrier()
-    if comm is not None:
-        comm.torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.steps
-    dump = os.environ.get("UNIPEAK_BENCH_DUMP")
-    if final is not None and dump:  # rehearsals: the merged records of the last step
-        blocks, _, _ = border.blocks(final[1])
-        recs = [b.copy() for _, b, _ in blocks]
-        for (gunit, _, _), r in zip(blocks, recs):
-            r["unit"] = gunit  # rank-local unit id -> global unit id
-        np.savez(dump, recs=np.concatenate(recs) if recs else np.zeros(0, capi.REGION_DTYPE),
-                 counts=np.concatenate([c for _, _, c in blocks]) if blocks else np.zeros((0, S), np.uint32))
-    if final is not None:  # the last step's records: accepted count (outside the timing)
-        final = (final[0], sum(int(np.count_nonzero(r["accepted"])) for r, _ in final[1] if len(r)))
+    def run_leg(name):
+        """warm-up passes, then exactly args.steps timed steps under the leg's
+        index policy (barrier + sync on both sides, max over ranks), then
+        three blocking passes for the isolated per-kernel breakdown"""
+        barrier()
+        g.set_index_policy(policy_of[name])
+        g.set_timing(2)  # warm-up passes report every phase
+        for _ in range(args.warmup):
+            step()
+        drain()
+        warm = [float(x) for x in done_times[-1]] if done_times else [0.0] * 5
+        if rank == 0 and done_times:
+            tt = done_times[-1]
+            print(f"[bench] {name} warmup: K1 {tt[0]:.3f} ms (exact part {tt[4]:.3f}), K2 {tt[1]:.3f} ms, "
+                  f"K3 {tt[2]:.3f} ms, pass wall {tt[3]:.3f} ms", file=sys.stderr, flush=True)
+        # K1a algorithmic bytes per bp per strand per non-control sample: what
+        # its stream reads -- the chunk-sum plane (1 byte per 16 bp) for one
+        # directional track with the index on, else the TB-bit counts (DESIGN.md §3-4)
+        dens = g.scan_density()  # bytes per 1,024 positions of a unit
+        alg_bytes = mine_bp * dens // 1024
+        builds0 = g.index_state()[1]
+        g.set_timing(1)  # timed passes: HIP events around K1a only
+        timed[0] = True
+        for k in phase:
+            phase[k] = 0.0
+        for k in sub:
+            sub[k] = 0.0
+        read_s[0], read_s[1] = 0.0, 0
+        done_times.clear()
+        bbase[0] += it[0]
+        it[0] = 0
+        barrier()
+        if comm is not None:
+            comm.torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        final = drain()  # inside the timed region: the last step's records reach rank 0
+        barrier()
+        if comm is not None:
+            comm.torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        timed[0] = False
+        builds = g.index_state()[1] - builds0  # index builds inside the timed steps
+        dump = os.environ.get("UNIPEAK_BENCH_DUMP")
+        if final is not None and dump and name == legs[0]:  # rehearsals: the merged records of the last step
+            blocks, _, _ = border.blocks(final[1])
+            recs = [b.copy() for _, b, _ in blocks]
+            for (gunit, _, _), r in zip(blocks, recs):
+                r["unit"] = gunit  # rank-local unit id -> global unit id
+            np.savez(dump, recs=np.concatenate(recs) if recs else np.zeros(0, capi.REGION_DTYPE),
+                     counts=np.concatenate([c for _, _, c in blocks]) if blocks else np.zeros((0, S), np.uint32))
+        if final is not None:  # the last step's records: accepted count (outside the timing)
+            final = (final[0], sum(int(np.count_nonzero(r["accepted"])) for r, _ in final[1] if len(r)))
+        # after the timed region: blocking passes (nothing overlapping) for the
+        # per-kernel breakdown of one pass on an otherwise idle GPU
+        iso = []
+        if pipelined:
+            g.set_record_target(nr.my_slot_address(it[0]), cap)
+        g.set_timing(2)
+        for _ in range(3):
+            g.run()
+            iso.append(g.timings())
+        iso = [float(np.median([t[k] for t in iso])) for k in range(5)]
+        # K1a = K1 minus its exact part (timing level 1: K1b = 0); level-0 passes carry no events
+        k1a = [t[0] - t[4] for t in done_times if t[0] > 0] or [t[0] for t in done_times]
+        k1a_ms = float(np.mean(k1a))
+        my_achieved = alg_bytes / (k1a_ms * 1e-3) / 1e9
+        if comm is not None:
+            dt = comm.max_over_ranks(dt)
+            achieved = comm.sum_over_ranks(my_achieved) / world  # mean per-GPU K1a GB/s
+            k1a_max = comm.max_over_ranks(k1a_ms)
+        else:
+            achieved, k1a_max = my_achieved, k1a_ms
+        if rank == 0:
+            print(f"[bench] {name}: {dt * 1e3:.4f} ms/step, K1a {k1a_ms:.4f} ms ({alg_bytes / 1e6:.1f} MB), "
+                  f"index builds {builds}; per-step phases (ms): " + ", ".join(
+                      f"{k} {v / args.steps * 1e3:.3f}" for k, v in phase.items()) +
+                  f"; record read {read_s[0] / max(read_s[1], 1) * 1e3:.3f} ms x{read_s[1]} (helper thread)"
+                  "; launch = " + ", ".join(f"{k} {v / args.steps * 1e3:.3f}" for k, v in sub.items()),
+                  file=sys.stderr, flush=True)
+        return dict(dt=dt, k1a_ms=k1a_ms, k1a_max=k1a_max, achieved=achieved, alg_bytes=alg_bytes, dens=dens,
+                    iso=iso, warm=warm, final=final, index_builds=builds)
+
+    res_leg = {}
+    for name in legs:
+        res_leg[name] = run_leg(name)
+    L0 = res_leg[legs[0]]
+    dt, k1a_ms, k1a_max, achieved = L0["dt"], L0["k1a_ms"], L0["k1a_max"], L0["achieved"]
+    alg_bytes, dens, iso, warm = L0["alg_bytes"], L0["dens"], L0["iso"], L0["warm"]
+    final = L0["final"]
     last = (None, final if final is not None else (n0, 0), None)
-    # after the timed region: blocking passes (nothing overlapping) for the
-    # per-kernel breakdown of one pass on an otherwise idle GPU
-    iso = []
+    k1_ms = k1a_ms
+    # one cold pass as a user's single run pays it (blocking up_run: first
+    # launch -> records in host memory), median of 5: without the index
+    # (the headline's pass), and with the index built inside it
+    single = {}
     if pipelined:
         g.set_record_target(nr.my_slot_address(it[0]), cap)
-    g.set_timing(2)
-    for _ in range(3):
-        g.run()
-        iso.append(g.timings())
-    iso = [float(np.median([t[k] for t in iso])) for k in range(5)]
-    # K1a = K1 minus its exact part (timing level 1: K1b = 0); level-0 passes carry no events
-    k1a = [t[0] - t[4] for t in done_times if t[0] > 0] or [t[0] for t in done_times]
-    k1 = k1a
-    k1_ms = float(np.mean(k1))
-    k1a_ms = float(np.mean(k1a))
-    my_achieved = alg_bytes / (k1a_ms * 1e-3) / 1e9
-    if comm is not None:
-        dt = comm.max_over_ranks(dt)
-        achieved = comm.sum_over_ranks(my_achieved) / world  # mean per-GPU K1a GB/s
-        k1a_max = comm.max_over_ranks(k1a_ms)
-    else:
-        achieved, k1a_max = my_achieved, k1a_ms
-
+    g.set_timing(0)
+    for tag, pol in (("no_index", capi.INDEX_NEVER), ("index_built_in_pass", capi.INDEX_ALWAYS)):
+        g.set_index_policy(pol)
+        ts = []
+        for _ in range(5):
+            g.invalidate_index()
+            t = time.perf_counter()
+            g.run()
+            ts.append((time.perf_counter() - t) * 1e3)
+        single[tag] = ts
     if rank == 0:
-        print("[bench] per-step phases (ms): " + ", ".join(
-            f"{k} {v / args.steps * 1e3:.3f}" for k, v in phase.items()) +
-            f"; record read {read_s[0] / max(read_s[1], 1) * 1e3:.3f} ms x{read_s[1]} (helper thread)"
-            "; launch = " + ", ".join(f"{k} {v / args.steps * 1e3:.3f}" for k, v in sub.items()),
-            file=sys.stderr, flush=True)
         value = genome / dt / 1e9
         if sim_world > 1:  # not a headline line: one rank's shard of an N-GPU plan
-            print(json.dumps({"sim_world": sim_world, "sim_rank": sim_rank, "ms_per_step": round(dt * 1e3, 4),
+            print(json.dumps({"sim_world": sim_world, "sim_rank": sim_rank, "leg": legs[0],
+                              "ms_per_step": round(dt * 1e3, 4),
+                              "legs_ms_per_step": {k: round(v["dt"] * 1e3, 4) for k, v in res_leg.items()},
                               "shard_bp": int(sum(lens[units[k][0]] * nstr for k in mine)), "k1a_ms": round(k1a_ms, 4),
-                              "k1_ms": round(k1_ms, 4), "warmup_timings_ms": [round(x, 4) for x in warm], "phases_ms": {k: round(v / args.steps * 1e3, 4)
-                                                                      for k, v in phase.items()}}), flush=True)
+                              "k1_ms": round(k1_ms, 4), "warmup_timings_ms": [round(x, 4) for x in warm],
+                              "isolated_ms": [round(x, 4) for x in iso]}), flush=True)
             g.set_record_target(0, 0)
             g.close()
             if pool is not None:
@@ -567,13 +620,22 @@ def main():
                        "genome_bp": genome, "units": len(units), "samples": S,
                        "parallelism": f"contig{'' if nondir else '-strand'} units LPT over {world} GPU(s)"},
             "regions": {"candidates": int(last[1][0]), "accepted": int(last[1][1])},
+            "index": ({"cold": "none: every pass reads only the packed 2-bit tracks (+ their overflow "
+                               "table); nothing derived from them survives between passes "
+                               "(UP_INDEX_NEVER, DESIGN.md §3) -- the reference's one pass per run",
+                       "warm": "chunk-sum plane / pooled planes / pooled count tracks built once before "
+                               "the timed steps and reused (UP_INDEX_ALWAYS): a re-scan of the same "
+                               "tracks"}[legs[0]]),
+            "index_builds_in_timed_steps": int(L0["index_builds"]),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "traffic_unit": "GB per launch (rocprofv3 PMC FETCH_SIZE+WRITE_SIZE, gfx950-corrected)",
                          "traffic_source": traffic_src,
-                         "kernel": "scan_kernel<..., kModeScreen> (K1a: stream + integer screen)",
+                         "kernel": ("scan_kernel<..., kModeScreenF> (K1a: stream of the 2-bit fields + screen)"
+                                    if legs[0] == "cold" else
+                                    "scan_kernel<..., kModeScreen> (K1a: stream + integer screen)"),
                          "kernel_ms": round(k1a_ms, 4), "kernel_ms_max_rank": round(k1a_max, 4),
                          "bytes_per_launch": int(alg_bytes),
                          "bytes_rule": (f"{dens / 1024} B per bp of a unit (" +
@@ -605,6 +667,30 @@ def main():
             rf["survey_rule_note"] = ("above 1: the kernel does not read SURVEY's uint32 bytes -- the tracks are "
                                       f"{TB}-bit counts with an exact overflow table and a chunk-sum plane "
                                       "(DESIGN.md §3)")
+        for name, Lg in res_leg.items():
+            if name == legs[0]:
+                continue
+            res["value_" + name] = round(genome / Lg["dt"] / 1e9, 3)
+            res[name] = {"ms_per_step": round(Lg["dt"] * 1e3, 4), "value": round(genome / Lg["dt"] / 1e9, 3),
+                         "index_builds": int(Lg["index_builds"]),
+                         "roofline": {"achieved": round(Lg["achieved"], 1),
+                                      "frac": round(Lg["achieved"] / HBM_PEAK_GBS, 4),
+                                      "kernel_ms": round(Lg["k1a_ms"], 4), "bytes_per_launch": int(Lg["alg_bytes"]),
+                                      "bytes_rule": f"{Lg['dens'] / 1024} B per bp of a unit",
+                                      "isolated_ms": {"k1a": round(Lg["iso"][0] - Lg["iso"][4], 4),
+                                                      "k1b_k1x": round(Lg["iso"][4], 4), "k2": round(Lg["iso"][1], 4),
+                                                      "k3": round(Lg["iso"][2], 4), "pass_wall": round(Lg["iso"][3], 4)}},
+                         "regions": {"candidates": int((Lg["final"] or (0, 0))[0]),
+                                     "accepted": int((Lg["final"] or (0, 0))[1])}}
+        res["single_pass_ms"] = {k: {"median": round(float(np.median(v)), 4), "runs": [round(x, 4) for x in v]}
+                                 for k, v in single.items()}
+        res["single_pass_note"] = ("one blocking up_run on an idle GPU, first launch -> records in host memory, "
+                                   "median of 5; no_index: the headline's cold pass; index_built_in_pass: "
+                                   "up_invalidate_index, then a pass that builds the planes/pooled tracks first")
+        res["hw_queues"] = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"),
+                            "inherited": HWQ_INHERITED, "library_streams": 5,
+                            "note": "set by bench.py before HIP initialisation; library streams: context "
+                                    "(high priority), K1a (high priority), three chain streams"}
         if world == 1 and not args.no_cpu_baseline and args.workload == "hg19-dir1":
             res["cpu_baseline"] = cpu_baseline(contigs, args, value, bg_set[0], last[1])
         print(json.dumps(res), flush=True)
@@ -649,6 +735,7 @@ def shift_pipeline(args, W):
     ctx = []
     for off in (0, shift):
         g = capi.Lib(0)
+        g.set_index_policy(capi.INDEX_NEVER)  # one pass per tool run, as the reference's (no index)
         g.set_params(bw, 1, 0.0029, nondir=True)
         tags = 0
         for ci, L in enumerate(lens):

@@ -179,8 +179,10 @@ int up_reset_units(up_ctx *ctx);
  * name their closing add in close_pos like the whole-buffer replay's.
  * bw > UP_MAX_PARALLEL_BW (511: K1's register-resident halo of NH <= 8
  * 64-position words) on directional units with a threshold > 0 runs K1w,
- * the parallel scan for wide kernels (up to 65535; pipelined like K1; no
- * dense profile).  A negative coefficient at a threshold <= 0, the -w
+ * the parallel scan for wide kernels (up to 32767, a window of 65535 cells;
+ * pipelined like K1; no dense profile).  Wider kernels (32768..65535, where
+ * the reference's UShort retirement count wraps, misc/peakcall.cpp:172-177)
+ * take the whole-buffer replay.  A negative coefficient at a threshold <= 0, the -w
  * capture with a head unit or with bw > 511, and bw > 511 on nondirectional
  * units or at a threshold <= 0 run the exact state machine over every unit
  * instead (K0, as independent chains from every run start: exact, far
@@ -249,11 +251,35 @@ int up_shift_scan(up_ctx *ctx, const uint64_t *region_idx, size_t n,
 int up_shift_best(up_ctx *ctx, const uint64_t *region_idx, size_t n,
                   uint16_t max_shift, uint16_t *best_shift, double *best_corr);
 
-/* bytes the streaming scan (K1a) reads per 1,024 positions of a unit under
- * the current parameters (its algorithmic bytes): 64 when it
- * streams a chunk-sum plane (bw <= 255: the pooled track's own plane, or the
- * unit's pooled plane of several samples / both strands), else
- * 1024 * up_track_bits() / 8 per pooled track and strand */
+/* The per-dataset index (DESIGN.md §3 "Index policy"): data derived from
+ * the packed tracks that repeated passes over the same tracks may reuse --
+ * per track a chunk-sum plane (1 byte per 16 positions), per unit a pooled
+ * plane and, with several pooled samples, a pooled count track (1 byte per
+ * position and strand).  The reference makes ONE pass per run
+ * (src/regions.cpp:311-391): a pass without the index reads only the packed
+ * tracks and pays no build.  Policies:
+ *   UP_INDEX_AUTO   (default) the first pass after a track or pooling change
+ *                   runs without it; the index is built (one launch per
+ *                   kind over every stale unit) before the second;
+ *   UP_INDEX_NEVER  no pass uses it: every pass costs what one cold pass
+ *                   costs (bw > UP_MAX_PARALLEL_BW still builds it: K1w
+ *                   screens on the planes);
+ *   UP_INDEX_ALWAYS built before the first pass.
+ * Refused while a pass is in flight (UP_E_STATE).  up_invalidate_index drops
+ * what was built (the next pass that wants it rebuilds it; AUTO counts
+ * passes anew).  up_index_state: *on = the next pass uses the index now,
+ * *builds = index builds so far in this context. */
+#define UP_INDEX_AUTO 0
+#define UP_INDEX_NEVER 1
+#define UP_INDEX_ALWAYS 2
+int up_set_index_policy(up_ctx *ctx, int policy);
+int up_invalidate_index(up_ctx *ctx);
+int up_index_state(up_ctx *ctx, int *on, uint64_t *builds);
+/* bytes the streaming scan (K1a) reads per 1,024 positions of a unit in the
+ * index state of the moment (its algorithmic bytes): 64 when
+ * it streams a chunk-sum plane (index on and bw <= 255: the pooled track's
+ * own plane, or the unit's pooled plane of several samples / both strands),
+ * else 1024 * up_track_bits() / 8 per pooled track and strand */
 int up_scan_density(up_ctx *ctx, uint32_t *bytes_per_1024);
 /* device-side timings of the last up_run in ms: [0]=K1 scan, [1]=K2
  * segment, [2]=K3 stats, [3]=whole up_run wall, [4]=K1 launches */

@@ -1,11 +1,13 @@
-"""K1a's chunk-sum plane (kernels.h, csum_kernel): one byte per
+"""K1a's chunk-sum plane (kernels.h, csum_units_kernel): one byte per
 16 positions, escaped fields at their counts, saturated at 255.  With one
 directional pooled track and bw <= 255 the screen streams the plane instead
 of the 2-bit fields.  These cases aim at the saturation (a chunk of 255 or
 more tags is unbounded; with a threshold high enough that the screen's
 tag budget wskip reaches 255 the saturated value must not pass as a bound),
 at every window width the plane serves (R = 1..16 chunks), and at planes
-rebuilt when tracks change between passes -- against the oracle."""
+rebuilt when tracks change between passes -- against the oracle.  The
+index policy is UP_INDEX_ALWAYS here (the plane serves the first pass
+too); tests/test_gpu_index.py runs passes without it."""
 import numpy as np
 import pytest
 
@@ -27,6 +29,7 @@ def dense_unit(rng, length, bw, blocks):
 
 def run(capi, bw, bg, length, pos, cnt, thr):
     with capi.Lib(0) as g:
+        g.set_index_policy(capi.INDEX_ALWAYS)
         g.set_params(bw, 1, bg, region_thr=thr, kurt_thr=50.0, corr_thr=-1.0, hit_thr=10.0)
         assert g.scan_density() == (64 if bw <= 255 else 256)
         u = g.add_unit(length)
@@ -77,6 +80,7 @@ def test_plane_follows_scatter_between_passes(gpu_lib, oracle):
     rng = np.random.default_rng(3)
     pos, cnt = dense_unit(rng, length, bw, [(50_000, 8, 3)])
     with gpu_lib.Lib(0) as g:
+        g.set_index_policy(gpu_lib.INDEX_ALWAYS)
         g.set_params(bw, 1, bg)
         u = g.add_unit(length)
         g.scatter(u, 0, 0, pos, cnt[:, 0])
@@ -111,6 +115,7 @@ def test_pooled_plane_follows_pooling_changes(gpu_lib, oracle):
                 dict(control=[0, 0, 1], coeffs=[2.5, 0.4]), dict(control=[0, 0, 0])]
     got = []
     with gpu_lib.Lib(0) as g:
+        g.set_index_policy(gpu_lib.INDEX_ALWAYS)
         g.set_params(bw, S, bg, **settings[0])
         u = g.add_unit(length)
         for s in range(S):

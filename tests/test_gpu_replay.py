@@ -201,3 +201,21 @@ def test_q11_blocking_only_profile_allowed(gpu_lib, oracle):
             g.run_async()  # K1q records are finished on the host: blocking up_run only
         f, _ = g.profile(u, length)
     assert oracle.profile(bw, bg, length, pos, cnt).tobytes() == f.tobytes()
+
+
+def test_threshold_zero_after_reset_reports_nothing(gpu_lib):
+    """a K1q pass (-r 0) with records, then up_reset_units and a pass over no
+    unit: no region (the K1q placement status of the earlier pass must not
+    be reported again)"""
+    rng = np.random.default_rng(720)
+    length, bw, bg = 60_000, 50, 0.003
+    pos, cnt = random_unit(rng, length, bw)
+    with gpu_lib.Lib(0) as g:
+        g.set_params(bw, 1, bg, region_thr=0.0)
+        u = g.add_unit(length)
+        g.scatter(u, 0, 0, pos, cnt[:, 0])
+        assert g.run() > 3
+        g.reset_units()
+        assert g.run() == 0
+        regs, _ = g.regions(0)
+        assert len(regs) == 0

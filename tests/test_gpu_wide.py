@@ -1,5 +1,6 @@
 """K1w (csrc/wide.hip): kernels wider than K1's register-resident halo (bw >
-511, up to the reference's UShort 65535, misc/kernel.hpp:16) on directional
+511, up to 32,767 -- a window of 65,535 cells, the reference's UShort
+retirement count; wider kernels replay, test_ushort_*) on directional
 units with a threshold > 0 -- a chunk-plane screen over each word's union
 window, then every lane's FP64 score over the window's adds in ascending
 position (the order the reference's deque cell receives them,
@@ -91,3 +92,38 @@ def test_wide_regions_cli(orc_bin, gpu_lib, tmp_path, bw):
     ct, files = make_inputs(tmp_path, 70 + int(bw), contigs, 2, n_cl=12, sd=200)
     out = compare_tool(orc_bin, tmp_path, "regions", ["-q", "-c", ct, "-f", "-b", bw, "-k", "0"] + files)
     assert out.count("\n") > 3
+
+
+@pytest.mark.parametrize("bw", [32767, 32768, 40000, 65535])
+def test_ushort_retirement_wrap(gpu_lib, oracle, bw):
+    """From bw 32,768 on the window (2bw + 1 cells) exceeds the reference's
+    UShort retirement count (misc/peakcall.cpp:172-177): a gap of 65,536 or
+    more between adds retires (gap mod 65,536) cells -- or (2bw + 1) mod
+    65,536 past 2bw -- and the rest of the window stays misaligned.  K1w
+    covers bw <= 32,767 only; wider kernels take the whole-buffer replay,
+    which models the wrap (emulate.hip).  Clusters 75,000 - 120,000 apart
+    with nothing between them; every candidate against the oracle."""
+    rng = np.random.default_rng(bw)
+    length, bg = 480_000, 0.002
+    d = {}
+    for c, n in ((20_000, 300), (95_000, 260), (215_000, 400), (290_000, 220), (400_000, 350)):
+        for o in np.rint(rng.normal(0, 80, n)).astype(np.int64):
+            d[int(c + o)] = d.get(int(c + o), 0) + 1
+    pos = np.array(sorted(d), np.uint32)
+    cnt = np.array([[d[int(p)]] for p in pos], np.uint32)
+    ref, ref_sums = oracle.run_unit(bw, bg, pos, cnt, region_thr=0.3, kurt_thr=0.0, hit_thr=1.0, cap=1 << 20)
+    regs, gcnt = run_units(gpu_lib, bw, bg, [(length, pos, cnt, None)], region_thr=0.3, kurt_thr=0.0,
+                           hit_thr=1.0)
+    assert len(ref) > 0
+    compare(ref, ref_sums, regs, gcnt)
+
+
+@pytest.mark.parametrize("bw", ["32767", "32768", "40000", "65535"])
+def test_ushort_wrap_regions_cli(orc_bin, gpu_lib, tmp_path, bw):
+    """bin/regions -b at and past the UShort wrap: tables byte-identical to
+    the oracle CLI (three contigs per buffer, both buffers)"""
+    contigs = [("chrA", 200_000), ("chrB", 90_000), ("chrC", 60_000)]
+    ct, files = make_inputs(tmp_path, 7 + int(bw), contigs, 1, n_cl=5, sd=300)
+    out = compare_tool(orc_bin, tmp_path, "regions",
+                       ["-q", "-c", ct, "-f", "-b", bw, "-k", "0", "-r", "0.2", "-t", "1"] + files)
+    assert any(line and not line.startswith("#") for line in out.splitlines())

@@ -64,6 +64,8 @@ def compile_lib(out, extra=(), jobs=None):
         (f"nh{k}", os.path.join(csrc, "nh_tu.hip"), [f"-DUPK_NH_TU={k}"]) for k in range(1, 9)]
     stamp = os.path.join(objdir, "flags.txt")  # objects built with other flags are stale
     same = os.path.exists(stamp) and open(stamp).read() == " ".join(flags)
+    if not same and os.path.exists(stamp):
+        os.remove(stamp)  # a partial build with new flags must not inherit the old stamp
     def one(u):
         name, src, defs = u
         obj = os.path.join(objdir, name + ".o")
@@ -72,9 +74,9 @@ def compile_lib(out, extra=(), jobs=None):
         return obj
     with ThreadPoolExecutor(jobs or min(7, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(one, units))
-    with open(stamp, "w") as f:
-        f.write(" ".join(flags))
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
+    with open(stamp, "w") as f:  # only after every object and the link succeeded
+        f.write(" ".join(flags))
     return out
 
 

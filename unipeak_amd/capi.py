@@ -72,10 +72,12 @@ EXPORTS = [
     "up_timings", "up_scan_density", "up_unit_profile", "up_hbm_copy_gbps", "up_set_record_target",
     "up_host_register", "up_unit_profile_range", "up_run_async", "up_run_wait", "up_set_timing",
     "up_set_profile_capture", "up_unit_replay_profile",
+    "up_set_index_policy", "up_invalidate_index", "up_index_state",
     "up_tir_open", "up_tir_close", "up_tir_set_stream", "up_tir_query", "up_tir_timings",
     "up_cm_open", "up_cm_close", "up_cm_add", "up_cm_collect", "up_cm_timings",
 ]
 TIR_HOST = 0xFFFFFFFF  # UP_TIR_HOST
+INDEX_AUTO, INDEX_NEVER, INDEX_ALWAYS = 0, 1, 2  # UP_INDEX_*
 
 
 def load_library(path=LIB_PATH):
@@ -123,6 +125,9 @@ def load_library(path=LIB_PATH):
         "up_shift_best": (c.c_int, [vp, vp, c.c_size_t, c.c_uint16, vp, vp]),
         "up_timings": (c.c_int, [vp, vp, c.c_int]),
         "up_scan_density": (c.c_int, [vp, u32p]),
+        "up_set_index_policy": (c.c_int, [vp, c.c_int]),
+        "up_invalidate_index": (c.c_int, [vp]),
+        "up_index_state": (c.c_int, [vp, c.POINTER(c.c_int), c.POINTER(c.c_uint64)]),
         "up_unit_profile": (c.c_int, [vp, c.c_uint32, vp, vp, c.c_uint32]),
         "up_hbm_copy_gbps": (c.c_int, [vp, c.c_uint64, c.c_int, c.POINTER(c.c_double)]),
         "up_set_record_target": (c.c_int, [vp, vp, c.c_uint64]),
@@ -333,6 +338,19 @@ class Lib:
         v = ctypes.c_double()
         _ck(self.L.up_hbm_copy_gbps(self.ctx, nbytes, reps, ctypes.byref(v)))
         return v.value
+
+    def set_index_policy(self, policy):
+        """INDEX_AUTO / INDEX_NEVER / INDEX_ALWAYS (up_set_index_policy)"""
+        _ck(self.L.up_set_index_policy(self.ctx, int(policy)))
+
+    def invalidate_index(self):
+        _ck(self.L.up_invalidate_index(self.ctx))
+
+    def index_state(self):
+        """(the next pass uses the index, index builds so far)"""
+        on, b = ctypes.c_int(0), ctypes.c_uint64(0)
+        _ck(self.L.up_index_state(self.ctx, ctypes.byref(on), ctypes.byref(b)))
+        return bool(on.value), int(b.value)
 
     def scan_density(self):
         """bytes K1a streams per 1,024 positions of a unit (up_scan_density)"""

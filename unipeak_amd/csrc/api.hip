@@ -117,6 +117,7 @@ struct Unit {
     bool cs_dirty = false;     // a track changed: rebuild its chunk-sum plane (csum_kernel)
     bool pool_dirty = true;    // rebuild the unit's pooled plane (pool_kernel)
     uint32_t ovf_max = 0;          // largest escaped count of any track
+    uint32_t pad_bw = 0;           // the widest kernel the track padding covers (unit_stride)
 };
 
 template <typename T>
@@ -222,6 +223,16 @@ struct up_ctx {
     bool units_dirty = true;
     std::vector<uint32_t> pool_sig;  // non-control samples + screen weights the pooled planes hold
     DevBuf<UnitDesc> d_units;
+    std::vector<UnitDesc> h_units;   // host copy of d_units
+    // the per-dataset index (chunk-sum planes, pooled planes, pooled count
+    // tracks; DESIGN.md §3 "Index policy"): up_set_index_policy, whether the
+    // unit table and the passes use it now, passes launched since the tracks
+    // or the pooling last changed, builds so far
+    int index_policy = UP_INDEX_AUTO;
+    bool index_on = false;
+    uint32_t passes_on_tracks = 0;
+    uint64_t index_builds = 0;
+    DevBuf<uint64_t> d_index_lists;  // sync_index's unit lists
     uint32_t nstrips = 0;
     int bw_layout = -1;  // bw the strip layout was computed for
     // per (track slot strand * S + sample, global strip): the strip or its
@@ -379,6 +390,10 @@ struct up_ctx {
 
 static bool busy(const up_ctx *c) { return c && c->seq_launched != c->seq_done; }
 
+// the tracks or the pooling changed: the index is rebuilt when a pass wants it
+// (the per-unit dirty flags say what), and UP_INDEX_AUTO counts passes anew
+static void index_stale(up_ctx *c) { c->passes_on_tracks = 0; }
+
 // the context, K1a and chain streams idle
 static void sync_all(up_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
@@ -408,12 +423,38 @@ int up_track_bits(void) { return kTB; }
 static bool plane_scan(const up_ctx *c);
 static int pool_mode(const up_ctx *c);
 static bool pct_mode(const up_ctx *c);
+static bool wide_mode(const up_ctx *c);
+
+static bool want_index(const up_ctx *c);
 
 int up_scan_density(up_ctx *c, uint32_t *b) {
     if (!c || !b) return UP_E_ARG;
     if (!c->have_params) return UP_E_STATE;
-    *b = plane_scan(c) ? 1024u / 16u
-                       : 1024u * (uint32_t)kTB / 8u * (uint32_t)c->nc.size() * (c->p.nondir ? 2u : 1u);
+    // (the next pass: it builds the index first if it wants it)
+    const bool plane = kTB == 2 && (c->p.bw + 64) / 64 <= 4 && want_index(c);
+    *b = plane ? 1024u / 16u : 1024u * (uint32_t)kTB / 8u * (uint32_t)c->nc.size() * (c->p.nondir ? 2u : 1u);
+    return UP_OK;
+}
+
+int up_set_index_policy(up_ctx *c, int policy) {
+    if (!c || policy < UP_INDEX_AUTO || policy > UP_INDEX_ALWAYS) return UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;  // passes in flight read the unit table
+    c->index_policy = policy;
+    return UP_OK;
+}
+
+int up_invalidate_index(up_ctx *c) {
+    if (!c) return UP_E_ARG;
+    if (busy(c)) return UP_E_STATE;
+    for (Unit &u : c->units) u.cs_dirty = u.pool_dirty = true;
+    index_stale(c);
+    return UP_OK;
+}
+
+int up_index_state(up_ctx *c, int *on, uint64_t *builds) {
+    if (!c) return UP_E_ARG;
+    if (on) *on = c->index_on ? 1 : 0;
+    if (builds) *builds = c->index_builds;
     return UP_OK;
 }
 
@@ -631,6 +672,7 @@ int up_set_params(up_ctx *c, const up_params *p) {
             c->pool_sig = sig;
             for (Unit &u : c->units) u.pool_dirty = true;
             c->units_dirty = true;
+            index_stale(c);
         }
         double kmax = 0.0;
         for (double v : c->kern) kmax = v > kmax ? v : kmax;
@@ -729,10 +771,12 @@ static bool q_mode(const up_ctx *c) {
 // track geometry (bytes): positions 1..len plus the scan domain up to
 // len+bw (Q16), rounded to whole strips, two positions per byte, with
 // kPadBytes zero bytes on both sides
-static uint64_t unit_stride(uint32_t len) {
-    // (the domain of the widest UShort kernel: K1w and K3 read windows up to
-    // len + bw, bw <= 65535)
-    const uint64_t dom = (uint64_t)len + 65536;
+static uint64_t unit_stride(uint32_t len, int bw) {
+    // (the scan domain [1, len + bw] and the windows around it, whose loads
+    // reach len + 2bw; at least K1's widest kernel, kMaxBw; a later wider
+    // -b regrows the unit, sync_layout)
+    const uint64_t w = (uint64_t)std::max(bw, kMaxBw);
+    const uint64_t dom = (uint64_t)len + 2 * w + 2;
     const uint64_t strips = (dom + kStrip - 1) / kStrip;
     return (uint64_t)kPadBytes + strips * kStripBytes + kPadBytes;
 }
@@ -746,7 +790,8 @@ int up_add_unit(up_ctx *c, uint32_t len, int32_t nstrands, int32_t buffer_id, ui
     u.len = len;
     u.nstrands = nstrands;
     u.buffer = buffer_id;
-    u.stride = unit_stride(len);
+    u.stride = unit_stride(len, c->p.bw);
+    u.pad_bw = std::max<uint32_t>(c->p.bw, kMaxBw);
     // the tracks, their chunk-sum planes (stride / 4 bytes each, kernels.h),
     // the unit's pooled plane
     const size_t bytes = u.stride * (size_t)c->p.n_samples * nstrands / 4 * 5 + u.stride / 4;
@@ -817,6 +862,7 @@ static int pack_track(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample,
         u.ovf_dirty = true;
         u.cs_dirty = u.pool_dirty = true;
         c->units_dirty = true;
+        index_stale(c);
         return UP_OK;
     }
     return UP_E_INTERNAL;
@@ -862,6 +908,7 @@ int up_unit_scatter(up_ctx *c, uint32_t unit, int32_t strand, uint16_t sample, s
         }
         u.cs_dirty = u.pool_dirty = true;  // the chunk sums change with any count
         c->units_dirty = true;
+        index_stale(c);
     }
     // the caller's arrays are copied into the staging buffers before we
     // return, so they may be reused at once; the kernels stay stream-ordered
@@ -1077,10 +1124,44 @@ int up_unit_last_add(up_ctx *c, uint32_t unit, uint32_t *last) {
     return UP_OK;
 }
 
-static int sync_units(up_ctx *c) {
+// every pass in flight has been launched and has finished on the device
+// (its completion is still the caller's up_run_wait)
+static void settle_in_flight(up_ctx *c);
+
+// track geometry of a unit after a bw change that its padding does not
+// cover: a larger allocation, every track copied at the new stride (the
+// padding past the domain reads zeros); the index is rebuilt
+static int regrow_unit(up_ctx *c, Unit &u) {
+    const int S = c->p.n_samples;
+    const uint64_t stride = unit_stride(u.len, c->p.bw);
+    const size_t bytes = stride * (size_t)S * u.nstrands / 4 * 5 + stride / 4;
+    uint8_t *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return UP_E_NOMEM;
+    HIPCHK(hipMemsetAsync(p, 0, bytes, c->stream));
+    HIPCHK(hipMemcpy2DAsync(p, stride, u.dptr, u.stride, u.stride, (size_t)S * u.nstrands, hipMemcpyDeviceToDevice,
+                            c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    (void)hipFree(u.dptr);
+    u.dptr = p;
+    u.stride = stride;
+    u.pad_bw = std::max<uint32_t>(c->p.bw, kMaxBw);
+    if (u.d_pct) (void)hipFree(u.d_pct);
+    u.d_pct = nullptr;
+    u.cs_dirty = u.pool_dirty = true;
+    return UP_OK;
+}
+
+// the unit layout: strips, overflow tables, escape bitmap, the unit table
+static int sync_layout(up_ctx *c) {
     if (!c->units_dirty && c->bw_layout == c->p.bw) return UP_OK;
     c->aligned_valid = false;
-    std::vector<UnitDesc> d(c->units.size());
+    for (Unit &u : c->units)
+        if ((uint32_t)c->p.bw > u.pad_bw) {
+            if (int r = regrow_unit(c, u)) return r;
+            index_stale(c);
+        }
+    std::vector<UnitDesc> &d = c->h_units;
+    d.assign(c->units.size(), UnitDesc{});
     uint32_t strip = 0;
     for (size_t i = 0; i < c->units.size(); ++i) {
         Unit &u = c->units[i];
@@ -1144,24 +1225,12 @@ static int sync_units(up_ctx *c) {
     c->nstrips = strip;
     c->ovf_max_all = 0;
     for (const Unit &u : c->units) c->ovf_max_all = std::max(c->ovf_max_all, u.ovf_max);
-    // pooled count tracks while several samples pool in uint32 (POOL 1):
-    // K1b, K3 and K4 read one byte track instead of every pooled sample's
-    const bool want_pct = pct_mode(c);
-    for (size_t i = 0; i < c->units.size(); ++i) {
-        Unit &u = c->units[i];
-        if (want_pct && !u.d_pct) {
-            HIPCHK(hipMalloc(&u.d_pct, (size_t)u.nstrands * kPerByte * u.stride));
-            u.pool_dirty = true;
-        } else if (!want_pct && u.d_pct) {
-            (void)hipFree(u.d_pct);
-            u.d_pct = nullptr;
-        }
-        d[i].pct = (uint64_t)(uintptr_t)u.d_pct;
-    }
     {
         // escape bitmap: bit (strip) of row (strand * S + sample) is set when
         // a block of the strip, or the block either side (the screen's halos,
         // <= kScrHalo chunks < kOvfBlk), holds an escaped field of that track
+        // (a function of the overflow entries, i.e. of the packed tracks:
+        // part of the track format, not of the index)
         const uint32_t S = (uint32_t)std::max<int32_t>(1, (int32_t)c->p.n_samples);
         const uint32_t nw = (strip + 31) / 32;
         std::vector<uint32_t> esc((size_t)2 * S * nw, 0u);
@@ -1183,46 +1252,120 @@ static int sync_units(up_ctx *c) {
             HIPCHK(hipMemcpy(c->d_esc.p, esc.data(), esc.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         c->esc_nw = nw;
     }
+    c->index_on = false;  // the table below carries no pooled count tracks
     HIPCHK(c->d_units.ensure(d.size()));
-    HIPCHK(hipMemcpy(c->d_units.p, d.data(), d.size() * sizeof(UnitDesc), hipMemcpyHostToDevice));
-    // chunk-sum planes of the tracks that changed (after their escape tables:
-    // escaped fields enter at their counts); stream-ordered after the writes
-    bool planes = false;
-    for (size_t i = 0; i < c->units.size(); ++i) {
-        Unit &u = c->units[i];
-        if (!u.cs_dirty) continue;
-        const uint64_t n = u.stride / 4 * (uint64_t)u.nstrands * c->p.n_samples;
-        const unsigned blocks = (unsigned)std::min<uint64_t>((n + 255) / 256, 65536);
-        if (kTB == 2 && n)
-            hipLaunchKernelGGL(csum_kernel, dim3(blocks), dim3(256), 0, c->stream, c->d_units.p, (uint32_t)i,
-                               (int)c->p.n_samples);
-        u.cs_dirty = false;
-        planes = true;
-    }
-    // pooled planes: several pooled tracks (or both strands) screen as one
-    if (kTB == 2 && (c->p.nondir || pool_mode(c) != 0)) {
-        for (size_t i = 0; i < c->units.size(); ++i) {
-            Unit &u = c->units[i];
-            if (!u.pool_dirty) continue;
-            const uint64_t n = u.stride / 4;
-            hipLaunchKernelGGL(pool_kernel, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 65536)), dim3(256), 0,
-                               c->stream, c->d_units.p, (uint32_t)i, (int)c->p.n_samples, (int)c->nc.size(),
-                               c->d_nc.p, c->d_wscreen.p);
-            if (u.d_pct)
-                hipLaunchKernelGGL(pct_kernel, dim3((unsigned)std::min<uint64_t>((n * u.nstrands + 255) / 256, 65536)),
-                                   dim3(256), 0, c->stream, c->d_units.p, (uint32_t)i, (int)c->p.n_samples,
-                                   (int)c->nc.size(), c->d_nc.p);
-            u.pool_dirty = false;
-            planes = true;
-        }
-    }
-    if (planes) {
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(c->stream));
-    }
+    if (!d.empty()) HIPCHK(hipMemcpy(c->d_units.p, d.data(), d.size() * sizeof(UnitDesc), hipMemcpyHostToDevice));
     c->units_dirty = false;
     c->bw_layout = c->p.bw;
     return UP_OK;
+}
+
+// Index policy: whether the next pass uses the per-dataset
+// index -- chunk-sum planes, pooled planes, pooled count tracks, all derived
+// from the packed tracks.  K1w screens on the planes, so it always does.
+static bool want_index(const up_ctx *c) {
+    if (kTB != 2) return false;
+    if (wide_mode(c)) return true;
+    switch (c->index_policy) {
+    case UP_INDEX_ALWAYS: return true;
+    case UP_INDEX_NEVER: return false;
+    default: return c->passes_on_tracks >= 1;  // UP_INDEX_AUTO: from the second pass on
+    }
+}
+
+// build what the index lacks (one launch per kind over every stale unit) and
+// switch the unit table and the passes to it -- or off it
+static int sync_index(up_ctx *c) {
+    const bool want = want_index(c);
+    const bool want_pct = pct_mode(c);
+    const bool pooled = c->p.nondir || pool_mode(c) != 0;
+    bool stale = false;
+    for (const Unit &u : c->units)
+        stale |= u.cs_dirty || (pooled && u.pool_dirty) || (want_pct && !u.d_pct) || (!want_pct && u.d_pct);
+    if (want && stale) {
+        if (busy(c)) settle_in_flight(c);  // (UP_INDEX_AUTO's second pass: the first one ran without it)
+        const int S = c->p.n_samples;
+        std::vector<uint32_t> lc, lp, lt;
+        std::vector<uint64_t> oc{0}, op{0}, ot{0};
+        std::vector<uint8_t *> pt;
+        for (size_t i = 0; i < c->units.size(); ++i) {
+            Unit &u = c->units[i];
+            if (want_pct && !u.d_pct) {
+                HIPCHK(hipMalloc(&u.d_pct, (size_t)u.nstrands * kPerByte * u.stride));
+                u.pool_dirty = true;
+            } else if (!want_pct && u.d_pct) {
+                (void)hipFree(u.d_pct);
+                u.d_pct = nullptr;
+            }
+            if (u.cs_dirty) {
+                lc.push_back((uint32_t)i);
+                oc.push_back(oc.back() + u.stride / 16 * (uint64_t)u.nstrands * S);
+                u.pool_dirty = true;  // (the pooled plane sums the track planes)
+            }
+            if (pooled && u.pool_dirty) {
+                lp.push_back((uint32_t)i);
+                op.push_back(op.back() + u.stride / 16);
+                if (u.d_pct) {
+                    lt.push_back((uint32_t)i);
+                    ot.push_back(ot.back() + u.stride / 4 * (uint64_t)u.nstrands);
+                    pt.push_back(u.d_pct);
+                }
+            }
+        }
+        // one device block of lists: [lc | lp | lt] ids, their prefixes, pct pointers
+        const size_t nid = lc.size() + lp.size() + lt.size(), noff = oc.size() + op.size() + ot.size();
+        std::vector<uint64_t> blob(nid + noff + pt.size());
+        uint32_t *ids = (uint32_t *)blob.data();  // (nid uint32s fit in nid uint64s)
+        std::copy(lc.begin(), lc.end(), ids);
+        std::copy(lp.begin(), lp.end(), ids + lc.size());
+        std::copy(lt.begin(), lt.end(), ids + lc.size() + lp.size());
+        uint64_t *offs = blob.data() + nid;
+        std::copy(oc.begin(), oc.end(), offs);
+        std::copy(op.begin(), op.end(), offs + oc.size());
+        std::copy(ot.begin(), ot.end(), offs + oc.size() + op.size());
+        for (size_t k = 0; k < pt.size(); ++k) blob[nid + noff + k] = (uint64_t)(uintptr_t)pt[k];
+        HIPCHK(c->d_index_lists.ensure(std::max<size_t>(blob.size(), 1)));
+        uint64_t *db = c->d_index_lists.p;
+        HIPCHK(hipMemcpyAsync(db, blob.data(), blob.size() * 8, hipMemcpyHostToDevice, c->stream));
+        const uint32_t *dids = (const uint32_t *)db;
+        const uint64_t *doff = db + nid;
+        auto grid = [](uint64_t items) { return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((items + 255) / 256, 8192))); };
+        if (!lc.empty())
+            hipLaunchKernelGGL(csum_units_kernel, grid(oc.back()), dim3(256), 0, c->stream, c->d_units.p, dids, doff,
+                               (uint32_t)lc.size(), S);
+        if (!lp.empty())
+            hipLaunchKernelGGL(pool_units_kernel, grid(op.back()), dim3(256), 0, c->stream, c->d_units.p,
+                               dids + lc.size(), doff + oc.size(), (uint32_t)lp.size(), S, (int)c->nc.size(),
+                               c->d_nc.p, c->d_wscreen.p);
+        if (!lt.empty())
+            hipLaunchKernelGGL(pct_units_kernel, grid(ot.back()), dim3(256), 0, c->stream, c->d_units.p,
+                               dids + lc.size() + lp.size(), doff + oc.size() + op.size(), (uint32_t)lt.size(), S,
+                               (int)c->nc.size(), c->d_nc.p, (uint8_t *const *)(db + nid + noff));
+        HIPCHK(hipGetLastError());
+        for (Unit &u : c->units) {
+            u.cs_dirty = false;
+            if (pooled) u.pool_dirty = false;
+        }
+        HIPCHK(hipStreamSynchronize(c->stream));  // (the host blob above is freed on return)
+        ++c->index_builds;
+        stale = false;
+    }
+    const bool on = want && !stale;
+    if (on != c->index_on) {
+        if (busy(c)) settle_in_flight(c);  // passes in flight read the unit table
+        for (size_t i = 0; i < c->units.size(); ++i)
+            c->h_units[i].pct = on ? (uint64_t)(uintptr_t)c->units[i].d_pct : 0;
+        if (!c->h_units.empty())
+            HIPCHK(hipMemcpy(c->d_units.p, c->h_units.data(), c->h_units.size() * sizeof(UnitDesc),
+                             hipMemcpyHostToDevice));
+        c->index_on = on;
+    }
+    return UP_OK;
+}
+
+static int sync_units(up_ctx *c) {
+    if (int r = sync_layout(c)) return r;
+    return sync_index(c);
 }
 
 // 0: one non-control sample; 1: several, summed in uint32 window words
@@ -1246,7 +1389,7 @@ static bool pct_mode(const up_ctx *c) {
 }
 
 static bool plane_scan(const up_ctx *c) {
-    return kTB == 2 && (c->p.bw + 64) / 64 <= 4;
+    return kTB == 2 && (c->p.bw + 64) / 64 <= 4 && c->index_on;
 }
 
 static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps, uint32_t ovf_cap) {
@@ -1307,7 +1450,8 @@ static uint32_t resident_blocks(const up_ctx *c, const void *kernel, size_t lds)
 
 template <bool PROF, int MODE>
 static void dispatch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32_t b, uint32_t e) {
-    const size_t lds = MODE == kModeScreen ? kScreenLds : MODE == kModeExact ? kExactLds : kScanLds;
+    constexpr bool kScr = MODE == kModeScreen || MODE == kModeScreenF;
+    const size_t lds = kScr ? kScreenLds : MODE == kModeExact ? kExactLds : kScanLds;
     const void *k = scan_kernel_for(P.bw, pool_mode(c), c->p.nondir != 0, PROF, MODE);
     uint32_t blocks = resident_blocks(c, k, lds);
     if (MODE == kModeExact) {
@@ -1318,7 +1462,7 @@ static void dispatch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32
         // alternating pairs: 4,332 vs 4,214 Gbp/s, UNIPEAK_K1B_PER_CU A/B)
         if (c->k1b_per_cu > 0) blocks = (uint32_t)c->k1b_per_cu * (uint32_t)(c->ncu > 0 ? c->ncu : 256);
     } else {
-        if (MODE == kModeScreen) {
+        if (kScr) {
             // K1a leaves room on every CU for the previous pass's K1b/K3
             // (they overlap it, launch_pass): k1a_per_cu workgroups per CU
             const uint32_t cap = (uint32_t)c->k1a_per_cu * (uint32_t)(c->ncu > 0 ? c->ncu : 256);
@@ -1330,7 +1474,7 @@ static void dispatch_scan(up_ctx *c, hipStream_t st, const ScanParams &P, uint32
         if (blocks == 0) return;
     }
     ScanParams Q = P;
-    if (MODE == kModeScreen) {  // per-wave work-list stash regions (ScanParams::xlist)
+    if (kScr) {  // per-wave work-list stash regions (ScanParams::xlist)
         c->k1a_waves = 4 * blocks;
         c->k1a_xcap = Q.xcap = (e - b + c->k1a_waves - 1) / c->k1a_waves;
     }
@@ -1364,6 +1508,7 @@ static StatParams stat_params(up_ctx *c, up_ctx::Pass &ps) {
     P.out_counts = nullptr;
     P.cap = 0;
     P.qmode = q_mode(c) ? 1 : 0;
+    P.planes = c->index_on ? 1 : 0;
     return P;
 }
 
@@ -1414,14 +1559,20 @@ static bool q11_whole_replay() {
 }
 
 // K1w (wide.hip) for kernels wider than K1's halo: directional units, a
-// threshold > 0, no -w capture (its retirements come from the replay);
+// threshold > 0, no -w capture (its retirements come from the replay), and
+// a window of at most 65,535 cells (bw <= kMaxWideBw): the reference counts
+// the cells add() retires in a UShort (misc/peakcall.cpp:172-177), so from
+// bw 32,768 on a gap of 2bw + 1 or more retires (gap mod 65,536) cells, the
+// rest of the window stays misaligned and a flush leaks into the buffer's
+// next unit -- only the whole-buffer replay models that (emulate.hip);
 // UNIPEAK_WIDE=0: the replay instead
 static bool wide_mode(const up_ctx *c) {
     static const bool on = [] {
         const char *e = getenv("UNIPEAK_WIDE");
         return !(e && *e == '0');
     }();
-    return on && c->p.bw > kMaxBw && kTB == 2 && c->p.region_thr > 0 && !c->p.nondir && !c->prof_capture;
+    return on && c->p.bw > kMaxBw && c->p.bw <= kMaxWideBw && kTB == 2 && c->p.region_thr > 0 && !c->p.nondir &&
+           !c->prof_capture;
 }
 
 static bool replay_mode(const up_ctx *c) {
@@ -2064,7 +2215,10 @@ static int launch_pass(up_ctx *c, int slot) {
             else if (pm == 1) hipLaunchKernelGGL(wide_kernel<1>, dim3(blocks), dim3(64), 0, s1, SP);
             else hipLaunchKernelGGL(wide_kernel<2>, dim3(blocks), dim3(64), 0, s1, SP);
         } else {
-            dispatch_scan<false, kModeScreen>(c, s1, SP, 0, ns);   // K1a: stream + screen
+            // K1a: stream + screen -- the chunk-sum plane when the index is
+            // on, else the 2-bit fields (one-pass cost: no derived data read)
+            if (plane_scan(c) || window_nh(c->p.bw) > 4) dispatch_scan<false, kModeScreen>(c, s1, SP, 0, ns);
+            else dispatch_scan<false, kModeScreenF>(c, s1, SP, 0, ns);
         }
     }
     HIPCHK(hipGetLastError());
@@ -2157,6 +2311,11 @@ static void launcher_drain(up_ctx *c) {
     c->lcv.wait(lk, [&] { return c->lq.empty() && !c->lbusy; });
 }
 
+static void settle_in_flight(up_ctx *c) {
+    launcher_drain(c);
+    sync_all(c);
+}
+
 static void launcher_stop(up_ctx *c) {
     if (!c->launcher.joinable()) return;
     {
@@ -2204,6 +2363,7 @@ int up_run_async(up_ctx *c) {
         return r;
     }
     ++c->seq_launched;
+    ++c->passes_on_tracks;
     return UP_OK;
 }
 
@@ -2420,7 +2580,10 @@ static int run_replay(up_ctx *c, uint64_t *n_regions) {
             const char *e = getenv("UNIPEAK_REPLAY_WHOLE");
             return e && *e == '1';
         }();
-        if (!c->prof_capture && kTB == 2 && !whole) {
+        // (the segmented replay's chains assume a window drained after 2bw + 1
+        // positions without an add: false from bw 32,768 on, where the
+        // reference's UShort retirement count wraps -- wide_mode)
+        if (!c->prof_capture && kTB == 2 && !whole && c->p.bw <= kMaxWideBw) {
             if ((r = replay_segments(c, emu, ecnt, soff, order))) return r;
             c->h_resync.assign(nu, 0);
         } else {
@@ -2479,7 +2642,8 @@ static int q11_finish(up_ctx *c, const std::vector<uint32_t> *heads) {
     c->h_pf_off.assign(nu + 1, 0);
     const unsigned long long *st = c->hp_status[slot].p;
     if (!heads) {  // placed inside the pass
-        c->nreg = st[3] ? st[3] - 1 : 0;
+        // (no unit: no pass ran, and st[3] may still hold an earlier pass's count)
+        c->nreg = (nu && st[3]) ? st[3] - 1 : 0;
         return UP_OK;
     }
     // each unit's K1q records (the placement table without edits)

@@ -41,7 +41,11 @@ constexpr int kChunkBytes = kChunk / kPerByte;    // bytes of one 16-position ch
 constexpr int kPadBytes = 256;      // zero bytes before position 1 and after the domain
 constexpr int kPadPos = kPerByte * kPadBytes;  // the same padding in positions
 constexpr int kStripBytes = kStrip / kPerByte;  // one strip of one track
-constexpr int kMaxBw = 511;         // register-resident halo: NH <= 8 words (wider: the replay)
+constexpr int kMaxBw = 511;         // register-resident halo: NH <= 8 words (wider: K1w or the replay)
+// K1w (wide.hip) and the segmented replay: windows of at most 65,535 cells,
+// i.e. bw <= 32,767 (wider: the reference's UShort retirement count wraps,
+// misc/peakcall.cpp:172-177, and only the whole-buffer replay models it)
+constexpr int kMaxWideBw = 32767;
 // Chunk-sum planes (2-bit tracks): after a unit's tracks, one byte per track
 // per 16-position chunk -- byte j = the tag sum of fields 16j .. 16j+15 (the
 // track's dword j), escaped fields at their overflow counts, saturated at 255
@@ -71,7 +75,10 @@ constexpr int kOvfStride = 6 * kOvfHalf;
 constexpr uint32_t kEsc = kTMask;   // escape field: the count lives in the overflow table
 constexpr int kXEntry = 2 + kWave / 2;  // strip, exact-block mask, 64 x 16-bit chunk masks
 constexpr int kMaxK1aWaves = 16384;     // K1a grid cap (stash regions)
-constexpr int kModeFused = 0, kModeScreen = 1, kModeExact = 2;  // K1 variants
+// K1 variants; kModeScreenF: K1a streaming the 2-bit fields where kModeScreen
+// would stream the chunk-sum plane (a pass without the per-dataset index:
+// DESIGN.md §3 "Index policy")
+constexpr int kModeFused = 0, kModeScreen = 1, kModeExact = 2, kModeScreenF = 3;
 constexpr uint32_t kBig = 1u << 22; // screen value of a chunk holding an escape (4-bit: a count >= 8)
 
 // overflow entries are indexed per block of kOvfBlk positions, so a lookup
@@ -188,6 +195,7 @@ struct StatParams {
     int32_t qmode;        // K1 peaks are Q keys (ScanParams::qmode): K3 scores the peak
     int32_t q11;          // runs of K1q (threshold <= 0): the peak skips the run's first
                           // position (it joined by a leap, peakcall.cpp:76-78)
+    int32_t planes;       // the chunk-sum planes are current (range sums may read them)
 };
 
 }  // namespace upk

@@ -796,17 +796,19 @@ __device__ __forceinline__ bool plane_clean_any(int R, const uint32_t (&a)[16], 
 #ifndef UPK_SCAN_ATTR
 #define UPK_SCAN_ATTR                                                                                   \
     __attribute__((amdgpu_waves_per_eu(MODE == kModeExact ? (NONDIR ? UPK_K1B_WPE_ND : UPK_K1B_WPE) \
-                                       : MODE == kModeScreen ? UPK_K1A_WPE                           \
-                                                             : 1)))
+                                       : (MODE == kModeScreen || MODE == kModeScreenF) ? UPK_K1A_WPE \
+                                                                                       : 1)))
 #endif
 template <int NH, int POOL, bool NONDIR, bool PROF, int MODE>
 __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, uint32_t strip_begin,
                                                    uint32_t strip_end) {
     extern __shared__ double lds_[];
+    // K1a, over the chunk-sum plane (kModeScreen, bw <= 255) or the 2-bit fields
+    constexpr bool kScr = MODE == kModeScreen || MODE == kModeScreenF;
     const int bw = P.bw;
     double *ktab = lds_ + kKPad;
-    if constexpr (MODE != kModeScreen) ktab = load_ktab(lds_, P.kern, bw);
-    uint32_t *scr = (uint32_t *)(MODE == kModeScreen ? lds_ : lds_ + kKTab) + (threadIdx.x >> 6) * kScrWords;
+    if constexpr (!kScr) ktab = load_ktab(lds_, P.kern, bw);
+    uint32_t *scr = (uint32_t *)(kScr ? lds_ : lds_ + kKTab) + (threadIdx.x >> 6) * kScrWords;
     // this wave's block scores (K1b has no screen area)
     double *scs = (MODE == kModeExact ? lds_ + kKTab : (double *)((uint32_t *)(lds_ + kKTab) + 4 * kScrWords)) +
                   (threadIdx.x >> 6) * (kStepWords * kWave);
@@ -912,8 +914,8 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         dh = u32x4{0u, 0u, 0u, 0u};
         if (lane < 2) dh = pl[lane == 0 ? -1 : kPlaneStrip / 16];  // the halos' 16 chunks each side
     };
-    constexpr bool kCheap = MODE == kModeScreen && !PROF && POOL == 0 && !NONDIR && kTB == 2 && kPf && !kPlane;
-    u32x4 pv[MODE == kModeScreen && !PROF ? kLoads : 1];
+    constexpr bool kCheap = kScr && !PROF && POOL == 0 && !NONDIR && kTB == 2 && kPf && !kPlane;
+    u32x4 pv[kScr && !PROF ? kLoads : 1];
     u32x4 phv = {0u, 0u, 0u, 0u};
     uint32_t pf_strip = 0, pf_cur = 0;
     int pf_st = 0, pf_k = 0;
@@ -927,7 +929,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         const int64_t q0 = 1 + (int64_t)(strip_n - Un.strip0) * kStrip;
         gu32x4 *t = (gu32x4 *)(track_u8(Un, S, st, ncs[k]) + fbyte(kPadPos + q0 - 1));
 #pragma unroll
-        for (int q = 0; q < (MODE == kModeScreen && !PROF ? kLoads : 1); ++q)
+        for (int q = 0; q < (kScr && !PROF ? kLoads : 1); ++q)
             pv[q] = __builtin_nontemporal_load(t + 64 * q + lane);
         phv = u32x4{0u, 0u, 0u, 0u};
         if (lane < 2 * HL_) phv = t[lane < HL_ ? lane - HL_ : kLoads * kWave + lane - HL_];
@@ -945,7 +947,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     if constexpr (kPlane) {
         if (it0 < it_end) pf_plane(it0, pv[0], phv);
         if (it0 + 1 < it_end) pf_plane(it0 + 1, pv[1], phv2);
-    } else if constexpr (MODE == kModeScreen && !PROF && kPf) {
+    } else if constexpr (kScr && !PROF && kPf) {
         if (it0 < it_end) pf_issue(it0, find_unit(units, P.nunits, it0), 0, 0);
     }
     for (uint32_t it = it0; it < it_end; it += istep) {
@@ -1196,7 +1198,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             // readlane) plus both halos bounds it.  Background strips -- most
             // of the genome -- end here; the others (and any escaped field,
             // whose count the screen does not know) take the LDS screen below.
-            if constexpr (MODE == kModeScreen) {
+            if constexpr (kScr) {
                 if (!clean && (R + CPL - 1) / CPL <= 2 && !any_esc) {
                     uint32_t T[kLoads];
 #pragma unroll
@@ -1348,7 +1350,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             __builtin_amdgcn_wave_barrier();
             }  // !clean
         }
-        if constexpr (MODE == kModeScreen) {
+        if constexpr (kScr) {
             if (exact_blocks == 0) {  // no run can touch this strip
                 const uint64_t info = ((uint64_t)(local == 0) << 34) | ((uint64_t)(local + 1 == unstrips) << 35);
                 if (lane == 0) P.strip_info[strip] = info;
@@ -1715,7 +1717,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
         atomicAdd(&P.dbg[23], (unsigned long long)dt_q);
     }
 #endif
-    if constexpr (MODE == kModeScreen) {
+    if constexpr (kScr) {
         if (lane == 0) {
             P.xwcount[2 * wave] = xnf;
             P.xwcount[2 * wave + 1] = xnb;
@@ -2057,71 +2059,113 @@ __global__ void __launch_bounds__(kSegBlock) seg_compact_kernel(
     if (xe) { peak_pos[oe] = 0; peak_val[oe] = 0.0; ends[oe++] = (uint32_t)(p0 + kStrip - 1); }
 }
 
-// the chunk-sum planes of one unit's tracks (kernels.h): one thread per
-// chunk (the track's dword j), escaped fields at their overflow counts
-__global__ void __launch_bounds__(256) csum_kernel(const UnitDesc *units, uint32_t unit, int S) {
-    const UnitDesc U = units[unit];
-    const uint64_t nd = U.stride / 4;  // dwords (chunks) per track
-    const uint32_t ntr = (uint32_t)U.nstrands * (uint32_t)S;
-    uint8_t *plane = (uint8_t *)U.base + (uint64_t)ntr * U.stride;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ntr * nd;
+// ---- the per-dataset index (kernels.h: chunk-sum planes, pooled planes,
+// pooled count tracks), built for many units in one launch each.  Work item
+// i of the launch belongs to list entry k with off[k] <= i < off[k + 1]
+// (off: exclusive prefix of the entries' item counts, off[n] = total).
+__device__ __forceinline__ uint32_t list_entry(const uint64_t *off, uint32_t n, uint64_t i) {
+    uint32_t lo = 0, hi = n;  // the last k with off[k] <= i
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// chunk-sum planes: one item per 4 chunks (one 16-byte load of a track, one
+// dword of its plane) of every track of the listed units; escaped fields at
+// their overflow counts, each chunk saturated at 255
+__global__ void __launch_bounds__(256) csum_units_kernel(const UnitDesc *units, const uint32_t *list,
+                                                         const uint64_t *off, uint32_t n, int S) {
+    const uint64_t total = off[n];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t t = (uint32_t)(i / nd);
-        const uint64_t j = i - (uint64_t)t * nd;
-        const uint32_t d = ((const uint32_t *)((const uint8_t *)U.base + (uint64_t)t * U.stride))[j];
-        uint32_t s = fsum32(d, 0u);  // an escaped field counts kEsc here
-        uint32_t e = fbig32(d);
-        while (e && s < 255u) {
-            const int b = __builtin_ctz(e);
-            e &= e - 1u;
-            const int64_t p = (int64_t)(16 * j) + b / kTB - kPadPos + 1;  // the field's position
-            const uint32_t c = ovf_lookup(U, t, (uint32_t)p);
-            s = s - kEsc + (c < 255u ? c : 255u);
+        const uint32_t k = list_entry(off, n, i);
+        const UnitDesc U = units[list[k]];
+        const uint64_t nq = U.stride / 16;  // items per track
+        const uint64_t r = i - off[k];
+        const uint32_t t = (uint32_t)(r / nq);
+        const uint64_t q = r - (uint64_t)t * nq;
+        const uint32_t ntr = (uint32_t)U.nstrands * (uint32_t)S;
+        const u32x4 v = *(const u32x4 *)((const uint8_t *)U.base + (uint64_t)t * U.stride + 16 * q);
+        const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+        uint32_t out = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint32_t sum = fsum32(d[c], 0u);  // an escaped field counts kEsc here
+            uint32_t e = fbig32(d[c]);
+            while (e && sum < 255u) {
+                const int b = __builtin_ctz(e);
+                e &= e - 1u;
+                const int64_t p = (int64_t)(16 * (4 * q + c)) + b / kTB - kPadPos + 1;  // the field's position
+                const uint32_t cnt = ovf_lookup(U, t, (uint32_t)p);
+                sum = sum - kEsc + (cnt < 255u ? cnt : 255u);
+            }
+            out |= (sum < 255u ? sum : 255u) << (8 * c);
         }
-        plane[(uint64_t)t * nd + j] = (uint8_t)(s < 255u ? s : 255u);
+        uint8_t *plane = (uint8_t *)U.base + (uint64_t)ntr * U.stride;
+        *(uint32_t *)(plane + (uint64_t)t * (U.stride / 4) + 4 * q) = out;
     }
 }
 
-// the pooled plane of one unit (kernels.h): per chunk the weighted sum of
-// the non-control samples' planes over the unit's strands, saturated at 255
-__global__ void __launch_bounds__(256) pool_kernel(const UnitDesc *units, uint32_t unit, int S, int nnc,
-                                                   const int32_t *nc, const uint32_t *w) {
-    const UnitDesc U = units[unit];
-    const uint64_t nd = U.stride / 4;
-    const uint8_t *planes = (const uint8_t *)U.base + (uint64_t)U.nstrands * S * U.stride;
-    uint8_t *pooled = (uint8_t *)planes + (uint64_t)U.nstrands * S * nd;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t s = 0;
-        for (int st = 0; st < U.nstrands && s < 255u; ++st)
-            for (int k = 0; k < nnc && s < 255u; ++k)
-                s += w[k] * (uint32_t)planes[((uint64_t)st * S + nc[k]) * nd + j];  // w <= 4096: no wrap
-        pooled[j] = (uint8_t)(s < 255u ? s : 255u);
-    }
-}
-
-// the pooled count track of one unit (UnitDesc::pct): one thread per track
-// dword (16 positions) and strand, the pooled samples' fields summed (escapes
-// at their counts), saturated at 255
-__global__ void __launch_bounds__(256) pct_kernel(const UnitDesc *units, uint32_t unit, int S, int nnc,
-                                                  const int32_t *nc) {
-    const UnitDesc U = units[unit];
-    const uint64_t nd = U.stride / 4;  // dwords per track
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nd * (uint64_t)U.nstrands;
+// pooled planes: one item per 4 chunks of each listed unit -- per chunk the
+// weighted sum of the non-control samples' planes over the unit's strands
+// (w <= 4096: no wrap), saturated at 255
+__global__ void __launch_bounds__(256) pool_units_kernel(const UnitDesc *units, const uint32_t *list,
+                                                         const uint64_t *off, uint32_t n, int S, int nnc,
+                                                         const int32_t *nc, const uint32_t *w) {
+    const uint64_t total = off[n];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const int st = (int)(i / nd);
-        const uint64_t j = i - (uint64_t)st * nd;
+        const uint32_t k = list_entry(off, n, i);
+        const UnitDesc U = units[list[k]];
+        const uint64_t nd = U.stride / 4;  // plane bytes per track
+        const uint64_t q = i - off[k];
+        const uint8_t *planes = (const uint8_t *)U.base + (uint64_t)U.nstrands * S * U.stride;
+        uint32_t s[4] = {0u, 0u, 0u, 0u};
+        for (int st = 0; st < U.nstrands; ++st)
+            for (int j = 0; j < nnc; ++j) {
+                const uint32_t b = *(const uint32_t *)(planes + ((uint64_t)st * S + nc[j]) * nd + 4 * q);
+                if (!b) continue;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint32_t v = s[c] + w[j] * ((b >> (8 * c)) & 0xFFu);
+                    s[c] = v < 255u ? v : 255u;
+                }
+            }
+        uint8_t *pooled = (uint8_t *)planes + (uint64_t)U.nstrands * S * nd;
+        *(uint32_t *)(pooled + 4 * q) = s[0] | (s[1] << 8) | (s[2] << 16) | (s[3] << 24);
+    }
+}
+
+// pooled count tracks (UnitDesc::pct): one item per track dword (16
+// positions) and strand of each listed unit, the pooled samples' fields
+// summed (escapes at their counts), saturated at 255; pct: the unit's
+// allocation (listed units only)
+__global__ void __launch_bounds__(256) pct_units_kernel(const UnitDesc *units, const uint32_t *list,
+                                                        const uint64_t *off, uint32_t n, int S, int nnc,
+                                                        const int32_t *nc, uint8_t *const *pct) {
+    const uint64_t total = off[n];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t k = list_entry(off, n, i);
+        const UnitDesc U = units[list[k]];
+        const uint64_t nd = U.stride / 4;  // dwords per track
+        const uint64_t r = i - off[k];
+        const int st = (int)(r / nd);
+        const uint64_t j = r - (uint64_t)st * nd;
         uint32_t sum[16];
 #pragma unroll
         for (int f = 0; f < 16; ++f) sum[f] = 0;
-        for (int k = 0; k < nnc; ++k) {
-            const uint32_t d = ((const uint32_t *)((const uint8_t *)U.base + ((uint64_t)st * S + nc[k]) * U.stride))[j];
+        for (int m = 0; m < nnc; ++m) {
+            const uint32_t d = ((const uint32_t *)((const uint8_t *)U.base + ((uint64_t)st * S + nc[m]) * U.stride))[j];
             if (!d) continue;
 #pragma unroll
             for (int f = 0; f < 16; ++f) {
                 uint32_t v = (d >> (2 * f)) & 3u;
                 if (v == kEsc) {
                     const int64_t p = (int64_t)(16 * j) + f - kPadPos + 1;
-                    v = ovf_lookup(U, (uint32_t)(st * S + nc[k]), (uint32_t)p);
+                    v = ovf_lookup(U, (uint32_t)(st * S + nc[m]), (uint32_t)p);
                 }
                 sum[f] += v;
             }
@@ -2133,7 +2177,7 @@ __global__ void __launch_bounds__(256) pct_kernel(const UnitDesc *units, uint32_
 #pragma unroll
             for (int b = 0; b < 4; ++b) o[q] |= (sum[4 * q + b] < 255u ? sum[4 * q + b] : 255u) << (8 * b);
         }
-        uint4 *dst = (uint4 *)((uint8_t *)U.pct + (uint64_t)st * (4 * U.stride) + 16 * j);
+        uint4 *dst = (uint4 *)(pct[k] + (uint64_t)st * (4 * U.stride) + 16 * j);
         *dst = make_uint4(o[0], o[1], o[2], o[3]);
     }
 }
@@ -2205,8 +2249,9 @@ __device__ __forceinline__ void region_words(WinT<POOL> (&cs)[2 * NH + 1], uint6
 // sum of one track's counts over positions [left, right]: the chunk-sum plane
 // for whole chunks (a saturated 255 and the two partial chunks at the ends
 // from the track's dword, escapes at their overflow counts)
+// (planes false: the pass runs without the index -- every chunk from its dword)
 __device__ __forceinline__ uint32_t track_range_sum(const UnitDesc &U, int S, int st, int smp, uint32_t left,
-                                                    uint32_t right) {
+                                                    uint32_t right, bool planes) {
     gu32 *tw = (gu32 *)track_u8(U, S, st, smp);
     gu8 *pl = plane_u8(U, S, st, smp);
     const uint32_t track = (uint32_t)(st * S + smp);
@@ -2229,7 +2274,7 @@ __device__ __forceinline__ uint32_t track_range_sum(const UnitDesc &U, int S, in
     uint32_t sum = dsum(j0, (int)(n0 & 15), 15) + dsum(j1, 0, (int)(n1 & 15));
 #pragma unroll 4
     for (int64_t j = j0 + 1; j < j1; ++j) {
-        const uint32_t b = pl[j];
+        const uint32_t b = planes ? (uint32_t)pl[j] : 255u;
         sum += b == 255u ? dsum(j, 0, 15) : b;
     }
     return sum;
@@ -2251,7 +2296,7 @@ __device__ __forceinline__ void nc_range_sums(uint32_t (&esum)[4], const UnitDes
     for (int t = lane; t < nnc * NSTR; t += 64) {
         const int st = t >= nnc ? 1 : 0;
         const int smp = P.nc[t - st * nnc];
-        atomicAdd(&sc[smp], track_range_sum(U, S, st, smp, left, right));
+        atomicAdd(&sc[smp], track_range_sum(U, S, st, smp, left, right, P.planes != 0));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

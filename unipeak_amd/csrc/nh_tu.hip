@@ -20,11 +20,15 @@ constexpr int kNH = UPK_NH_TU;
 template <int POOL, bool ND>
 static const void *scan_ptr(bool prof, int mode) {
     if (prof) return (const void *)scan_kernel<kNH, POOL, ND, true, kModeFused>;
-    return mode == kModeScreen ? (const void *)scan_kernel<kNH, POOL, ND, false, kModeScreen>
-                               : (const void *)scan_kernel<kNH, POOL, ND, false, kModeExact>;
+    if constexpr (kNH <= 4) {  // (wider kernels stream the fields in kModeScreen already)
+        if (mode == kModeScreenF) return (const void *)scan_kernel<kNH, POOL, ND, false, kModeScreenF>;
+    }
+    return mode == kModeExact ? (const void *)scan_kernel<kNH, POOL, ND, false, kModeExact>
+                              : (const void *)scan_kernel<kNH, POOL, ND, false, kModeScreen>;
 }
 
-// K1: the variants the library launches -- K1a (screen), K1b (exact) and the
+// K1: the variants the library launches -- K1a (screen: over the chunk-sum
+// plane or, without the index, the 2-bit fields), K1b (exact) and the
 // profile kernel (PROF, fused) -- for every pool mode and strand layout
 const void *UPK_CAT(scan_kernel_nh, UPK_NH_TU)(int pool, bool nd, bool prof, int mode) {
     if (nd) {

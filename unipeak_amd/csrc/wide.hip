@@ -1,5 +1,8 @@
 // unipeak_amd/csrc/wide.hip -- K1w: the scan for kernels wider than K1's
-// register-resident halo (bw > kMaxBw = 511, up to the UShort 65535 of
+// register-resident halo (bw > kMaxBw = 511, up to kMaxWideBw = 32,767: a
+// window of at most 65,535 cells -- beyond it the reference's UShort
+// retirement count wraps, misc/peakcall.cpp:172-177, and the whole-buffer
+// replay runs instead; the reference's -b itself is a UShort,
 // misc/kernel.hpp:16).  #included by api.hip.
 //
 // One wave per strip (16,384 positions), directional units with a threshold
@@ -18,13 +21,13 @@
 //    K1b);
 //  * runs, peaks (first maximum) and the strip's record list and edge flags
 //    exactly as K1b writes them, so K2 and K3 (known peaks) follow unchanged.
-// The tracks of every unit are padded past len + 65536 (unit_stride), so the
+// The tracks of every unit are padded past len + 2bw (unit_stride), so the
 // window loads of positions up to len + bw stay in bounds.
 
 namespace upk {
 
 constexpr uint32_t kWideSat = 1u << 18;  // a saturated chunk in the prefix sums
-constexpr int kWideChunks = (kStrip + 2 * 65535 + 64) / 16 + 4;  // 9,224: the widest strip window
+constexpr int kWideChunks = (kStrip + 2 * kMaxWideBw + 64) / 16 + 4;  // 5,127: the widest strip window
 
 template <int POOL>
 __global__ void __launch_bounds__(64) wide_kernel(ScanParams P) {
