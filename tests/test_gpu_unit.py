@@ -311,3 +311,40 @@ def test_shift_best_is_first_maximum_of_table(gpu_lib, seed):
                     if tab[k, s] > c:
                         b, c = s, tab[k, s]
                 assert best[k] == b and bc[k] == c, (k, max_shift)
+
+
+@pytest.mark.parametrize("S,nondir", [(300, False), (1024, False), (260, True)])
+def test_many_samples(gpu_lib, oracle, S, nondir):
+    """more than 256 samples (the reference's nExpt_ is a UShort,
+    misc/peakcall.hpp:49): K3 keeps the exptSums beyond 256 in an LDS row per
+    wave; pooled planes, the pooled count track and K1b's batched sample
+    fetch over many tracks; two controls; per-sample counts of every
+    candidate against the oracle.  1,025 samples are refused loudly."""
+    rng = np.random.default_rng(1000 + S)
+    length, bw, bg = 40_000, 50, 0.004
+    control = [0] * S
+    control[7] = control[S - 2] = 1
+    pos_f, cnt_f = random_unit(rng, length, bw, S=S, n_clusters=6, n_bg=40)
+    hit = 10.0 * (S - 2)
+    if not nondir:
+        ref, ref_sums = oracle.run_unit(bw, bg, pos_f, cnt_f, control=control, hit_thr=hit)
+        regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, pos_f, cnt_f, control=control, hit_thr=hit)
+    else:
+        pos_r, cnt_r = random_unit(rng, length, bw, S=S, n_clusters=6, n_bg=40)
+        allp = np.union1d(pos_f, pos_r).astype(np.uint32)
+        cf = np.zeros((allp.size, S), np.uint32)
+        cr = np.zeros((allp.size, S), np.uint32)
+        cf[np.searchsorted(allp, pos_f)] = cnt_f
+        cr[np.searchsorted(allp, pos_r)] = cnt_r
+        ref, ref_sums = oracle.run_unit(bw, bg, allp, cf, cr, nondir=True, control=control, hit_thr=hit,
+                                        corr_thr=0.3)
+        regs, gcnt, *_ = run_gpu(gpu_lib, bw, bg, length, allp, cf, cr, nondir=True, control=control,
+                                 hit_thr=hit, corr_thr=0.3, want_corr=True)
+    assert len(ref) > 0
+    compare(ref, ref_sums, regs, gcnt)
+    if S == 1024:
+        with gpu_lib.Lib(0) as g:
+            g.set_params(bw, 1025, bg)
+            g.add_unit(1000)
+            with pytest.raises(gpu_lib.UpError):
+                g.run()

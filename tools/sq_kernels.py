@@ -15,8 +15,9 @@ def family(name):
     m = re.search(r"scan_kernel<(.*)>", name)
     if m:
         mode = m.group(1).split(",")[-1].strip()
-        return {"1": "K1a", "2": "K1b"}.get(mode, "scan_mode" + mode)
-    for pat, fam in (("stats_kernel", "K3"), ("proc_runs", "K1q"), ("seg_", "K2"), ("xref", "K1x")):
+        return {"1": "K1a", "2": "K1b", "3": "K1a_fields"}.get(mode, "scan_mode" + mode)
+    for pat, fam in (("k1a_fields_kernel", "K1a_fields"), ("stats1_kernel", "K3_one"), ("stats_kernel", "K3"), ("proc_runs", "K1q"), ("seg_", "K2"),
+                     ("xref", "K1x")):
         if pat in name:
             return fam
     return name.split("(")[0][:40]

@@ -1517,7 +1517,8 @@ static void dispatch_stats(up_ctx *c, hipStream_t st, const StatParams &P, uint6
     // (stats1.hip; UNIPEAK_K3_ONE=0 keeps the general kernel, for A/B and tests)
     const bool one = c->k3_one && kTB == 2 && pool_mode(c) == 0 && c->p.nondir == 0 && c->p.n_samples == 1 &&
                      P.peak_pos != nullptr;
-    const size_t lds = one ? kStat1Lds : kStatLds;
+    // (beyond 256 samples one LDS row of exptSums per wave, kernels.hip add_es)
+    const size_t lds = one ? kStat1Lds : kStatLds + (c->p.n_samples > 256 ? 4 * 4 * (size_t)c->p.n_samples : 0);
     const void *k = stats_kernel_for(P.bw, pool_mode(c), c->p.nondir != 0, one);
     uint64_t cap = resident_blocks(c, k, lds);
     if (c->k3_per_cu > 0) cap = std::min<uint64_t>(cap, (uint64_t)c->k3_per_cu * (uint64_t)(c->ncu > 0 ? c->ncu : 256));
@@ -1582,7 +1583,7 @@ static bool replay_mode(const up_ctx *c) {
 static int check_params(up_ctx *c) {
     if (!c || !c->have_params) return UP_E_STATE;
     if (c->p.bw < 1) return UP_E_ARG;
-    if (c->p.n_samples > 256) return UP_E_UNSUPPORTED;
+    if (c->p.n_samples > kMaxSamples) return UP_E_UNSUPPORTED;
     return UP_OK;
 }
 

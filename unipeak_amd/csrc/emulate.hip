@@ -136,7 +136,7 @@ __device__ static bool any_at(const EmuParams &P, uint32_t u, int strand, int s,
 // copies stay identical).  Stores and atomics of a single value go through
 // lane 0.
 struct EmuLds {
-    uint32_t counts[256];   // the current add's counts per sample
+    uint32_t counts[kMaxSamples];  // the current add's counts per sample
     double t0[64], t1[64], t2[64];
 };
 

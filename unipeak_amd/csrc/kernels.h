@@ -46,6 +46,10 @@ constexpr int kMaxBw = 511;         // register-resident halo: NH <= 8 words (wi
 // i.e. bw <= 32,767 (wider: the reference's UShort retirement count wraps,
 // misc/peakcall.cpp:172-177, and only the whole-buffer replay models it)
 constexpr int kMaxWideBw = 32767;
+// samples per context: the reference's nExpt_ is a UShort (misc/peakcall.hpp:49);
+// K3 keeps up to 256 exptSums in registers and up to kMaxSamples in an LDS
+// row per wave, K0 one add's counts per sample in LDS
+constexpr int kMaxSamples = 1024;
 // Chunk-sum planes (2-bit tracks): after a unit's tracks, one byte per track
 // per 16-position chunk -- byte j = the tag sum of fields 16j .. 16j+15 (the
 // track's dword j), escaped fields at their overflow counts, saturated at 255

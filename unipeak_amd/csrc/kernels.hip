@@ -1052,6 +1052,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 #pragma unroll
             for (int i = 0; i < CPL; ++i) hs[i] = 0;
             bool clean = false;
+            bool pre_done = false;  // kCheap's packed pre-screen ran (and failed)
             // the pre-screen bound of every lane: max over its groups of the
             // tags of groups g-D .. g+D, plus both halos (below)
             auto pre_bound = [&](const uint32_t (&T)[kLoads], uint32_t hl) -> uint32_t {
@@ -1096,6 +1097,43 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
                     uint32_t nc_ = cur;
                     while (it + istep >= units[nc_].strip0 + units[nc_].nstrips) ++nc_;
                     pf_issue(it + istep, nc_, 0, 0);
+                }
+                // Packed pre-screen (R <= CPL: a position's window lies in its
+                // 64-position group g and the groups beside it; no escape in
+                // reach, so the fields are the counts): the group sums of the
+                // lane's four loads, capped at 31, as the bytes of one dword;
+                // one DPP rotate each way brings the neighbouring lanes' groups
+                // (lane 0 / 63: the other end of the wave shifted by a byte,
+                // plus the halo group beside the strip), one 32-bit add sums
+                // all four triples (<= 93 per byte, no carry), and a bytewise
+                // compare against wskip + 1 < 32 settles the strip -- about
+                // half the VALU of the chunk sums + per-load DPP bound below,
+                // which then run only for strips that fail here.
+                if (R <= CPL && P.wskip < 31u && !mesc) {
+                    pre_done = true;
+                    uint32_t pk = 0;
+#pragma unroll
+                    for (int q = 0; q < kLoads; ++q) {
+                        uint32_t t = fsum32(v[q].x, 0u);
+                        t = fsum32(v[q].y, t);
+                        t = fsum32(v[q].z, t);
+                        t = fsum32(v[q].w, t);
+                        pk |= (t < 31u ? t : 31u) << (8 * q);
+                    }
+                    uint32_t th = fsum32(hv.x, 0u);  // halo groups (lanes 0 .. 2HL-1)
+                    th = fsum32(hv.y, th);
+                    th = fsum32(hv.z, th);
+                    th = fsum32(hv.w, th);
+                    const uint32_t hl = rl_u(th, HL_ - 1), hr = rl_u(th, HL_);  // the groups beside the strip
+                    uint32_t lw = dpp32<0x13C, 0xf, false>(0u, pk);  // wave_ror:1 -> lane l - 1 (lane 0: 63)
+                    uint32_t rw = dpp32<0x134, 0xf, false>(0u, pk);  // wave_rol:1 -> lane l + 1 (lane 63: 0)
+                    lw = lane == 0 ? (lw << 8) | (hl < 31u ? hl : 31u) : lw;
+                    rw = lane == 63 ? (rw >> 8) | ((hr < 31u ? hr : 31u) << 24) : rw;
+                    const uint32_t sum3 = lw + pk + rw;
+                    const uint32_t k = (P.wskip + 1u) * 0x01010101u;
+                    // (128 + s - k >= 128 exactly when a byte's sum s > wskip)
+                    const bool over = (((sum3 | 0x80808080u) - k) & 0x80808080u) != 0u;
+                    clean = __ballot(over) == 0;
                 }
                 if (!clean) {  // the exact chunk sums of the same registers
 #pragma unroll
@@ -1199,7 +1237,7 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
             // of the genome -- end here; the others (and any escaped field,
             // whose count the screen does not know) take the LDS screen below.
             if constexpr (kScr) {
-                if (!clean && (R + CPL - 1) / CPL <= 2 && !any_esc) {
+                if (!clean && (R + CPL - 1) / CPL <= 2 && !any_esc && !pre_done) {
                     uint32_t T[kLoads];
 #pragma unroll
                     for (int q = 0; q < kLoads; ++q) {
@@ -1725,6 +1763,245 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
     }
 }
 
+// ------------------------------------------------------------------------
+// K1a over the 2-bit fields of ONE pooled directional track (POOL 0), the
+// pass without the per-dataset index (kModeScreenF, DESIGN.md §3 "Index
+// policy") -- configs[1]'s cold pass.  Same outputs as scan_kernel's screen
+// (strip summaries of clean strips, work-list stash entries of the others),
+// built for the stream:
+//  * each wave screens a contiguous run of strips; a cursor walks the unit
+//    table (one scalar load per unit, not per strip), so no load address
+//    waits on a scalar load;
+//  * three strip buffers in rotation (the loop is unrolled by three, each
+//    buffer a fixed set of registers): the loads of strips i+1 and i+2 are
+//    in flight while strip i is screened -- scan_kernel's kCheap path copied
+//    its prefetch buffer each strip, which waited for every load of the wave
+//    (vmcnt(0)) and then for the next strip's unit-table loads before
+//    issuing the next loads: one strip in flight per wave, SQ_WAIT_ANY 60 %
+//    of the wave cycles (profiles/r06/);
+//  * the packed pre-screen (scan_kernel's, R <= 4) settles background
+//    strips; the others take chunk sums, escape bits and the LDS screen.
+template <int NH>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K1A_WPE)))
+k1a_fields_kernel(ScanParams P, uint32_t strip_begin, uint32_t strip_end) {
+    extern __shared__ double lds_[];
+    uint32_t *scr = (uint32_t *)lds_ + (threadIdx.x >> 6) * kScrWords;
+    constexpr int CPL = 16 / kChunkBytes;           // chunks per 16-byte lane load (4)
+    constexpr int kLoads = kStripBytes / (kWave * 16);
+    constexpr int SH = scr_halo(NH);                // screen halo chunks per side (16)
+    constexpr int HL = SH * kChunkBytes / 16;       // halo lane loads per side (4)
+    static_assert(kTB == 2 && CPL == 4 && kChunkBytes == 4 && kLoads == 4, "2-bit layout");
+    const auto *units = cptr(P.units);
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    const int R = (P.bw + kChunk - 1) / kChunk;
+    const int S = P.S;
+    const int nc0 = cptr(P.nc)[0];
+    const uint32_t wskip = P.wskip;
+    const bool packed_ok = R <= CPL && wskip < 31u;
+    const uint32_t nsr = strip_end - strip_begin;
+    const uint32_t per = (nsr + nwaves - 1) / nwaves;
+    const uint32_t off = (uint64_t)wave * per < nsr ? wave * per : nsr;
+    const uint32_t it0 = strip_begin + off;
+    const uint32_t it_end = it0 + per < strip_end ? it0 + per : strip_end;
+    const auto *eb = cptr(P.esc);  // (constant address space: scalar loads)
+    const uint32_t esc_row = (uint32_t)nc0 * P.esc_nw;  // strand 0, the pooled sample
+    uint32_t xnf = 0, xnb = 0;
+
+    struct Buf {
+        u32x4 v[4];
+        u32x4 h;
+    };
+    // prefetch cursor (the unit of the strip being issued)
+    uint32_t pc_u = 0, pc_s0 = 0, pc_end = 0;
+    gu8 *pc_base = nullptr;
+    auto issue = [&](uint32_t strip, Buf &b) {
+        while (strip >= pc_end) {
+            pc_u = pc_end == 0 ? find_unit(units, P.nunits, strip) : pc_u + 1;
+            const UnitDesc Un = units[pc_u];
+            pc_s0 = Un.strip0;
+            pc_end = Un.strip0 + Un.nstrips;
+            pc_base = track_u8(Un, S, 0, nc0) + fbyte(kPadPos);  // position 1
+        }
+        gu32x4 *t = (gu32x4 *)(pc_base + (uint64_t)(strip - pc_s0) * kStripBytes);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b.v[q] = __builtin_nontemporal_load(t + 64 * q + lane);
+        // (every lane loads -- lanes past the halo repeat the right halo's
+        // pieces and drop them -- so no load is under a branch and the
+        // compiler can count the loads still in flight exactly)
+        const u32x4 h = t[lane < HL ? lane - HL : kLoads * kWave + ((lane - HL) & (HL - 1))];
+        b.h = lane < 2 * HL ? h : u32x4{0u, 0u, 0u, 0u};
+    };
+    // current cursor (the unit of the strip being screened)
+    uint32_t c_u = 0, c_s0 = 0, c_end = 0;
+
+    auto screen = [&](uint32_t strip, const Buf &b) {
+        while (strip >= c_end) {
+            c_u = c_end == 0 ? find_unit(units, P.nunits, strip) : c_u + 1;
+            c_s0 = units[c_u].strip0;
+            c_end = c_s0 + units[c_u].nstrips;
+        }
+        const uint32_t local = strip - c_s0, unstrips = c_end - c_s0;
+        // the strip's escape bit (a scalar load: its wait never holds the
+        // vector loads in flight; 32 strips share a word)
+        const uint32_t escw = eb ? eb[esc_row + (strip >> 5)] : ~0u;
+        const bool mesc = (escw >> (strip & 31u)) & 1u;
+        bool clean = false, pre_done = false;
+        if (packed_ok && !mesc) {  // (scan_kernel's packed pre-screen; see there)
+            pre_done = true;
+            uint32_t pk = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t t = fsum32(b.v[q].x, 0u);
+                t = fsum32(b.v[q].y, t);
+                t = fsum32(b.v[q].z, t);
+                t = fsum32(b.v[q].w, t);
+                pk |= (t < 31u ? t : 31u) << (8 * q);
+            }
+            uint32_t th = fsum32(b.h.x, 0u);
+            th = fsum32(b.h.y, th);
+            th = fsum32(b.h.z, th);
+            th = fsum32(b.h.w, th);
+            const uint32_t hl = rl_u(th, HL - 1), hr = rl_u(th, HL);
+            uint32_t lw = dpp32<0x13C, 0xf, false>(0u, pk);  // wave_ror:1
+            uint32_t rw = dpp32<0x134, 0xf, false>(0u, pk);  // wave_rol:1
+            lw = lane == 0 ? (lw << 8) | (hl < 31u ? hl : 31u) : lw;
+            rw = lane == 63 ? (rw >> 8) | ((hr < 31u ? hr : 31u) << 24) : rw;
+            const uint32_t sum3 = lw + pk + rw;
+            const uint32_t k = (wskip + 1u) * 0x01010101u;
+            clean = __ballot((((sum3 | 0x80808080u) - k) & 0x80808080u) != 0u) == 0;
+        }
+        uint32_t mchunk = 0, exact_blocks = 0;
+        if (!clean) {
+            uint32_t cs[16], hs[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t d[4] = {b.v[q].x, b.v[q].y, b.v[q].z, b.v[q].w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cs[4 * q + i] = fsum32(d[i], 0u);
+            }
+            {
+                const uint32_t d[4] = {b.h.x, b.h.y, b.h.z, b.h.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) hs[i] = fsum32(d[i], 0u);
+            }
+            // a chunk holding an escaped field goes exact (one pooled
+            // sample: its escapes sit at peaks that are exact anyway)
+            uint32_t big = 0, hbig = 0;
+            if (mesc) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t d[4] = {b.v[q].x, b.v[q].y, b.v[q].z, b.v[q].w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) big |= (fbig32(d[i]) ? 1u : 0u) << (4 * q + i);
+                }
+                const uint32_t d[4] = {b.h.x, b.h.y, b.h.z, b.h.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) hbig |= (fbig32(d[i]) ? 1u : 0u) << i;
+            }
+            // scan_kernel's register pre-screen over groups g-D .. g+D (D = 2)
+            if (!pre_done && !mesc && (R + CPL - 1) / CPL <= 2) {
+                uint32_t T[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) T[q] = cs[4 * q] + cs[4 * q + 1] + cs[4 * q + 2] + cs[4 * q + 3];
+                const uint32_t hsum = hs[0] + hs[1] + hs[2] + hs[3];
+                uint32_t htot = 0;
+#pragma unroll
+                for (int l = 0; l < 2 * HL; ++l) htot += rl_u(hsum, l);
+                const int D = (R + CPL - 1) / CPL;
+                uint32_t bmax = 0;
+                uint32_t l1[4], r1[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    l1[q] = dpp32<0x138, 0xf, false>(0u, T[q]);
+                    r1[q] = dpp32<0x130, 0xf, false>(0u, T[q]);
+                    const uint32_t lf = q > 0 ? rl_u(T[q > 0 ? q - 1 : 0], 63) : 0u;
+                    const uint32_t rf = q + 1 < 4 ? rl_u(T[q + 1 < 4 ? q + 1 : q], 0) : 0u;
+                    l1[q] = lane == 0 ? lf : l1[q];
+                    r1[q] = lane == 63 ? rf : r1[q];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t bq = T[q] + l1[q] + r1[q];
+                    if (D == 2) {
+                        uint32_t l2 = dpp32<0x138, 0xf, false>(0u, l1[q]);
+                        uint32_t r2 = dpp32<0x130, 0xf, false>(0u, r1[q]);
+                        const uint32_t lf = q > 0 ? rl_u(l1[q > 0 ? q - 1 : 0], 63) : 0u;
+                        const uint32_t rf = q + 1 < 4 ? rl_u(r1[q + 1 < 4 ? q + 1 : q], 0) : 0u;
+                        l2 = lane == 0 ? lf : l2;
+                        r2 = lane == 63 ? rf : r2;
+                        bq += l2 + r2;
+                    }
+                    bmax = bq > bmax ? bq : bmax;
+                }
+                clean = __ballot(bmax + htot > wskip) == 0;
+            }
+            if (!clean) {  // the LDS screen (scan_kernel's layout and screen_any)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t *d = scr + scr_at(kScrHalo + kWave * CPL * q + CPL * lane);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) d[i] = ((big >> (4 * q + i)) & 1u) ? kBig : cs[4 * q + i];
+                }
+                if (lane < 2 * HL) {
+                    uint32_t *d = scr + scr_at(lane < HL ? kScrHalo - SH + CPL * lane
+                                                         : kScrHalo + kBlocks * kWave + CPL * (lane - HL));
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) d[i] = ((hbig >> i) & 1u) ? kBig : hs[i];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t *rd = scr + 17 * lane;  // index 16l + j = word 17l + j + j/16
+                const uint32_t m = screen_any<4 * NH>(R, rd, wskip, P.fw, P.fthr);
+                const uint64_t lanes = __ballot(m != 0u);
+                mchunk = m;
+#pragma unroll
+                for (int bk = 0; bk < kBlocks; ++bk)
+                    exact_blocks |= ((lanes >> (4 * bk)) & 0xFull) ? (1u << bk) : 0u;
+                __builtin_amdgcn_wave_barrier();  // the next strip reuses scr after every lane read it
+            }
+        }
+        if (exact_blocks == 0) {  // no run can touch this strip
+            const uint64_t info = ((uint64_t)(local == 0) << 34) | ((uint64_t)(local + 1 == unstrips) << 35);
+            if (lane == 0) P.strip_info[strip] = info;
+        } else {
+            const bool front = __builtin_popcount(exact_blocks) >= kXFront;
+            const uint32_t slot = wave * P.xcap + (front ? xnf++ : P.xcap - 1u - xnb++);
+            uint32_t *e = P.xlist + (uint64_t)slot * kXEntry;
+            const uint32_t hi = (uint32_t)__shfl_down((int)mchunk, 1);
+            if ((lane & 1) == 0) e[2 + (lane >> 1)] = mchunk | (hi << 16);
+            if (lane == 0) { e[0] = strip; e[1] = exact_blocks | ((c_u < 0xFFFFu ? c_u : 0xFFFFu) << 16); }
+        }
+    };
+
+    // (loads past the run repeat its last strip: unconditional issues keep
+    // the in-flight count exact, so each screen waits for its own buffer only)
+    if (it0 < it_end) {
+        const uint32_t last = it_end - 1;
+        auto cl = [&](uint32_t x) { return x < last ? x : last; };
+        Buf b0, b1, b2;
+        issue(it0, b0);
+        issue(cl(it0 + 1), b1);
+        for (uint32_t it = it0;; it += 3) {
+            issue(cl(it + 2), b2);
+            screen(it, b0);
+            if (it + 1 > last) break;
+            issue(cl(it + 3), b0);
+            screen(it + 1, b1);
+            if (it + 2 > last) break;
+            issue(cl(it + 4), b1);
+            screen(it + 2, b2);
+            if (it + 3 > last) break;
+        }
+    }
+    if (lane == 0) {
+        P.xwcount[2 * wave] = xnf;
+        P.xwcount[2 * wave + 1] = xnb;
+    }
+}
+
 #ifndef UPK_NH_TU  // the per-NH translation units hold only the templated kernels
 // ------------------------------------------------------------------------
 // K1q: the region scan of a threshold <= 0 (quirk Q11 live), parallel.
@@ -2063,13 +2340,19 @@ __global__ void __launch_bounds__(kSegBlock) seg_compact_kernel(
 // pooled count tracks), built for many units in one launch each.  Work item
 // i of the launch belongs to list entry k with off[k] <= i < off[k + 1]
 // (off: exclusive prefix of the entries' item counts, off[n] = total).
-__device__ __forceinline__ uint32_t list_entry(const uint64_t *off, uint32_t n, uint64_t i) {
-    uint32_t lo = 0, hi = n;  // the last k with off[k] <= i
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (off[mid] <= i) lo = mid; else hi = mid;
+// (a grid-stride loop's items only grow: the entry advances from the
+// previous one, a binary search only for the thread's first item)
+__device__ __forceinline__ uint32_t list_entry(const uint64_t *off, uint32_t n, uint64_t i, uint32_t &k) {
+    if (k == ~0u) {
+        uint32_t lo = 0, hi = n;  // the last k with off[k] <= i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (off[mid] <= i) lo = mid; else hi = mid;
+        }
+        k = lo;
     }
-    return lo;
+    while (k + 1 < n && off[k + 1] <= i) ++k;
+    return k;
 }
 
 // chunk-sum planes: one item per 4 chunks (one 16-byte load of a track, one
@@ -2078,9 +2361,10 @@ __device__ __forceinline__ uint32_t list_entry(const uint64_t *off, uint32_t n, 
 __global__ void __launch_bounds__(256) csum_units_kernel(const UnitDesc *units, const uint32_t *list,
                                                          const uint64_t *off, uint32_t n, int S) {
     const uint64_t total = off[n];
+    uint32_t kc = ~0u;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t k = list_entry(off, n, i);
+        const uint32_t k = list_entry(off, n, i, kc);
         const UnitDesc U = units[list[k]];
         const uint64_t nq = U.stride / 16;  // items per track
         const uint64_t r = i - off[k];
@@ -2115,9 +2399,10 @@ __global__ void __launch_bounds__(256) pool_units_kernel(const UnitDesc *units, 
                                                          const uint64_t *off, uint32_t n, int S, int nnc,
                                                          const int32_t *nc, const uint32_t *w) {
     const uint64_t total = off[n];
+    uint32_t kc = ~0u;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t k = list_entry(off, n, i);
+        const uint32_t k = list_entry(off, n, i, kc);
         const UnitDesc U = units[list[k]];
         const uint64_t nd = U.stride / 4;  // plane bytes per track
         const uint64_t q = i - off[k];
@@ -2146,9 +2431,10 @@ __global__ void __launch_bounds__(256) pct_units_kernel(const UnitDesc *units, c
                                                         const uint64_t *off, uint32_t n, int S, int nnc,
                                                         const int32_t *nc, uint8_t *const *pct) {
     const uint64_t total = off[n];
+    uint32_t kc = ~0u;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t k = list_entry(off, n, i);
+        const uint32_t k = list_entry(off, n, i, kc);
         const UnitDesc U = units[list[k]];
         const uint64_t nd = U.stride / 4;  // dwords per track
         const uint64_t r = i - off[k];
@@ -2280,14 +2566,47 @@ __device__ __forceinline__ uint32_t track_range_sum(const UnitDesc &U, int S, in
     return sum;
 }
 
+// exptSums[s] += t (t wave-uniform): up to 256 samples in registers -- lane
+// s % 64, slot s / 64 -- beyond that (esl != null) in the wave's LDS row of
+// S words (the reference's nExpt_ is a UShort, misc/peakcall.hpp:49)
+__device__ __forceinline__ void add_es(uint32_t (&esum)[4], uint32_t *esl, int s, uint32_t t, int lane) {
+    if (esl) {
+        if (lane == 0) esl[s] += t;
+        return;
+    }
+    if (lane == (s & 63)) {
+        const int slot = s >> 6;
+        esum[0] += slot == 0 ? t : 0u;
+        esum[1] += slot == 1 ? t : 0u;
+        esum[2] += slot == 2 ? t : 0u;
+        esum[3] += slot == 3 ? t : 0u;
+    }
+}
+
 // exptSums of the non-control samples over a region: every tag of a
 // non-control sample is a pooled hit, so its exptSum is its track's range
-// sum (one lane per (strand, sample) track; sc: 256 words of the wave's LDS)
+// sum (one lane per (strand, sample) track; sc: 256 words of the wave's LDS,
+// or the wave's exptSums row esl itself beyond 256 samples)
 template <bool NONDIR>
-__device__ __forceinline__ void nc_range_sums(uint32_t (&esum)[4], const UnitDesc &U, const StatParams &P,
-                                              uint32_t left, uint32_t right, int lane, uint32_t *sc) {
+__device__ __forceinline__ void nc_range_sums(uint32_t (&esum)[4], uint32_t *esl, const UnitDesc &U,
+                                              const StatParams &P, uint32_t left, uint32_t right, int lane,
+                                              uint32_t *sc) {
     const int S = P.S, nnc = P.nnc;
     constexpr int NSTR = NONDIR ? 2 : 1;
+    if (esl) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // lane 0's row updates are visible
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int t = lane; t < nnc * NSTR; t += 64) {
+            const int st = t >= nnc ? 1 : 0;
+            const int smp = P.nc[t - st * nnc];
+            atomicAdd(&esl[smp], track_range_sum(U, S, st, smp, left, right, P.planes != 0));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        return;
+    }
     __builtin_amdgcn_wave_barrier();  // earlier readers of the area are done
     for (int i = lane; i < S; i += 64) sc[i] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2334,7 +2653,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
     uint64_t wm[2 * NH + 1];
 #pragma unroll
     for (int d = -NH; d <= NH; ++d) wm[d + NH] = win_mask(d, bw);
-    const int S = P.S;  // <= 256 (checked by the host)
+    const int S = P.S;  // <= kMaxSamples (checked by the host)
+    // exptSums beyond 256 samples: one row of S words per wave after the
+    // terms areas (dynamic LDS sized by the host, dispatch_stats)
+    uint32_t *esl = S > 256 ? (uint32_t *)((double2 *)((uint32_t *)(lds_ + kKTab) + 4 * kStatCache * 64) + 4 * 64) +
+                                  (threadIdx.x >> 6) * S
+                            : nullptr;
     // several samples, integer pooling: the non-control samples' exptSums are
     // range sums of their chunk-sum planes (nc_range_sums), the pooled count
     // of a hit is the window word's own value
@@ -2376,7 +2700,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
         const uint64_t rn = ri + nwaves;
         const uint32_t dsc_n = rn < nreg ? desc_load(rn) : 0u;
         const UnitDesc U = P.units[u];
-        uint32_t esum[4] = {0, 0, 0, 0};  // exptSums[s] lives in lane s%64, slot s/64
+        uint32_t esum[4] = {0, 0, 0, 0};  // exptSums[s] lives in lane s%64, slot s/64 (or esl)
+        if (esl) {
+            __builtin_amdgcn_wave_barrier();  // the previous region's reads are done
+            for (int i = lane; i < S; i += 64) esl[i] = 0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         uint32_t esum1 = 0;               // S == 1: lane-local partial of exptSums[0]
 
         uint32_t cnt_acc = 0, sum_acc = 0;
@@ -2559,13 +2890,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                         if constexpr (NONDIR) c += h1 ? fld(S + s) : 0u;
                         pc += c;
                         const uint32_t t = wave_sum_u32(c);
-                        if (lane == (s & 63)) {
-                            const int slot = s >> 6;
-                            esum[0] += slot == 0 ? t : 0u;
-                            esum[1] += slot == 1 ? t : 0u;
-                            esum[2] += slot == 2 ? t : 0u;
-                            esum[3] += slot == 3 ? t : 0u;
-                        }
+                        add_es(esum, esl, s, t, lane);
                     }
                     if (blk < kStatCache) pcache[64 * blk + lane] = pc;
                     cnt_acc += pc;
@@ -2602,13 +2927,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                         if (h1) c += count_at(U, S, 1, s, x);
                         pc += c;
                         const uint32_t t = wave_sum_u32(c);
-                        if (lane == (s & 63)) {
-                            const int slot = s >> 6;
-                            esum[0] += slot == 0 ? t : 0u;
-                            esum[1] += slot == 1 ? t : 0u;
-                            esum[2] += slot == 2 ? t : 0u;
-                            esum[3] += slot == 3 ? t : 0u;
-                        }
+                        add_es(esum, esl, s, t, lane);
                     }
                 } else {
                     for (int s = 0; s < S; ++s) {
@@ -2617,13 +2936,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                         if (h1) c += count_at(U, S, 1, s, x);
                         pc += c;
                         const uint32_t t = wave_sum_u32(c);
-                        if (lane == (s & 63)) {
-                            const int slot = s >> 6;
-                            esum[0] += slot == 0 ? t : 0u;
-                            esum[1] += slot == 1 ? t : 0u;
-                            esum[2] += slot == 2 ? t : 0u;
-                            esum[3] += slot == 3 ? t : 0u;
-                        }
+                        add_es(esum, esl, s, t, lane);
                     }
                 }
                 if (blk < kStatCache) pcache[64 * blk + lane] = pc;
@@ -2775,13 +3088,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                     }
                     pc += c;
                     const uint32_t t = wave_sum_u32(c);
-                    if (lane == (s & 63)) {
-                        const int slot = s >> 6;
-                        esum[0] += slot == 0 ? t : 0u;
-                        esum[1] += slot == 1 ? t : 0u;
-                        esum[2] += slot == 2 ? t : 0u;
-                        esum[3] += slot == 3 ? t : 0u;
-                    }
+                    add_es(esum, esl, s, t, lane);
                 }
             } else {
                 for (int s = 0; s < S; ++s) {
@@ -2792,13 +3099,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                     }
                     pc += c;
                     const uint32_t t = wave_sum_u32(c);
-                    if (lane == (s & 63)) {
-                        const int slot = s >> 6;
-                        esum[0] += slot == 0 ? t : 0u;
-                        esum[1] += slot == 1 ? t : 0u;
-                        esum[2] += slot == 2 ? t : 0u;
-                        esum[3] += slot == 3 ? t : 0u;
-                    }
+                    add_es(esum, esl, s, t, lane);
                 }
             }
             if (blk < kStatCache) pcache[64 * blk + lane] = pc;
@@ -2816,7 +3117,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
             }
         }
         }  // !kn
-        if (kRS && S > 1 && !staged) nc_range_sums<NONDIR>(esum, U, P, left, right, lane, (uint32_t *)terms);
+        if (kRS && S > 1 && !staged) nc_range_sums<NONDIR>(esum, esl, U, P, left, right, lane, (uint32_t *)terms);
         if (POOL == 0 && S == 1) {
             const uint32_t t = wave_sum_u32(esum1);
             esum[0] = lane == 0 ? t : 0u;
@@ -2975,12 +3276,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
         // ---- processRegion filters (peakcall.cpp:33-53) ----
         // exptSums: lane s % 64 holds sample s (slot s / 64); one coalesced row
         uint32_t nc_part = 0;
+        if (esl) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int s = lane; s < S; s += 64) {
+                const uint32_t v = esl[s];
+                if (!P.is_control[s]) nc_part += v;
+                P.out_counts[ri * S + s] = v;
+            }
+        } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int s = 64 * q + lane;
-            if (s < S) {
-                if (!P.is_control[s]) nc_part += esum[q];
-                P.out_counts[ri * S + s] = esum[q];
+            for (int q = 0; q < 4; ++q) {
+                const int s = 64 * q + lane;
+                if (s < S) {
+                    if (!P.is_control[s]) nc_part += esum[q];
+                    P.out_counts[ri * S + s] = esum[q];
+                }
             }
         }
         const uint32_t nonctl = wave_sum_u32(nc_part);  // HitCount sum (wraps like the reference)

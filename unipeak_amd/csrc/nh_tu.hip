@@ -21,7 +21,10 @@ template <int POOL, bool ND>
 static const void *scan_ptr(bool prof, int mode) {
     if (prof) return (const void *)scan_kernel<kNH, POOL, ND, true, kModeFused>;
     if constexpr (kNH <= 4) {  // (wider kernels stream the fields in kModeScreen already)
-        if (mode == kModeScreenF) return (const void *)scan_kernel<kNH, POOL, ND, false, kModeScreenF>;
+        if (mode == kModeScreenF) {
+            if constexpr (POOL == 0 && !ND) return (const void *)k1a_fields_kernel<kNH>;  // one track
+            return (const void *)scan_kernel<kNH, POOL, ND, false, kModeScreenF>;
+        }
     }
     return mode == kModeExact ? (const void *)scan_kernel<kNH, POOL, ND, false, kModeExact>
                               : (const void *)scan_kernel<kNH, POOL, ND, false, kModeScreen>;
