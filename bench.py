@@ -578,7 +578,8 @@ def main():
     if pipelined:
         g.set_record_target(nr.my_slot_address(it[0]), cap)
     g.set_timing(0)
-    for tag, pol in (("no_index", capi.INDEX_NEVER), ("index_built_in_pass", capi.INDEX_ALWAYS)):
+    for tag, pol in ((("no_index", capi.INDEX_NEVER), ("index_built_in_pass", capi.INDEX_ALWAYS))
+                     if os.environ.get("UNIPEAK_BENCH_SINGLE", "1") != "0" else ()):
         g.set_index_policy(pol)
         ts = []
         for _ in range(5):
@@ -683,7 +684,7 @@ def main():
                          "regions": {"candidates": int((Lg["final"] or (0, 0))[0]),
                                      "accepted": int((Lg["final"] or (0, 0))[1])}}
         res["single_pass_ms"] = {k: {"median": round(float(np.median(v)), 4), "runs": [round(x, 4) for x in v]}
-                                 for k, v in single.items()}
+                                 for k, v in single.items()} or None
         res["single_pass_note"] = ("one blocking up_run on an idle GPU, first launch -> records in host memory, "
                                    "median of 5; no_index: the headline's cold pass; index_built_in_pass: "
                                    "up_invalidate_index, then a pass that builds the planes/pooled tracks first")

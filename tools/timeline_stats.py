@@ -28,9 +28,12 @@ def main():
     rows.sort()
 
     def short(n):
+        if "k1a_fields_kernel" in n:
+            return "K1a"
         if "scan_kernel" in n:
-            return "K1a" if n.split(">")[0].endswith(", 1") else ("K1b" if n.split(">")[0].endswith(", 2") else "K1?")
-        for k, v in (("stats_kernel", "K3"), ("seg_count", "K2a"), ("seg_compact", "K2b"), ("xref", "K1x"),
+            m = n.split(">")[0]
+            return "K1a" if (m.endswith(", 1") or m.endswith(", 3")) else ("K1b" if m.endswith(", 2") else "K1?")
+        for k, v in (("stats1_kernel", "K3"), ("stats_kernel", "K3"), ("seg_count", "K2a"), ("seg_compact", "K2b"), ("xref", "K1x"),
                      ("emulate", "K0"), ("head", "K0h"), ("fillBuffer", "fill"), ("copyBuffer", "copy")):
             if k in n:
                 return v

@@ -36,14 +36,14 @@ const void *scan_kernel_nh5(int, bool, bool, int);
 const void *scan_kernel_nh6(int, bool, bool, int);
 const void *scan_kernel_nh7(int, bool, bool, int);
 const void *scan_kernel_nh8(int, bool, bool, int);
-const void *stats_kernel_nh1(int, bool, bool);
-const void *stats_kernel_nh2(int, bool, bool);
-const void *stats_kernel_nh3(int, bool, bool);
-const void *stats_kernel_nh4(int, bool, bool);
-const void *stats_kernel_nh5(int, bool, bool);
-const void *stats_kernel_nh6(int, bool, bool);
-const void *stats_kernel_nh7(int, bool, bool);
-const void *stats_kernel_nh8(int, bool, bool);
+const void *stats_kernel_nh1(int, bool, int);
+const void *stats_kernel_nh2(int, bool, int);
+const void *stats_kernel_nh3(int, bool, int);
+const void *stats_kernel_nh4(int, bool, int);
+const void *stats_kernel_nh5(int, bool, int);
+const void *stats_kernel_nh6(int, bool, int);
+const void *stats_kernel_nh7(int, bool, int);
+const void *stats_kernel_nh8(int, bool, int);
 const void *shift_kernel_nh1(int);
 const void *shift_kernel_nh2(int);
 const void *shift_kernel_nh3(int);
@@ -66,7 +66,7 @@ static const void *scan_kernel_for(int bw, int pool, bool nd, bool prof, int mod
     default: return scan_kernel_nh8(pool, nd, prof, mode);
     }
 }
-static const void *stats_kernel_for(int bw, int pool, bool nd, bool one) {
+static const void *stats_kernel_for(int bw, int pool, bool nd, int one) {
     switch (window_nh(bw)) {
     case 1: return stats_kernel_nh1(pool, nd, one);
     case 2: return stats_kernel_nh2(pool, nd, one);
@@ -1517,12 +1517,21 @@ static void dispatch_stats(up_ctx *c, hipStream_t st, const StatParams &P, uint6
     // (stats1.hip; UNIPEAK_K3_ONE=0 keeps the general kernel, for A/B and tests)
     const bool one = c->k3_one && kTB == 2 && pool_mode(c) == 0 && c->p.nondir == 0 && c->p.n_samples == 1 &&
                      P.peak_pos != nullptr;
+    // one: a lane per region (stats1L_kernel, round 6; UNIPEAK_K3_LANE=0: a
+    // wave per region, stats1_kernel)
+    static const bool lane_k3 = [] {
+        const char *e = getenv("UNIPEAK_K3_LANE");
+        return !(e && *e == '0');
+    }();
+    const int kind = one ? (lane_k3 ? 2 : 1) : 0;
     // (beyond 256 samples one LDS row of exptSums per wave, kernels.hip add_es)
-    const size_t lds = one ? kStat1Lds : kStatLds + (c->p.n_samples > 256 ? 4 * 4 * (size_t)c->p.n_samples : 0);
-    const void *k = stats_kernel_for(P.bw, pool_mode(c), c->p.nondir != 0, one);
+    const size_t lds = kind == 2 ? kStat1LLds : kind == 1 ? kStat1Lds
+                                                          : kStatLds + (c->p.n_samples > 256 ? 4 * 4 * (size_t)c->p.n_samples : 0);
+    const void *k = stats_kernel_for(P.bw, pool_mode(c), c->p.nondir != 0, kind);
     uint64_t cap = resident_blocks(c, k, lds);
     if (c->k3_per_cu > 0) cap = std::min<uint64_t>(cap, (uint64_t)c->k3_per_cu * (uint64_t)(c->ncu > 0 ? c->ncu : 256));
-    const uint64_t blocks = std::min<uint64_t>((nreg + 3) / 4, cap);
+    // (a lane per region: 256 regions per block; the kernels grid-stride past the estimate)
+    const uint64_t blocks = std::min<uint64_t>(kind == 2 ? (nreg + 255) / 256 : (nreg + 3) / 4, cap);
     if (blocks == 0) return;
     StatParams Q = P;
     void *args[] = {&Q};

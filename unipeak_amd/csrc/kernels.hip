@@ -787,11 +787,17 @@ __device__ __forceinline__ bool plane_clean_any(int R, const uint32_t (&a)[16], 
 #ifndef UPK_K1A_WPE
 #define UPK_K1A_WPE 1
 #endif
+// Round 6: directional K1b at 4 waves per SIMD (<= 128 VGPRs; one pooled
+// sample: 7 spilled VGPRs, several: none) -- the cold pass's K1a holds 120
+// VGPRs, so three K1a waves left no room for a 168-VGPR K1b wave on their
+// SIMD; same box, three alternating rounds of the cold configs[1] leg:
+// 6,919 / 6,957 / 6,922 -> 7,219 / 7,170 / 7,193 Gbp/s (profiles/r06/ab_k1b4.txt).
+// Nondirectional K1b stays at 3 (29-61 spilled VGPRs at 128).
 #ifndef UPK_K1B_WPE
-#define UPK_K1B_WPE 3
+#define UPK_K1B_WPE 4
 #endif
 #ifndef UPK_K1B_WPE_ND
-#define UPK_K1B_WPE_ND UPK_K1B_WPE
+#define UPK_K1B_WPE_ND 3
 #endif
 #ifndef UPK_SCAN_ATTR
 #define UPK_SCAN_ATTR                                                                                   \
@@ -1781,6 +1787,9 @@ __global__ void __launch_bounds__(256) UPK_SCAN_ATTR scan_kernel(ScanParams P, u
 //    of the wave cycles (profiles/r06/);
 //  * the packed pre-screen (scan_kernel's, R <= 4) settles background
 //    strips; the others take chunk sums, escape bits and the LDS screen.
+#ifndef UPK_K1AF_DEPTH
+#define UPK_K1AF_DEPTH 3  // strip buffers in rotation (2 or 3)
+#endif
 template <int NH>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K1A_WPE)))
 k1a_fields_kernel(ScanParams P, uint32_t strip_begin, uint32_t strip_end) {
@@ -1978,9 +1987,22 @@ k1a_fields_kernel(ScanParams P, uint32_t strip_begin, uint32_t strip_end) {
 
     // (loads past the run repeat its last strip: unconditional issues keep
     // the in-flight count exact, so each screen waits for its own buffer only)
+    // (UPK_K1AF_DEPTH 2: one strip in flight beside the screened one)
     if (it0 < it_end) {
         const uint32_t last = it_end - 1;
         auto cl = [&](uint32_t x) { return x < last ? x : last; };
+#if UPK_K1AF_DEPTH == 2
+        Buf b0, b1;
+        issue(it0, b0);
+        for (uint32_t it = it0;; it += 2) {
+            issue(cl(it + 1), b1);
+            screen(it, b0);
+            if (it + 1 > last) break;
+            issue(cl(it + 2), b0);
+            screen(it + 1, b1);
+            if (it + 2 > last) break;
+        }
+#else
         Buf b0, b1, b2;
         issue(it0, b0);
         issue(cl(it0 + 1), b1);
@@ -1995,6 +2017,7 @@ k1a_fields_kernel(ScanParams P, uint32_t strip_begin, uint32_t strip_end) {
             screen(it + 2, b2);
             if (it + 3 > last) break;
         }
+#endif
     }
     if (lane == 0) {
         P.xwcount[2 * wave] = xnf;

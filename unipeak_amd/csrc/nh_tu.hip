@@ -44,8 +44,10 @@ const void *UPK_CAT(scan_kernel_nh, UPK_NH_TU)(int pool, bool nd, bool prof, int
     return scan_ptr<2, false>(prof, mode);
 }
 
-// K3 (one: one pooled directional sample with K1b's peaks, stats1.hip)
-const void *UPK_CAT(stats_kernel_nh, UPK_NH_TU)(int pool, bool nd, bool one) {
+// K3 (one: one pooled directional sample with K1b's peaks, stats1.hip --
+// 1: a wave per region, 2: a lane per region)
+const void *UPK_CAT(stats_kernel_nh, UPK_NH_TU)(int pool, bool nd, int one) {
+    if (one == 2) return (const void *)stats1L_kernel<kNH>;
     if (one) return (const void *)stats1_kernel<kNH>;
     if (nd) {
         if (pool == 0) return (const void *)stats_kernel<kNH, 0, true>;

@@ -353,3 +353,204 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
 }
 
 }  // namespace upk
+
+namespace upk {
+
+// ------------------------------------------------------------------------
+// K3L: the same statistics with ONE LANE PER REGION (round 6).  A region of
+// configs[1] holds ~245 positions and ~20 hits: stats1_kernel's wave spent
+// ~15 us per region in dependent loads and wave-wide bookkeeping for a
+// handful of terms, 8 regions in turn per wave, on every pass's chain
+// stream.  Here each lane walks its own region's 2-bit dwords (fields in
+// ascending position: ctz over the nonzero fields), so pass 1 (exptSums,
+// count, position moments with the Q8 uint16 offsets), pass 2 (the two
+// kurtosis sums in position order, data.cpp:164-182, powi semantics) and the
+// peak score (the reference's ordered sum over the peak's window,
+// peakcall.cpp:203-209) are plain sequential loops with the same FP64
+// operations in the same order as stats1_kernel's.  Regions whose Q-key peak
+// is tied (+0.5) get the wave's KDE afterwards, one at a time.  Records are
+// staged in LDS and written as contiguous wave stores.
+constexpr int kK3LRecWords = 7;  // 56-byte up_region as uint64 words
+constexpr size_t kStat1LLds = kKTab * sizeof(double) + 4 * 64 * kK3LRecWords * sizeof(uint64_t);
+
+template <int NH>
+__global__ void __launch_bounds__(256) stats1L_kernel(StatParams P) {
+    extern __shared__ double lds_[];
+    const int bw = P.bw;
+    const double *ktab = load_ktab(lds_, P.kern, bw);
+    uint64_t *rstage = (uint64_t *)(lds_ + kKTab) + (threadIdx.x >> 6) * 64 * kK3LRecWords;
+    constexpr int NWT = 2 * NH + 1;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    const uint64_t nreg = *P.nreg < P.cap ? *P.nreg : P.cap;
+    uint64_t wm[NWT];
+#pragma unroll
+    for (int d = -NH; d <= NH; ++d) wm[d + NH] = win_mask(d, bw);
+    const int nc0 = P.nc[0];
+    const uint32_t trk = (uint32_t)nc0;
+    const bool ctl0 = P.is_control[0] != 0;
+
+    for (uint64_t base = (uint64_t)wave * 64; base < nreg; base += (uint64_t)nwaves * 64) {
+        const uint64_t ri = base + (uint64_t)lane;
+        const bool live = ri < nreg;
+        const uint64_t rq = live ? ri : base;  // (lanes past the end shadow the wave's first region)
+        const uint32_t left = P.starts[rq], right = P.ends[rq], u = P.reg_unit[rq];
+        uint32_t kpos = P.peak_pos[rq];
+        double kval = P.peak_val[rq];
+        const UnitDesc U = P.units[u];
+        gu32 *tw = (gu32 *)((gu8 *)U.base + (uint64_t)nc0 * U.stride);
+        if (kpos == 0) {  // the run crossed a strip edge: its parts, in position order
+            const uint32_t sa = U.strip0 + (left - 1) / kStrip, sb = U.strip0 + (right - 1) / kStrip;
+            for (uint32_t s = sa; s <= sb; ++s) {
+                const uint32_t sp0 = 1 + (s - U.strip0) * kStrip;
+                const bool prt = (s > sa || left == sp0) && s == sb && right < sp0 + kStrip - 1;
+                const uint64_t *e = P.spk + 4ull * s + (prt ? 0 : 2);
+                const double v = __longlong_as_double((long long)e[0]);
+                if (P.qmode) {
+                    const double fv = __builtin_floor(v), fk = __builtin_floor(kval);
+                    if (s == sa || fv > fk) {
+                        kval = v;
+                        kpos = (uint32_t)e[1];
+                    } else if (fv == fk) {
+                        kval = fk + 0.5;
+                    }
+                } else if (s == sa || v > kval) {
+                    kval = v;
+                    kpos = (uint32_t)e[1];
+                }
+            }
+        }
+        const bool kn = !(P.qmode && kval != __builtin_floor(kval));
+        // fields of dword j restricted to positions [left, right]
+        const int64_t n0 = kPadPos + (int64_t)left - 1, n1 = kPadPos + (int64_t)right - 1;
+        const int64_t j0 = n0 >> 4, j1 = n1 >> 4;
+        auto dword_at = [&](int64_t j) -> uint32_t {
+            uint32_t d = tw[j];
+            if (j == j0) d &= ~0u << (2 * (n0 & 15));
+            if (j == j1 && (n1 & 15) != 15) d &= (1u << (2 * ((n1 & 15) + 1))) - 1u;
+            return d;
+        };
+        // every hit (position, count) of the region in ascending position
+        // (a version with the region's dwords loaded into registers up front
+        // measured slower: 107 VGPRs, same isolated time -- the walks are
+        // bound by their divergent field loops, not by the loads)
+        auto walk = [&](auto &&visit) {
+            for (int64_t j = j0; j <= j1; ++j) {
+                uint32_t d = dword_at(j);
+                while (d) {
+                    const int b = __builtin_ctz(d) & ~1;  // the field's low bit
+                    uint32_t c = (d >> b) & 3u;
+                    d &= ~(3u << b);
+                    const int64_t pos = 16 * j + b / 2 - kPadPos + 1;
+                    if (c == kEsc) c = ovf_lookup(U, trk, (uint32_t)pos);
+                    visit((uint32_t)pos, c);
+                }
+            }
+        };
+        uint32_t count = 0, psum = 0;
+        if (live)
+            walk([&](uint32_t pos, uint32_t c) {
+                count += c;
+                psum += c * (uint32_t)(uint16_t)(pos - left);  // Q8: uint16 offsets
+            });
+        const double x_bar = (double)psum / (double)count;
+        double sum2 = 0.0, sum4 = 0.0;
+        if (live)
+            walk([&](uint32_t pos, uint32_t c) {
+                const double d = (double)(uint16_t)(pos - left) - x_bar;
+                const double d2 = d * d;
+                sum2 = sum2 + (double)c * d2;
+                sum4 = sum4 + (double)c * (d2 * d2);
+            });
+        const double kurt = ((double)count - 1) * sum4 / (sum2 * sum2);
+        double best = kval;
+        int64_t best_x = kpos;
+        if (live && kn && P.qmode) {
+            // score(kpos): the hit at kpos - bw + t adds kernel[2bw - t] *
+            // countSum, in ascending t (positions outside the contig read 0)
+            const int64_t p0 = (int64_t)kpos - bw, p1 = (int64_t)kpos + bw;
+            const int64_t a0 = kPadPos + p0 - 1, a1 = kPadPos + p1 - 1;
+            double f = 0.0;
+            for (int64_t j = a0 >> 4; j <= (a1 >> 4); ++j) {
+                uint32_t d = tw[j];
+                if (j == (a0 >> 4)) d &= ~0u << (2 * (a0 & 15));
+                if (j == (a1 >> 4) && (a1 & 15) != 15) d &= (1u << (2 * ((a1 & 15) + 1))) - 1u;
+                while (d) {
+                    const int b = __builtin_ctz(d) & ~1;
+                    uint32_t c = (d >> b) & 3u;
+                    d &= ~(3u << b);
+                    const int64_t pos = 16 * j + b / 2 - kPadPos + 1;
+                    if (c == kEsc) c = ovf_lookup(U, trk, (uint32_t)pos);
+                    f = f + ktab[2 * bw - (int)(pos - p0)] * (double)c;
+                }
+            }
+            best = f;
+        }
+        // tied Q keys: the region's KDE, first maximum of the FP64 scores
+        // (Region::addPos, data.cpp:98-101) -- the wave, one region at a time
+        uint64_t tied = __ballot(live && !kn);
+        while (tied) {
+            const int l = __builtin_ctzll(tied);
+            tied &= tied - 1;
+            const uint32_t tl = rl_u(left, l), tr = rl_u(right, l), tu = rl_u(u, l);
+            const UnitDesc Ut = P.units[tu];
+            double tb = 0.0;
+            int64_t tx = -1;
+            for (int64_t x0 = tl; x0 <= (int64_t)tr; x0 += 64) {
+                const int64_t x = x0 + lane;
+                uint32_t cf[NWT];
+                uint64_t hf[NWT];
+                load_words<NWT, 0>(cf, Ut, 1, 0, x0 - 64 * NH, lane, 1, P.nc, nullptr);
+#pragma unroll
+                for (int w = 0; w < NWT; ++w) hf[w] = __ballot(cf[w] != 0u);
+                const double f = kde_word<NWT, NH, NH>(cf, hf, wm, lane, bw, ktab);
+                if (x <= (int64_t)tr && (tx < 0 || f > tb)) {
+                    tb = f;
+                    tx = x;
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const double ob = __shfl_xor(tb, o);
+                const long long ox = __shfl_xor((long long)tx, o);
+                if (ox >= 0 && (tx < 0 || ob > tb || (ob == tb && ox < tx))) {
+                    tb = ob;
+                    tx = ox;
+                }
+            }
+            if (lane == l) {
+                best = tb;
+                best_x = tx;
+            }
+        }
+        // processRegion filters (peakcall.cpp:33-53); strandCorr is NaN
+        const uint32_t nonctl = ctl0 ? 0u : count;  // S == 1
+        const uint32_t n = right - left + 1;
+        bool acc = (double)nonctl >= P.hit_thr;
+        if (acc) acc = P.kurt_thr == 0 || (n > 1 && kurt <= P.kurt_thr);
+        if (acc) acc = P.corr_thr <= -1;
+        if (live) {
+            P.out_counts[ri] = count;  // exptSums[0]
+            uint64_t *r = rstage + (uint64_t)lane * kK3LRecWords;
+            r[0] = (uint64_t)u | ((uint64_t)left << 32);
+            r[1] = (uint64_t)right | ((uint64_t)(uint32_t)best_x << 32);
+            r[2] = (uint64_t)count | ((uint64_t)nonctl << 32);
+            r[3] = (uint64_t)(uint32_t)(acc ? 1 : 0) | ((uint64_t)UP_CLOSE_RULE << 32);
+            r[4] = (uint64_t)__double_as_longlong(best);
+            r[5] = (uint64_t)__double_as_longlong(kurt);
+            r[6] = (uint64_t)__double_as_longlong(__builtin_nan(""));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the wave's records as one contiguous area: 8-byte lane stores, 512
+        // bytes per instruction (a caller's record target is 8-byte aligned)
+        const uint32_t nw = (uint32_t)((nreg - base < 64 ? nreg - base : 64) * kK3LRecWords);
+        uint64_t *dst = (uint64_t *)P.out + base * kK3LRecWords;
+        for (uint32_t q = (uint32_t)lane; q < nw; q += 64) dst[q] = rstage[q];
+        __builtin_amdgcn_wave_barrier();  // rstage reused
+    }
+}
+
+}  // namespace upk
