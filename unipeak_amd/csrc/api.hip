@@ -1523,7 +1523,16 @@ static void dispatch_stats(up_ctx *c, hipStream_t st, const StatParams &P, uint6
         const char *e = getenv("UNIPEAK_K3_LANE");
         return !(e && *e == '0');
     }();
-    const int kind = one ? (lane_k3 ? 2 : 1) : 0;
+    // K3L's time is its slowest lane's region (escaped counts resolved one
+    // by one at a large peak), whatever the region count: with many regions
+    // its few waves leave the overlapping K1a/K1b more of the GPU (configs[1]
+    // N = 1: 0.4304 / 0.4294 vs 0.4531 / 0.4356 ms per step), with the few of
+    // an 8-GPU rank's shard (~5,200) the wave-per-region kernel finishes
+    // sooner (simulated rank 4: 0.0779 / 0.0777 vs 0.1339 / 0.1322 ms;
+    // profiles/r06/ab_k3.txt) -- the pass's estimate of its region count
+    // (the last pass's) picks
+    constexpr uint64_t kK3LaneMin = 16384;
+    const int kind = one ? ((lane_k3 && nreg >= kK3LaneMin) ? 2 : 1) : 0;
     // (beyond 256 samples one LDS row of exptSums per wave, kernels.hip add_es)
     const size_t lds = kind == 2 ? kStat1LLds : kind == 1 ? kStat1Lds
                                                           : kStatLds + (c->p.n_samples > 256 ? 4 * 4 * (size_t)c->p.n_samples : 0);
