@@ -5,8 +5,12 @@ index, zlib sections) and must hold exactly the intervals and float32 values
 of the wiggle input (clipped at the chromosome ends), and the printed track
 headers must be the script's.  Host-only: runs on CPU.
 
+Zoom levels are checked against a restatement of wigToBigWig's summary
+algorithm (bbiAddRangeToSummary: bins that start at a run's first item,
+items split across bin edges, sums in double stored as float).
+
 Parity note: wigToBigWig is not in this image, so the files are checked for
-content, not bytes (its section sizes and zoom levels are its own)."""
+content, not bytes (its section sizes and its choice of levels are its own)."""
 import os
 import re
 import struct
@@ -85,7 +89,59 @@ def read_bigwig(path):
                 e = s + span
                 p += 4
             out.setdefault(chroms[cid][0], []).append((s, e, v))
-    return out, chroms
+    # zoom levels: headers after the 64-byte header, records through each R-tree
+    zl = []
+    for z in range(zooms):
+        red, _, zdata, zindex = struct.unpack_from("<IIQQ", b, 64 + 24 * z)
+        zm, zbs, zitems = struct.unpack_from("<IIQ", b, zindex)
+        assert zm == 0x2468ACE0
+        count, = struct.unpack_from("<I", b, zdata)
+        zblocks = []
+
+        def walk_z(off):
+            leaf, _, cnt = struct.unpack_from("<BBH", b, off)
+            off += 4
+            for _ in range(cnt):
+                if leaf:
+                    zblocks.append(struct.unpack_from("<IIIIQQ", b, off))
+                    off += 32
+                else:
+                    walk_z(struct.unpack_from("<IIIIQ", b, off)[4])
+                    off += 24
+        walk_z(zindex + 48)
+        recs = []
+        for c0, s0, c1, s1, doff, dsize in zblocks:
+            raw = zlib.decompress(b[doff:doff + dsize])
+            assert len(raw) <= ubuf and len(raw) % 32 == 0
+            for k in range(len(raw) // 32):
+                r = struct.unpack_from("<IIIIffff", raw, 32 * k)
+                assert r[0] == c0 == c1 and s0 <= r[1] and r[2] <= s1
+                recs.append(r)
+        assert len(recs) == count
+        zl.append((red, recs))
+    return out, chroms, zl
+
+
+def summarise(items_by_cid, csize, red):
+    """wigToBigWig's zoom records (bbiAddRangeToSummary), restated"""
+    out = []
+    for cid in sorted(items_by_cid):
+        cur = None
+        for s, e, v in items_by_cid[cid]:
+            e = min(e, csize[cid])
+            while s < e:
+                if cur is None or cur[2] <= s:
+                    st = s if (cur is None or cur[2] + red <= s) else cur[2]
+                    cur = [cid, st, min(st + red, csize[cid]), 0, v, v, 0.0, 0.0]
+                    out.append(cur)
+                ov = min(e, cur[2]) - max(s, cur[1])
+                cur[3] += ov
+                cur[4] = min(cur[4], v)
+                cur[5] = max(cur[5], v)
+                cur[6] += v * ov
+                cur[7] += v * v * ov
+                s += ov
+    return out
 
 
 def expected(path, sizes):
@@ -141,11 +197,31 @@ def test_wigs2bigwigs_roundtrip(tmp_path):
     assert hdr[0].endswith(" bigDataUrl=http://h/p+.bw") and hdr[1].endswith(" bigDataUrl=http://h/p-.bw")
     want = expected(tmp_path / "p.wig", sizes)
     for strand, items in want:
-        got, chroms = read_bigwig(tmp_path / f"p{strand}.bw")
+        got, chroms, zl = read_bigwig(tmp_path / f"p{strand}.bw")
         assert {v[0]: v[1] for v in chroms.values()} == {c: sizes[c] for c in items}
         assert set(got) == set(items)
         for c in items:
             assert got[c] == items[c], c
+        # zoom levels: 10x the average item span, then 4x per level, each
+        # with fewer records than the one before; every record as restated
+        cid = {name: i for i, (name, _) in chroms.items()}
+        by_cid = {cid[c]: v for c, v in items.items()}
+        csize = {i: L for i, (_, L) in chroms.items()}
+        n = sum(len(v) for v in items.values())
+        span = sum(e - s for v in items.values() for s, e, _ in v)
+        assert len(zl) >= 3
+        assert zl[0][0] == max(1, (span + n // 2) // n) * 10
+        prev = n
+        for k, (red, recs) in enumerate(zl):
+            if k:
+                assert red == 4 * zl[k - 1][0]
+            ref = summarise(by_cid, csize, red)
+            assert len(recs) == len(ref) < prev
+            prev = len(recs)
+            for r, q in zip(recs, ref):
+                assert r[:4] == tuple(q[:4]) and r[4] == q[4] and r[5] == q[5]
+                assert r[6] == np.float32(q[6]) and r[7] == np.float32(q[7])
+            assert sum(r[3] for r in recs) == span
 
 
 def test_wigs2bigwigs_errors(tmp_path):

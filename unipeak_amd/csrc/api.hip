@@ -1431,7 +1431,7 @@ static ScanParams scan_params(up_ctx *c, up_ctx::Pass &ps, uint32_t ovf_cap) {
 // exactly this many: a larger grid leaves its last workgroups waiting for a
 // slot and finishing their share of the work list after everyone else (a
 // tail of up to one whole per-workgroup share).
-static uint32_t resident_blocks(const up_ctx *c, const void *kernel, size_t lds) {
+static uint32_t resident_blocks(const up_ctx *c, const void *kernel, size_t lds, int threads = 256) {
     static std::mutex mu;
     static std::map<std::pair<const void *, size_t>, int> per_cu;
     int n = 0;
@@ -1441,7 +1441,7 @@ static uint32_t resident_blocks(const up_ctx *c, const void *kernel, size_t lds)
         if (it != per_cu.end()) {
             n = it->second;
         } else {
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, 256, lds) != hipSuccess || n < 1) n = 1;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, threads, lds) != hipSuccess || n < 1) n = 1;
             per_cu[{kernel, lds}] = n;
         }
     }
@@ -1519,9 +1519,10 @@ static void dispatch_stats(up_ctx *c, hipStream_t st, const StatParams &P, uint6
                      P.peak_pos != nullptr;
     // one: a lane per region (stats1L_kernel, round 6; UNIPEAK_K3_LANE=0: a
     // wave per region, stats1_kernel)
-    static const bool lane_k3 = [] {
+    // (UNIPEAK_K3_LANE=2: a lane per region whatever the count, for A/B)
+    static const int lane_k3 = [] {
         const char *e = getenv("UNIPEAK_K3_LANE");
-        return !(e && *e == '0');
+        return e && *e ? atoi(e) : 1;
     }();
     // K3L's time is its slowest lane's region (escaped counts resolved one
     // by one at a large peak), whatever the region count: with many regions
@@ -1532,19 +1533,19 @@ static void dispatch_stats(up_ctx *c, hipStream_t st, const StatParams &P, uint6
     // profiles/r06/ab_k3.txt) -- the pass's estimate of its region count
     // (the last pass's) picks
     constexpr uint64_t kK3LaneMin = 16384;
-    const int kind = one ? ((lane_k3 && nreg >= kK3LaneMin) ? 2 : 1) : 0;
+    const int kind = one ? ((lane_k3 == 2 || (lane_k3 == 1 && nreg >= kK3LaneMin)) ? 2 : 1) : 0;
     // (beyond 256 samples one LDS row of exptSums per wave, kernels.hip add_es)
     const size_t lds = kind == 2 ? kStat1LLds : kind == 1 ? kStat1Lds
                                                           : kStatLds + (c->p.n_samples > 256 ? 4 * 4 * (size_t)c->p.n_samples : 0);
     const void *k = stats_kernel_for(P.bw, pool_mode(c), c->p.nondir != 0, kind);
-    uint64_t cap = resident_blocks(c, k, lds);
+    uint64_t cap = resident_blocks(c, k, lds, kind == 2 ? kK3LThreads : 256);
     if (c->k3_per_cu > 0) cap = std::min<uint64_t>(cap, (uint64_t)c->k3_per_cu * (uint64_t)(c->ncu > 0 ? c->ncu : 256));
     // (a lane per region: 256 regions per block; the kernels grid-stride past the estimate)
-    const uint64_t blocks = std::min<uint64_t>(kind == 2 ? (nreg + 255) / 256 : (nreg + 3) / 4, cap);
+    const uint64_t blocks = std::min<uint64_t>(kind == 2 ? (nreg + kK3LThreads - 1) / kK3LThreads : (nreg + 3) / 4, cap);
     if (blocks == 0) return;
     StatParams Q = P;
     void *args[] = {&Q};
-    (void)hipLaunchKernel(k, dim3((unsigned)blocks), dim3(256), args, lds, st);
+    (void)hipLaunchKernel(k, dim3((unsigned)blocks), dim3(kind == 2 ? kK3LThreads : 256), args, lds, st);
 }
 
 // Configurations the parallel scan does not represent run through the

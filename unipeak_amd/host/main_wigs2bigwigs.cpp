@@ -3,8 +3,8 @@
 // bigWig file per track, with the track headers to load them printed on
 // stdout.  The script pipes each track into UCSC wigToBigWig -clip; this
 // writes the bigWig itself (BBI version 4: chromosome B+ tree, zlib-compressed
-// varStep sections of up to 1024 items, R-tree index), so the pipeline needs
-// no external tool.
+// varStep sections of up to 1024 items, R-tree index, and zoom levels as
+// wigToBigWig builds them), so the pipeline needs no external tool.
 //
 // Script behaviour kept (extras/wigs2bigwigs.pl:42-75): output root = input
 // name minus /.gz$/ or /.bz2$/ then /.wig$/; '#' lines skipped; a track line
@@ -142,6 +142,51 @@ void write_rtree(std::string &f, const std::vector<Block> &blocks, uint32_t bloc
     }
 }
 
+// one zoom-level record (bbiSummaryOnDisk): the bases of one bin that hold
+// data, and their value statistics
+struct Summary {
+    uint32_t chrom, start, end, valid;
+    float vmin, vmax;
+    double sum, sumsq;  // (double in memory, float on disk, as bbiSummary)
+};
+
+// the summaries of one zoom level as wigToBigWig builds them
+// (bbiAddRangeToSummary): bins of `reduction` bases that start at the first
+// item of a run (or continue the previous bin), items split across bin
+// edges, clipped at the chromosome's end
+std::vector<Summary> summarise(const std::vector<std::vector<Item>> &items, const std::vector<uint32_t> &csize,
+                               uint32_t reduction) {
+    std::vector<Summary> out;
+    for (uint32_t ci = 0; ci < items.size(); ++ci) {
+        bool have = false;
+        for (const Item &it : items[ci]) {
+            uint32_t start = it.start;
+            const uint32_t end = std::min(it.end, csize[ci]);
+            while (start < end) {
+                Summary *sm = have ? &out.back() : nullptr;
+                if (!sm || sm->end <= start) {
+                    Summary n{};
+                    n.chrom = ci;
+                    n.start = (!sm || (uint64_t)sm->end + reduction <= start) ? start : sm->end;
+                    n.end = (uint32_t)std::min<uint64_t>((uint64_t)n.start + reduction, csize[ci]);
+                    n.vmin = n.vmax = it.value;
+                    out.push_back(n);
+                    have = true;
+                    sm = &out.back();
+                }
+                const uint32_t ov = std::min(end, sm->end) - std::max(start, sm->start);
+                sm->valid += ov;
+                sm->vmin = std::min(sm->vmin, it.value);
+                sm->vmax = std::max(sm->vmax, it.value);
+                sm->sum += (double)it.value * ov;
+                sm->sumsq += (double)it.value * it.value * ov;
+                start += ov;
+            }
+        }
+    }
+    return out;
+}
+
 void write_bigwig(const Track &t, const std::map<std::string, uint32_t> &sizes) {
     // chromosome ids in name order (the B+ tree's key order)
     std::vector<std::string> names;
@@ -149,7 +194,32 @@ void write_bigwig(const Track &t, const std::map<std::string, uint32_t> &sizes) 
     std::sort(names.begin(), names.end());
     size_t key_size = 1;
     for (const std::string &n : names) key_size = std::max(key_size, n.size());
-    std::string f(64, '\0');  // header, patched at the end
+    std::vector<std::vector<Item>> sorted(names.size());
+    std::vector<uint32_t> csize(names.size());
+    uint64_t nitems = 0, bases = 0;
+    for (size_t ci = 0; ci < names.size(); ++ci) {
+        sorted[ci] = t.by.at(names[ci]);
+        std::stable_sort(sorted[ci].begin(), sorted[ci].end(),
+                         [](const Item &a, const Item &b) { return a.start < b.start; });
+        csize[ci] = sizes.at(names[ci]);
+        for (const Item &it : sorted[ci]) bases += it.end - it.start;
+        nitems += sorted[ci].size();
+    }
+    // zoom levels (wigToBigWig: up to 10, each 4x the previous, the first
+    // 10x the average item span): a level is kept while it has fewer
+    // summaries than the level before it (and than the items themselves)
+    std::vector<std::pair<uint32_t, std::vector<Summary>>> zooms;
+    if (nitems) {
+        uint64_t red = std::max<uint64_t>(1, (bases + nitems / 2) / nitems) * 10;
+        size_t prev = nitems;
+        for (int z = 0; z < 10 && red < 0xFFFFFFFFull; ++z, red *= 4) {
+            std::vector<Summary> sm = summarise(sorted, csize, (uint32_t)red);
+            if (sm.empty() || sm.size() >= prev) break;
+            prev = sm.size();
+            zooms.emplace_back((uint32_t)red, std::move(sm));
+        }
+    }
+    std::string f(64 + 24 * zooms.size(), '\0');  // header and zoom headers, patched at the end
     const uint64_t summary_off = f.size();
     f.append(40, '\0');
     const uint64_t tree_off = f.size();
@@ -179,8 +249,7 @@ void write_bigwig(const Track &t, const std::map<std::string, uint32_t> &sizes) 
     uint64_t valid = 0;
     double vmin = INFINITY, vmax = -INFINITY, vsum = 0, vsq = 0;
     for (uint32_t ci = 0; ci < nchrom; ++ci) {
-        std::vector<Item> items = t.by.at(names[ci]);
-        std::stable_sort(items.begin(), items.end(), [](const Item &a, const Item &b) { return a.start < b.start; });
+        const std::vector<Item> &items = sorted[ci];
         for (size_t i = 0; i < items.size();) {
             // a section: consecutive items with the same span, <= 1024
             const uint32_t span = items[i].end - items[i].start;
@@ -219,12 +288,48 @@ void write_bigwig(const Track &t, const std::map<std::string, uint32_t> &sizes) 
     set64(f, data_off, blocks.size());
     const uint64_t index_off = f.size();
     write_rtree(f, blocks, 256, 1024);
+    // zoom levels: per level a uint32 record count, zlib blocks of up to 1024
+    // summaries (one chromosome each), their R-tree
+    std::vector<std::pair<uint64_t, uint64_t>> zoff;  // data, index
+    for (const auto &zl : zooms) {
+        const std::vector<Summary> &sm = zl.second;
+        const uint64_t zdata = f.size();
+        put32(f, (uint32_t)sm.size());
+        std::vector<Block> zb;
+        for (size_t i = 0; i < sm.size();) {
+            size_t j = i;
+            while (j < sm.size() && j - i < 1024 && sm[j].chrom == sm[i].chrom) ++j;
+            std::string raw;
+            for (size_t k = i; k < j; ++k) {
+                put32(raw, sm[k].chrom);
+                put32(raw, sm[k].start);
+                put32(raw, sm[k].end);
+                put32(raw, sm[k].valid);
+                putf(raw, sm[k].vmin);
+                putf(raw, sm[k].vmax);
+                putf(raw, (float)sm[k].sum);
+                putf(raw, (float)sm[k].sumsq);
+            }
+            max_raw = std::max<uint32_t>(max_raw, (uint32_t)raw.size());
+            uLongf clen = compressBound(raw.size());
+            std::string comp(clen, '\0');
+            if (compress2((Bytef *)&comp[0], &clen, (const Bytef *)raw.data(), raw.size(), 6) != Z_OK)
+                die("error: compression failed\n");
+            comp.resize(clen);
+            zb.push_back(Block{sm[i].chrom, sm[i].start, sm[j - 1].end, f.size(), clen});
+            f += comp;
+            i = j;
+        }
+        const uint64_t zindex = f.size();
+        write_rtree(f, zb, 256, 1024);
+        zoff.emplace_back(zdata, zindex);
+    }
     put32(f, 0x888FFC26u);  // trailing magic
-    // header and total summary
+    // header, zoom headers and total summary
     std::string h;
     put32(h, 0x888FFC26u);
     put16(h, 4);
-    put16(h, 0);  // zoom levels: none (readers summarise the full data)
+    put16(h, (uint16_t)zooms.size());
     put64(h, tree_off);
     put64(h, data_off);
     put64(h, index_off);
@@ -234,7 +339,13 @@ void write_bigwig(const Track &t, const std::map<std::string, uint32_t> &sizes) 
     put64(h, summary_off);
     put32(h, max_raw);
     put64(h, 0);
-    std::memcpy(&f[0], h.data(), 64);
+    for (size_t z = 0; z < zooms.size(); ++z) {
+        put32(h, zooms[z].first);
+        put32(h, 0);
+        put64(h, zoff[z].first);
+        put64(h, zoff[z].second);
+    }
+    std::memcpy(&f[0], h.data(), h.size());
     std::string s;
     put64(s, valid);
     putd(s, valid ? vmin : 0);
