@@ -1509,6 +1509,11 @@ static StatParams stat_params(up_ctx *c, up_ctx::Pass &ps) {
     P.cap = 0;
     P.qmode = q_mode(c) ? 1 : 0;
     P.planes = c->index_on ? 1 : 0;
+    static const int k3l_cut = [] {
+        const char *e = getenv("UNIPEAK_K3L_CUT");
+        return e && *e ? atoi(e) : 0;
+    }();
+    P.cut = k3l_cut;
     return P;
 }
 

@@ -200,6 +200,7 @@ struct StatParams {
     int32_t q11;          // runs of K1q (threshold <= 0): the peak skips the run's first
                           // position (it joined by a leap, peakcall.cpp:76-78)
     int32_t planes;       // the chunk-sum planes are current (range sums may read them)
+    int32_t cut;          // measurement aid (UNIPEAK_K3L_CUT): K3L stops after phase `cut` (wrong records)
 };
 
 }  // namespace upk

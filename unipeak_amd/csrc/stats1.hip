@@ -433,6 +433,7 @@ __global__ void __launch_bounds__(kK3LThreads) stats1L_kernel(StatParams P) {
             }
         }
         const bool kn = !(P.qmode && kval != __builtin_floor(kval));
+        if (P.cut == 1) continue;  // (measurement aid: descriptors only)
         // fields of dword j restricted to positions [left, right]
         const int64_t n0 = kPadPos + (int64_t)left - 1, n1 = kPadPos + (int64_t)right - 1;
         const int64_t j0 = n0 >> 4, j1 = n1 >> 4;
@@ -516,6 +517,7 @@ __global__ void __launch_bounds__(kK3LThreads) stats1L_kernel(StatParams P) {
                 for (int64_t c0 = j0; c0 <= j1; c0 += kK3LRow) hits(stage(c0, j1, n0, n1), c0);
             }
         };
+        if (P.cut == 2) continue;  // (+ staging)
         uint32_t count = 0, psum = 0;
         if (live)
             walk(false, [&](uint32_t pos, uint32_t c) {
@@ -532,6 +534,8 @@ __global__ void __launch_bounds__(kK3LThreads) stats1L_kernel(StatParams P) {
                 sum4 = sum4 + (double)c * (d2 * d2);
             });
         const double kurt = ((double)count - 1) * sum4 / (sum2 * sum2);
+        if (P.cut == 3 && count == 12345u) P.out_counts[0] = (uint32_t)kurt;  // (+ both walks; keep them live)
+        if (P.cut == 3) continue;
         double best = kval;
         int64_t best_x = kpos;
         if (live && kn && P.qmode) {
@@ -563,6 +567,8 @@ __global__ void __launch_bounds__(kK3LThreads) stats1L_kernel(StatParams P) {
             }
             best = f;
         }
+        if (P.cut == 4 && count == 12345u) P.out_counts[0] = (uint32_t)best;  // (+ the peak's window)
+        if (P.cut == 4) continue;
         // tied Q keys: the region's KDE, first maximum of the FP64 scores
         // (Region::addPos, data.cpp:98-101) -- the wave, one region at a time
         uint64_t tied = __ballot(live && !kn);
@@ -600,6 +606,7 @@ __global__ void __launch_bounds__(kK3LThreads) stats1L_kernel(StatParams P) {
                 best_x = tx;
             }
         }
+        if (P.cut == 5) continue;  // (+ the tied regions' KDE)
         // processRegion filters (peakcall.cpp:33-53); strandCorr is NaN
         const uint32_t nonctl = ctl0 ? 0u : count;  // S == 1
         const uint32_t n = right - left + 1;
