@@ -1,0 +1,14 @@
+#!/bin/bash
+# K3L with the popcount first pass: parity (forced on), cut 3 / full isolated K3, A/B vs stats1
+set -o pipefail
+T=${1:-r6m}
+R=$GRAFT_REPO_ROOT
+mkdir -p gpurun_out/$T
+UNIPEAK_K3_LANE=2 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_keys.py tests/test_gpu_unit.py tests/test_gpu_k3.py tests/test_quirks.py tests/test_gpu_genome.py tests/test_gpu_tracks.py > gpurun_out/$T/pytest.log 2>&1 || { tail -40 gpurun_out/$T/pytest.log; exit 1; }
+tail -2 gpurun_out/$T/pytest.log
+for cut in 3 0; do
+  UNIPEAK_K3_LANE=2 UNIPEAK_K3L_CUT=$cut UNIPEAK_BENCH_LEGS=cold UNIPEAK_BENCH_SINGLE=0 timeout -k 10 200 python $R/bench.py --steps 10 --no-cpu-baseline > gpurun_out/$T/cut_$cut.json 2> gpurun_out/$T/cut_$cut.err || exit 1
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('cut', sys.argv[2], d['roofline']['isolated_ms'])" gpurun_out/$T/cut_$cut.json $cut
+done
+E="UNIPEAK_BENCH_LEGS=cold UNIPEAK_BENCH_SINGLE=0"
+REPS=2 tools/ab.sh "base|$E UNIPEAK_K3_LANE=2" "base|$E UNIPEAK_K3_LANE=0" | sed 's/UNIPEAK_BENCH_LEGS=cold UNIPEAK_BENCH_SINGLE=0//'

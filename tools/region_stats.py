@@ -31,3 +31,12 @@ print("regions", n, "len mean", ln.mean(), "p50", np.percentile(ln, 50), "p99", 
 print("words per region p99", np.percentile((ln + 63) // 64, 99), "max", ((ln + 63) // 64).max())
 print("timings", g.timings())
 g.close()
+cnt = c[:, 0].astype(np.int64)
+m = (len(cnt) + 63) // 64
+pad = np.zeros(m * 64, np.int64)
+pad[:len(cnt)] = cnt
+g = pad.reshape(m, 64)
+print("count per region mean", cnt.mean(), "p99", np.percentile(cnt, 99), "max", cnt.max())
+print("per 64-region wave: max count mean", g.max(1).mean(), "p50", np.percentile(g.max(1), 50),
+      "p99", np.percentile(g.max(1), 99), "max", g.max(1).max(), "; waves with a region > 48 tags",
+      int((g.max(1) > 48).sum()), "of", m, "; regions > 48 tags", int((cnt > 48).sum()))

@@ -1514,6 +1514,11 @@ static StatParams stat_params(up_ctx *c, up_ctx::Pass &ps) {
         return e && *e ? atoi(e) : 0;
     }();
     P.cut = k3l_cut;
+    static const int k3l_heavy = [] {
+        const char *e = getenv("UNIPEAK_K3L_HEAVY");
+        return e && *e ? atoi(e) : kK3LHeavy;
+    }();
+    P.heavy = k3l_heavy;
     return P;
 }
 

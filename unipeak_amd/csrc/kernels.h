@@ -50,6 +50,9 @@ constexpr int kMaxWideBw = 32767;
 // K3 keeps up to 256 exptSums in registers and up to kMaxSamples in an LDS
 // row per wave, K0 one add's counts per sample in LDS
 constexpr int kMaxSamples = 1024;
+// K3L (one lane per region): a region with more hits than this sums its
+// kurtosis terms with the whole wave instead of its lane (stats1.hip)
+constexpr int kK3LHeavy = 512;
 // Chunk-sum planes (2-bit tracks): after a unit's tracks, one byte per track
 // per 16-position chunk -- byte j = the tag sum of fields 16j .. 16j+15 (the
 // track's dword j), escaped fields at their overflow counts, saturated at 255
@@ -201,6 +204,7 @@ struct StatParams {
                           // position (it joined by a leap, peakcall.cpp:76-78)
     int32_t planes;       // the chunk-sum planes are current (range sums may read them)
     int32_t cut;          // measurement aid (UNIPEAK_K3L_CUT): K3L stops after phase `cut` (wrong records)
+    int32_t heavy;        // K3L: regions with more hits take the wave's kurtosis path (UNIPEAK_K3L_HEAVY)
 };
 
 }  // namespace upk

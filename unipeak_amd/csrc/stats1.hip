@@ -372,7 +372,7 @@ namespace upk {
 // staged in LDS and written as contiguous wave stores.
 constexpr int kK3LRecWords = 7;  // 56-byte up_region as uint64 words
 constexpr int kK3LRow = 32;      // region dwords staged per lane at a time (512 positions)
-constexpr int kK3LEsc = 16;      // escaped counts cached per lane (bytes)
+constexpr int kK3LEsc = 64;      // escaped counts cached per lane (bytes)
 constexpr int kK3LRowStride = kK3LRow + 1;  // (odd: the lanes' k-th words fall in distinct banks)
 constexpr int kK3LThreads = 128; // two waves per block (the per-lane LDS rows)
 constexpr size_t kStat1LLds = kKTab * sizeof(double) + (kK3LThreads / 64) * 64 * kK3LRecWords * sizeof(uint64_t) +
@@ -518,21 +518,206 @@ __global__ void __launch_bounds__(kK3LThreads) stats1L_kernel(StatParams P) {
             }
         };
         if (P.cut == 2) continue;  // (+ staging)
-        uint32_t count = 0, psum = 0;
-        if (live)
+        uint32_t count = 0, psum = 0, nh = 0;  // nh: hits (the second walk's iterations)
+        if (live && right - left < 65536u) {
+            // no offset wraps (Q8): each dword's count and position moment
+            // from popcounts -- sum_f v_f and sum_f f * v_f over its 16
+            // fields, the field index's bit q selected by kFb[q] -- so this
+            // pass costs dwords, not hits (uint32 arithmetic: exact mod 2^32
+            // like the reference's).  Escaped fields hold 3: the true count
+            // replaces it, and is cached for the second walk.
+            constexpr uint32_t kLo = 0x55555555u;
+            constexpr uint32_t kFb[4] = {0x44444444u, 0x50505050u, 0x55005500u, 0x55550000u};
+            uint32_t ne = 0;
+            // the escape tiles of the region's first two overflow blocks (a
+            // staged region spans at most two; longer ones may look up more)
+            const uint32_t nblk = ovf_nblk(U.len), b0 = (left - 1u) >> kOvfBlkShift;
+            const bool has_ovf = U.ovf != 0;
+            uint32_t ti0 = kNoTile, ti1 = kNoTile;
+            if (has_ovf) {
+                gu32 *tix = (gu32 *)U.ovf_tidx + (size_t)trk * nblk;
+                ti0 = tix[b0];
+                ti1 = tix[b0 + 1u < nblk ? b0 + 1u : b0];
+            }
+            auto moments = [&](uint32_t m, int64_t c0) {
+                uint32_t em = 0;  // dwords holding an escaped field
+                while (m) {
+                    const int k = __builtin_ctz(m);
+                    m &= m - 1u;
+                    const uint32_t d = row[k];
+                    const uint32_t off = (uint32_t)(16 * (c0 + k) - kPadPos + 1) - left;  // field 0's offset
+                    const uint32_t s = __builtin_popcount(d & kLo) + 2u * __builtin_popcount(d & ~kLo);
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        w += (__builtin_popcount(d & kFb[q]) + 2u * __builtin_popcount(d & (kFb[q] << 1))) << q;
+                    count += s;
+                    psum += s * off + w;
+                    nh += __builtin_popcount((d | (d >> 1)) & kLo);
+                    em |= ((d & (d >> 1) & kLo) != 0u ? 1u : 0u) << k;
+                }
+                // escaped fields, in position order: a dword's 16 tile bytes
+                // (counts up to 254) come as one 16-byte load, four dwords'
+                // loads in flight together (one dependent lookup per escape
+                // was most of this kernel's time: ~100 tags per region at 2
+                // bits leave several escapes in each)
+                while (em) {
+                    int ks[4];
+                    bool ok[4];
+                    gu8 *src[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        ok[i] = em != 0u;
+                        ks[i] = ok[i] ? __builtin_ctz(em) : ks[0];
+                        em &= em - 1u;
+                        const uint32_t p1 = (uint32_t)(16 * (c0 + ks[i]) - kPadPos);  // field 0's position - 1
+                        const uint32_t blk = p1 >> kOvfBlkShift;
+                        const uint32_t ti = blk == b0 ? ti0 : blk == b0 + 1u ? ti1 : kNoTile;
+                        src[i] = ti != kNoTile ? (gu8 *)U.ovf_tiles + (size_t)ti * kOvfBlk + (p1 & (kOvfBlk - 1u))
+                                               : (gu8 *)P.kern;  // (a safe address; not read)
+                    }
+                    u32x4 tv[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) tv[i] = *(gu32x4 *)src[i];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        if (!ok[i]) continue;
+                        const uint32_t d = row[ks[i]];
+                        const uint32_t off = (uint32_t)(16 * (c0 + ks[i]) - kPadPos + 1) - left;
+                        const bool direct = src[i] != (gu8 *)P.kern;
+                        for (uint32_t e = d & (d >> 1) & kLo; e; e &= e - 1u) {
+                            const uint32_t f = (uint32_t)__builtin_ctz(e) >> 1;
+                            const uint32_t q = f >> 2;
+                            const uint32_t word = q == 0 ? tv[i].x : q == 1 ? tv[i].y : q == 2 ? tv[i].z : tv[i].w;
+                            uint32_t c = (word >> (8 * (f & 3u))) & 255u;
+                            if (!has_ovf) {
+                                c = kEsc;
+                            } else if (!direct || c == 255u) {
+                                c = ovf_lookup(U, trk, off + f + left);
+                            }
+                            if (ne < (uint32_t)kK3LEsc) ecache[ne] = (uint8_t)(c < 255u ? c : 255u);
+                            ++ne;
+                            count += c - kEsc;
+                            psum += (c - kEsc) * (off + f);
+                        }
+                    }
+                }
+            };
+            if (staged) {
+                moments(nzm, j0);
+            } else {
+                for (int64_t c0 = j0; c0 <= j1; c0 += kK3LRow) moments(stage(c0, j1, n0, n1), c0);
+            }
+        } else if (live) {
             walk(false, [&](uint32_t pos, uint32_t c) {
                 count += c;
                 psum += c * (uint32_t)(uint16_t)(pos - left);  // Q8: uint16 offsets
             });
+            nh = ~0u;
+        }
         const double x_bar = (double)psum / (double)count;
+        if (P.cut == 6 && count == 12345u) P.out_counts[0] = (uint32_t)x_bar;  // (+ the first walk)
+        if (P.cut == 6) continue;
         double sum2 = 0.0, sum4 = 0.0;
-        if (live)
-            walk(true, [&](uint32_t pos, uint32_t c) {
-                const double d = (double)(uint16_t)(pos - left) - x_bar;
-                const double d2 = d * d;
-                sum2 = sum2 + (double)c * d2;
-                sum4 = sum4 + (double)c * (d2 * d2);
-            });
+        const bool heavy = live && nh > (uint32_t)P.heavy;
+        if (live && !heavy) {
+            // per nonzero dword, all 16 fields at once: an empty field's
+            // terms are +0.0, which leaves the (non-negative) sums unchanged
+            // exactly, so the adds stay the hits' adds in position order
+            // while the terms' FP64 work is independent across fields (a
+            // loop over hits ran one dependent chain per hit)
+            uint32_t ne = 0;
+            auto terms = [&](uint32_t m, int64_t c0) {
+                while (m) {
+                    const int k = __builtin_ctz(m);
+                    m &= m - 1u;
+                    const uint32_t d = row[k];
+                    const uint32_t off = (uint32_t)(16 * (c0 + k) - kPadPos + 1) - left;  // field 0's offset
+                    double t2[16], t4[16];
+#pragma unroll
+                    for (int f = 0; f < 16; ++f) {
+                        uint32_t c = (d >> (2 * f)) & 3u;
+                        if (c == kEsc) {
+                            c = ne < (uint32_t)kK3LEsc && ecache[ne] != 255u ? ecache[ne]
+                                                                             : ovf_lookup(U, trk, off + (uint32_t)f + left);
+                            ++ne;
+                        }
+                        const double dd = (double)(uint16_t)(off + (uint32_t)f) - x_bar;
+                        const double d2 = dd * dd;
+                        t2[f] = c != 0u ? (double)c * d2 : 0.0;
+                        t4[f] = c != 0u ? (double)c * (d2 * d2) : 0.0;
+                    }
+#pragma unroll
+                    for (int f = 0; f < 16; ++f) {
+                        sum2 = sum2 + t2[f];
+                        sum4 = sum4 + t4[f];
+                    }
+                }
+            };
+            if (staged) {
+                terms(nzm, j0);
+            } else {
+                for (int64_t c0 = j0; c0 <= j1; c0 += kK3LRow) terms(stage(c0, j1, n0, n1), c0);
+            }
+        }
+        // Regions with many hits would hold the whole wave in their lane's
+        // walk: the wave sums their terms instead, one region at a time, 64
+        // positions per step -- each step's terms formed by the lanes,
+        // compacted in LDS, then added in position order (the same FP64
+        // operations in the same order as the lane's walk).  Their dwords
+        // come from the lane's staged row, or 64 at a time from HBM.
+        uint64_t hv = __ballot(heavy);
+        if (hv) {
+            double *tx = (double *)rstage, *ty = tx + 64;  // (rstage is free until the records)
+            const uint32_t *rows0 = row - threadIdx.x * kK3LRowStride;
+            while (hv) {
+                const int l = __builtin_ctzll(hv);
+                hv &= hv - 1;
+                const uint32_t hl = rl_u(left, l), hr = rl_u(right, l), hu = rl_u(u, l);
+                const double hx = __shfl(x_bar, l);
+                const UnitDesc Uh = P.units[hu];
+                gu32 *htw = (gu32 *)((gu8 *)Uh.base + (uint64_t)nc0 * Uh.stride);
+                const int64_t hn0 = kPadPos + (int64_t)hl - 1, hn1 = kPadPos + (int64_t)hr - 1;
+                const int64_t hj0 = hn0 >> 4, hj1 = hn1 >> 4;
+                const bool hst = hj1 - hj0 + 1 <= kK3LRow;  // staged in lane l's row before the walks
+                const uint32_t *hrow = rows0 + ((threadIdx.x & ~63u) + (uint32_t)l) * kK3LRowStride;
+                double a = 0.0, b = 0.0;
+                for (int64_t cb = hj0; cb <= hj1; cb += 64) {
+                    uint32_t dv = 0u;
+                    if (cb + lane <= hj1) dv = hst ? hrow[lane] : htw[cb + lane];
+                    for (int w = 0; w < 16; ++w) {
+                        const int64_t g = 16 * cb + 64 * w + lane;  // the lane's field
+                        if (16 * cb + 64 * w > hn1) break;
+                        const uint32_t d = (uint32_t)__shfl((int)dv, 4 * w + (lane >> 4));
+                        uint32_t c = g >= hn0 && g <= hn1 ? (d >> (2 * (lane & 15))) & kTMask : 0u;
+                        const int64_t pos = g - kPadPos + 1;
+                        if (c == kEsc) c = ovf_lookup(Uh, trk, (uint32_t)pos);
+                        const double dd = (double)(uint16_t)(pos - (int64_t)hl) - hx;
+                        const double d2 = dd * dd;
+                        const uint64_t m = __ballot(c != 0u);
+                        if (c != 0u) {
+                            const uint32_t k =
+                                __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            tx[k] = (double)c * d2;
+                            ty[k] = (double)c * (d2 * d2);
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        const int n = __builtin_popcountll(m);
+                        for (int k = 0; k < n; ++k) {
+                            a = a + tx[k];
+                            b = b + ty[k];
+                        }
+                        __builtin_amdgcn_wave_barrier();  // the terms are reused
+                    }
+                }
+                if (lane == l) {
+                    sum2 = a;
+                    sum4 = b;
+                }
+            }
+        }
         const double kurt = ((double)count - 1) * sum4 / (sum2 * sum2);
         if (P.cut == 3 && count == 12345u) P.out_counts[0] = (uint32_t)kurt;  // (+ both walks; keep them live)
         if (P.cut == 3) continue;
