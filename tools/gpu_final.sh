@@ -42,8 +42,9 @@ bench)
 prof)
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$F/trace" -o p -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline > "$F/trace.log" 2>&1 || { tail "$F/trace.log"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$F/fetch" -o p -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$F/fetch.log" 2>&1 || exit 1
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$F/write" -o p -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$F/write.log" 2>&1 || exit 1
+  UNIPEAK_BENCH_LEGS=cold UNIPEAK_BENCH_SINGLE=0 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$F/fetch" -o p -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$F/fetch.log" 2>&1 || exit 1
+  UNIPEAK_BENCH_LEGS=cold UNIPEAK_BENCH_SINGLE=0 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$F/write" -o p -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$F/write.log" 2>&1 || exit 1
+  python3 "$R/tools/pmc_traffic.py" "$F/fetch" "$F/write" k1a_fields_kernel 1547846991 "$F/k1a_pmc_traffic.json" || exit 1
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d "$F/pmc_a" -o p -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$F/pmc_a.log" 2>&1 || exit 1
   timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR --output-format csv -d "$F/pmc_b" -o p -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$F/pmc_b.log" 2>&1 || exit 1
   echo prof-ok
@@ -56,8 +57,10 @@ sim)
     done
     python -c "
 import json
-v=[json.load(open('$F/sim8_${w}_r%d.json' % r))['ms_per_step'] for r in range(8)]
-print('$w sim8', [round(x, 4) for x in v], 'max', max(v))"
+d=[json.load(open('$F/sim8_${w}_r%d.json' % r)) for r in range(8)]
+v=[x['ms_per_step'] for x in d]
+wv=[x.get('legs_ms_per_step', {}).get('warm', float('nan')) for x in d]
+print('$w sim8 cold', [round(x, 4) for x in v], 'max', max(v), '| warm max', max(wv))"
   done
   NS=8 WS="hg19-dir1 hg19-8s1c" bash tools/rehearse.sh > "$F/rehearse.jsonl" 2>&1 || { tail -5 "$F/rehearse.jsonl"; exit 1; }
   cat "$F/rehearse.jsonl"
