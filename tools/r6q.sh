@@ -1,5 +1,5 @@
 #!/bin/bash
-# K3L second walk per dword (16 fields at once): parity (forced on, heavy path forced too), cuts, A/B
+# K3L peak window per dword: parity (forced on, heavy path forced too), cuts, A/B
 set -o pipefail
 T=${1:-r6q}
 R=$GRAFT_REPO_ROOT
@@ -8,7 +8,7 @@ UNIPEAK_K3_LANE=2 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --ti
 tail -1 gpurun_out/$T/pytest.log
 UNIPEAK_K3_LANE=2 UNIPEAK_K3L_HEAVY=4 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_unit.py tests/test_gpu_k3.py > gpurun_out/$T/pytest_heavy.log 2>&1 || { tail -40 gpurun_out/$T/pytest_heavy.log; exit 1; }
 tail -1 gpurun_out/$T/pytest_heavy.log
-for cut in 6 3 4 0; do
+for cut in 3 4 0; do
   UNIPEAK_K3_LANE=2 UNIPEAK_K3L_CUT=$cut UNIPEAK_BENCH_LEGS=cold UNIPEAK_BENCH_SINGLE=0 timeout -k 10 200 python $R/bench.py --steps 10 --no-cpu-baseline > gpurun_out/$T/cut_$cut.json 2> gpurun_out/$T/cut_$cut.err || exit 1
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('cut', sys.argv[2], d['roofline']['isolated_ms']['k3'])" gpurun_out/$T/cut_$cut.json $cut
 done

@@ -518,6 +518,17 @@ __global__ void __launch_bounds__(kK3LThreads) stats1L_kernel(StatParams P) {
             }
         };
         if (P.cut == 2) continue;  // (+ staging)
+        constexpr uint32_t kLo = 0x55555555u;
+        // the escape tiles of the region's first two overflow blocks (a
+        // staged region spans at most two; longer ones may look up more)
+        const uint32_t nblk = ovf_nblk(U.len), b0 = (left - 1u) >> kOvfBlkShift;
+        const bool has_ovf = U.ovf != 0;
+        uint32_t ti0 = kNoTile, ti1 = kNoTile;
+        if (live && has_ovf) {
+            gu32 *tix = (gu32 *)U.ovf_tidx + (size_t)trk * nblk;
+            ti0 = tix[b0];
+            ti1 = tix[b0 + 1u < nblk ? b0 + 1u : b0];
+        }
         uint32_t count = 0, psum = 0, nh = 0;  // nh: hits (the second walk's iterations)
         if (live && right - left < 65536u) {
             // no offset wraps (Q8): each dword's count and position moment
@@ -526,19 +537,8 @@ __global__ void __launch_bounds__(kK3LThreads) stats1L_kernel(StatParams P) {
             // pass costs dwords, not hits (uint32 arithmetic: exact mod 2^32
             // like the reference's).  Escaped fields hold 3: the true count
             // replaces it, and is cached for the second walk.
-            constexpr uint32_t kLo = 0x55555555u;
             constexpr uint32_t kFb[4] = {0x44444444u, 0x50505050u, 0x55005500u, 0x55550000u};
             uint32_t ne = 0;
-            // the escape tiles of the region's first two overflow blocks (a
-            // staged region spans at most two; longer ones may look up more)
-            const uint32_t nblk = ovf_nblk(U.len), b0 = (left - 1u) >> kOvfBlkShift;
-            const bool has_ovf = U.ovf != 0;
-            uint32_t ti0 = kNoTile, ti1 = kNoTile;
-            if (has_ovf) {
-                gu32 *tix = (gu32 *)U.ovf_tidx + (size_t)trk * nblk;
-                ti0 = tix[b0];
-                ti1 = tix[b0 + 1u < nblk ? b0 + 1u : b0];
-            }
             auto moments = [&](uint32_t m, int64_t c0) {
                 uint32_t em = 0;  // dwords holding an escaped field
                 while (m) {
@@ -729,25 +729,45 @@ __global__ void __launch_bounds__(kK3LThreads) stats1L_kernel(StatParams P) {
             const int64_t p0 = (int64_t)kpos - bw, p1 = (int64_t)kpos + bw;
             const int64_t a0 = kPadPos + p0 - 1, a1 = kPadPos + p1 - 1;
             double f = 0.0;
-            // the window's dwords staged like the region's (the row is free now)
+            // the window's dwords staged like the region's (the row is free
+            // now), then per nonzero dword all 16 fields' terms at once (an
+            // empty field's is +0.0, exact on the non-negative sum) and
+            // their adds in position order; a dword's escaped counts come
+            // from one 16-byte escape-tile load
             const int64_t q0 = a0 >> 4, q1 = a1 >> 4;
             for (int64_t c0 = q0; c0 <= q1; c0 += kK3LRow) {
                 uint32_t m = stage(c0, q1, a0, a1);
-                uint32_t d = 0;
-                int k = 0;
-                for (;;) {
-                    if (d == 0u) {
-                        if (m == 0u) break;
-                        k = __builtin_ctz(m);
-                        m &= m - 1u;
-                        d = row[k];
+                while (m) {
+                    const int k = __builtin_ctz(m);
+                    m &= m - 1u;
+                    const uint32_t d = row[k];
+                    const int64_t g0 = 16 * (c0 + k);  // field 0
+                    u32x4 tv = {0u, 0u, 0u, 0u};
+                    bool direct = false;
+                    if ((d & (d >> 1) & kLo) != 0u && has_ovf) {
+                        const uint32_t p1f = (uint32_t)(g0 - kPadPos);  // field 0's position - 1 (escapes lie in the contig)
+                        const uint32_t blk = p1f >> kOvfBlkShift;
+                        const uint32_t ti = blk == b0 ? ti0 : blk == b0 + 1u ? ti1 : kNoTile;
+                        if (ti != kNoTile) {
+                            tv = *(gu32x4 *)((gu8 *)U.ovf_tiles + (size_t)ti * kOvfBlk + (p1f & (kOvfBlk - 1u)));
+                            direct = true;
+                        }
                     }
-                    const int b = __builtin_ctz(d) & ~1;
-                    uint32_t c = (d >> b) & 3u;
-                    d &= ~(3u << b);
-                    const int64_t pos = 16 * (c0 + k) + b / 2 - kPadPos + 1;
-                    if (c == kEsc) c = ovf_lookup(U, trk, (uint32_t)pos);
-                    f = f + ktab[2 * bw - (int)(pos - p0)] * (double)c;
+                    double t[16];
+#pragma unroll
+                    for (int fi = 0; fi < 16; ++fi) {
+                        uint32_t c = (d >> (2 * fi)) & 3u;
+                        const int64_t g = g0 + fi;
+                        if (c == kEsc) {
+                            const uint32_t q = (uint32_t)fi >> 2;
+                            const uint32_t w = q == 0 ? tv.x : q == 1 ? tv.y : q == 2 ? tv.z : tv.w;
+                            const uint32_t v = (w >> (8 * (fi & 3))) & 255u;
+                            c = !has_ovf ? kEsc : (direct && v != 255u) ? v : ovf_lookup(U, trk, (uint32_t)(g - kPadPos + 1));
+                        }
+                        t[fi] = c != 0u ? ktab[2 * bw - (int)(g - a0)] * (double)c : 0.0;
+                    }
+#pragma unroll
+                    for (int fi = 0; fi < 16; ++fi) f = f + t[fi];
                 }
             }
             best = f;
