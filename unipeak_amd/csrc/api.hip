@@ -1519,6 +1519,11 @@ static StatParams stat_params(up_ctx *c, up_ctx::Pass &ps) {
         return e && *e ? atoi(e) : kK3LHeavy;
     }();
     P.heavy = k3l_heavy;
+    static const int k3l_w2 = [] {
+        const char *e = getenv("UNIPEAK_K3L_W2");
+        return e && *e ? atoi(e) : 1;
+    }();
+    P.w2hits = k3l_w2;
     return P;
 }
 

@@ -205,6 +205,7 @@ struct StatParams {
     int32_t planes;       // the chunk-sum planes are current (range sums may read them)
     int32_t cut;          // measurement aid (UNIPEAK_K3L_CUT): K3L stops after phase `cut` (wrong records)
     int32_t heavy;        // K3L: regions with more hits take the wave's kurtosis path (UNIPEAK_K3L_HEAVY)
+    int32_t w2hits;       // K3L second walk: 1 = four hits per step, 0 = 16 fields per dword (UNIPEAK_K3L_W2)
 };
 
 }  // namespace upk

@@ -654,7 +654,63 @@ __global__ void __launch_bounds__(kK3LThreads) stats1L_kernel(StatParams P) {
                     }
                 }
             };
-            if (staged) {
+            // or four hits per step: the four found one after another (integer
+            // work), their terms formed independently, then added in order --
+            // a dword holds ~5 hits, so this forms ~8 terms where the dword
+            // form forms 16
+            auto hits4 = [&](uint32_t m, int64_t c0) {
+                uint32_t d = 0;
+                int64_t j = 0;
+                for (;;) {
+                    uint32_t cv[4], ov[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        if (d == 0u && m != 0u) {
+                            const int k = __builtin_ctz(m);
+                            m &= m - 1u;
+                            d = row[k];
+                            j = c0 + k;
+                        }
+                        cv[i] = 0u;
+                        ov[i] = 0u;
+                        if (d != 0u) {
+                            const int b = __builtin_ctz(d) & ~1;
+                            cv[i] = (d >> b) & 3u;
+                            d &= ~(3u << b);
+                            ov[i] = (uint32_t)(16 * j + b / 2 - kPadPos + 1) - left;  // pos - left
+                        }
+                    }
+                    if (cv[0] == 0u) break;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        if (cv[i] == kEsc) {
+                            cv[i] = ne < (uint32_t)kK3LEsc && ecache[ne] != 255u ? ecache[ne]
+                                                                                 : ovf_lookup(U, trk, ov[i] + left);
+                            ++ne;
+                        }
+                    }
+                    double t2[4], t4[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const double dd = (double)(uint16_t)ov[i] - x_bar;
+                        const double d2 = dd * dd;
+                        t2[i] = cv[i] != 0u ? (double)cv[i] * d2 : 0.0;
+                        t4[i] = cv[i] != 0u ? (double)cv[i] * (d2 * d2) : 0.0;
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        sum2 = sum2 + t2[i];
+                        sum4 = sum4 + t4[i];
+                    }
+                }
+            };
+            if (P.w2hits) {
+                if (staged) {
+                    hits4(nzm, j0);
+                } else {
+                    for (int64_t c0 = j0; c0 <= j1; c0 += kK3LRow) hits4(stage(c0, j1, n0, n1), c0);
+                }
+            } else if (staged) {
                 terms(nzm, j0);
             } else {
                 for (int64_t c0 = j0; c0 <= j1; c0 += kK3LRow) terms(stage(c0, j1, n0, n1), c0);
