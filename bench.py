@@ -634,7 +634,9 @@ def main():
                          "traffic": traffic,
                          "traffic_unit": "GB per launch (rocprofv3 PMC FETCH_SIZE+WRITE_SIZE, gfx950-corrected)",
                          "traffic_source": traffic_src,
-                         "kernel": ("scan_kernel<..., kModeScreenF> (K1a: stream of the 2-bit fields + screen)"
+                         "kernel": (("k1a_fields_kernel" if (S - n_ctl == 1 and not nondir and args.bw <= 255)
+                                     else "scan_kernel<..., kModeScreenF>") +
+                                    " (K1a: stream of the 2-bit fields + screen)"
                                     if legs[0] == "cold" else
                                     "scan_kernel<..., kModeScreen> (K1a: stream + integer screen)"),
                          "kernel_ms": round(k1a_ms, 4), "kernel_ms_max_rank": round(k1a_max, 4),
