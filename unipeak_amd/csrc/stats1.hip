@@ -358,18 +358,25 @@ namespace upk {
 
 // ------------------------------------------------------------------------
 // K3L: the same statistics with ONE LANE PER REGION (round 6).  A region of
-// configs[1] holds ~245 positions and ~20 hits: stats1_kernel's wave spent
-// ~15 us per region in dependent loads and wave-wide bookkeeping for a
-// handful of terms, 8 regions in turn per wave, on every pass's chain
-// stream.  Here each lane walks its own region's 2-bit dwords (fields in
-// ascending position: ctz over the nonzero fields), so pass 1 (exptSums,
-// count, position moments with the Q8 uint16 offsets), pass 2 (the two
-// kurtosis sums in position order, data.cpp:164-182, powi semantics) and the
-// peak score (the reference's ordered sum over the peak's window,
-// peakcall.cpp:203-209) are plain sequential loops with the same FP64
-// operations in the same order as stats1_kernel's.  Regions whose Q-key peak
-// is tied (+0.5) get the wave's KDE afterwards, one at a time.  Records are
-// staged in LDS and written as contiguous wave stores.
+// configs[1] holds ~245 positions and ~107 tags: stats1_kernel's wave spent
+// ~15 us per region in dependent loads and wave-wide bookkeeping, 8 regions
+// in turn per wave, on every pass's chain stream.  Here each lane stages its
+// own region's 2-bit dwords in an LDS row (all loads in flight) and:
+//  * pass 1 (exptSums, count, position moments with the Q8 uint16 offsets)
+//    per dword from popcounts, escaped fields resolved four dwords at a time
+//    from 16-byte escape-tile loads and cached for pass 2;
+//  * pass 2 (the two kurtosis sums in position order, data.cpp:164-182,
+//    powi semantics) four hits per step: terms formed independently, added
+//    in order;
+//  * the peak score (the reference's ordered sum over the peak's window,
+//    peakcall.cpp:203-209) per staged dword, 16 terms at once (an empty
+//    field adds +0.0, exact on the non-negative sum);
+// so every FP64 sum has the same operations in the same order as
+// stats1_kernel's.  Regions whose Q-key peak is tied (+0.5) get the wave's
+// KDE afterwards, one at a time, as do regions above P.heavy hits for pass 2.
+// Records are staged in LDS and written as contiguous wave stores.
+// Measurements and the variants tried: DESIGN.md §4 "Round 6",
+// profiles/r06/ab_k3_walks.txt.
 constexpr int kK3LRecWords = 7;  // 56-byte up_region as uint64 words
 constexpr int kK3LRow = 32;      // region dwords staged per lane at a time (512 positions)
 constexpr int kK3LEsc = 64;      // escaped counts cached per lane (bytes)
