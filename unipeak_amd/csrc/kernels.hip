@@ -3077,7 +3077,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (int l = 0; l < nvalid; ++l) {
+                int l = 0;
+                for (; l + kTermBatch <= nvalid; l += kTermBatch) {  // a batch of reads in flight
+                    double2 v[kTermBatch];
+#pragma unroll
+                    for (int i = 0; i < kTermBatch; ++i) v[i] = terms[l + i];
+#pragma unroll
+                    for (int i = 0; i < kTermBatch; ++i) {
+                        sf = sf + v[i].x;
+                        sr = sr + v[i].y;
+                    }
+                }
+                for (; l < nvalid; ++l) {
                     const double2 v = terms[l];
                     sf = sf + v.x;
                     sr = sr + v.y;
@@ -3284,7 +3295,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPK_K3
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (int l = 0; l < nvalid; ++l) {  // sequential sums, broadcast reads
+                int l = 0;
+                for (; l + kTermBatch <= nvalid; l += kTermBatch) {  // sequential sums, broadcast reads in flight
+                    double v[3 * kTermBatch];
+#pragma unroll
+                    for (int i = 0; i < 3 * kTermBatch; ++i) v[i] = prod[3 * l + i];
+#pragma unroll
+                    for (int i = 0; i < kTermBatch; ++i) {
+                        ss1 = ss1 + v[3 * i];
+                        ss2 = ss2 + v[3 * i + 1];
+                        ssr = ssr + v[3 * i + 2];
+                    }
+                }
+                for (; l < nvalid; ++l) {
                     ss1 = ss1 + prod[3 * l];
                     ss2 = ss2 + prod[3 * l + 1];
                     ssr = ssr + prod[3 * l + 2];
