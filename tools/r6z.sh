@@ -1,7 +1,7 @@
 #!/bin/bash
 # closing check on the final build: every GPU test, smoke, the default bench line, its kernel stats
 set -o pipefail
-R=$GRAFT_REPO_ROOT; F=$R/gpurun_out/r6z; mkdir -p $F; cd $R || exit 1
+R=$GRAFT_REPO_ROOT; F=$R/gpurun_out/${1:-r6z}; mkdir -p $F; cd $R || exit 1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $F/pytest.log 2>&1 || { grep -E "FAILED|Error" $F/pytest.log | head; tail -3 $F/pytest.log; exit 1; }
 tail -1 $F/pytest.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $F/smoke.log 2>&1 || { cat $F/smoke.log; exit 1; }
